@@ -1,0 +1,275 @@
+"""Benchmark: device-resident masked reduce_chunk over a dummy_data-style
+variable in 64^3 float32 chunks (BASELINE.json metric; configs[2] = C3).
+
+One *step* = one pass of the hot path over one batch: every chunk of the
+rank's variable is un-shuffled (if filtered), selected, masked (_FillValue,
+valid_min, valid_max) and reduced to sum/count/min/max in one fused kernel,
+the per-chunk partials are combined on the device, and for N > 1 the 32-byte
+per-GPU partials are exchanged with one RCCL all-gather and combined in rank
+order.  Those statistics give mean, max and min (C3's three methods).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GB/s + chunks/s device-resident masked reduce_chunk, f32 64³ chunks, 1–8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
+
+CONFIGS = {
+    # name: (shape per rank, chunks, dtype, shuffle, masked, selection)
+    "c2": dict(shape=(1024, 1024, 1024), chunks=(64, 64, 64), dtype="f4", shuffle=False,
+               masked=False, hyperslab=None, desc="1024^3 f32, 64^3 chunks, no mask, sum"),
+    "c3": dict(shape=(1024, 1024, 1024), chunks=(64, 64, 64), dtype="f4", shuffle=False,
+               masked=True, hyperslab=None,
+               desc="1024^3 f32, 64^3 chunks, _FillValue + valid_min/valid_max, mean/max/min"),
+    "c4": dict(shape=(2048, 2048, 2048), chunks=(128, 128, 128), dtype="f4", shuffle=True,
+               masked=True, hyperslab=None, desc="2048^3 f32, 128^3 chunks, shuffle + mask, sum"),
+    "c5": dict(shape=(4096, 2048, 1024), chunks=(32, 32, 32), dtype="f8", shuffle=False,
+               masked=True, hyperslab=((16, 4080), (16, 2032), (16, 1008)),
+               desc="4096x2048x1024 f64, 32^3 chunks, hyperslab, masked mean"),
+}
+FILL = -999.0
+VMIN = 1000.0
+VMAX = 5e8
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--tile-bytes", type=int, default=0)
+    p.add_argument("--cpu-chunks", type=int, default=1024,
+                   help="chunks in the CPU-baseline sample (0 = skip)")
+    p.add_argument("--cpu-threads", type=int, default=30)
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return p.parse_args()
+
+
+def chunk_selections(cfg, rank_origin):
+    """Per-chunk hyperslab selections for c5 (None = all chunks full)."""
+    hs = cfg["hyperslab"]
+    if hs is None:
+        return None
+    from pyactivestorage_amd import selection
+    shape, chunks = cfg["shape"], cfg["chunks"]
+    grid = [-(-s // c) for s, c in zip(shape, chunks)]
+    sels = []
+    for ci in np.ndindex(*grid):
+        dims = []
+        for d, c in enumerate(ci):
+            lo = max(hs[d][0] - c * chunks[d], 0)
+            hi = min(hs[d][1] - c * chunks[d], chunks[d])
+            cnt = max(hi - lo, 0)
+            dims.append(selection.DimSel(lo if cnt else 0, 1, cnt, False))
+        sels.append(selection.ChunkSel(dims, tuple(d.count for d in dims), (0, 1, 2)))
+    return sels
+
+
+def cpu_baseline(cfg, host_chunks: np.ndarray, n_chunks: int, missing, threads: int):
+    """Time the oracle (NumPy restatement of storage.reduce_chunk + the
+    Active combine) on a page-cache-hot chunk-major file, fanned out over a
+    ThreadPoolExecutor like active.py:557-572."""
+    import concurrent.futures
+
+    from oracle import storage_ref as ref
+    dt = np.dtype(cfg["dtype"])
+    chunk_bytes = int(np.prod(cfg["chunks"])) * dt.itemsize
+    with tempfile.NamedTemporaryFile(dir="/tmp", suffix=".chunks", delete=False) as f:
+        f.write(host_chunks.tobytes())
+        path = f.name
+    filters = [ref.Shuffle(dt.itemsize)] if cfg["shuffle"] else None
+    sel = tuple(slice(0, c, 1) for c in cfg["chunks"])
+    axis = (0, 1, 2)
+    try:
+        with open(path, "rb") as fh:  # warm the page cache
+            while fh.read(1 << 26):
+                pass
+        t0 = time.perf_counter()
+        with concurrent.futures.ThreadPoolExecutor(max_workers=threads) as ex:
+            futs = [ex.submit(ref.reduce_chunk, path, c * chunk_bytes, chunk_bytes, None, filters,
+                              missing, dt, cfg["chunks"], "C", sel, axis, np.ma.sum)
+                    for c in range(n_chunks)]
+            parts = []
+            for c, fu in enumerate(futs):
+                tmp, cnt = fu.result()
+                parts.append((tmp, cnt, (slice(c, c + 1), slice(0, 1), slice(0, 1))))
+        out = ref.combine_partials(parts, (n_chunks, 1, 1), dt, axis, "mean", components=True)
+        dt_s = time.perf_counter() - t0
+    finally:
+        os.unlink(path)
+    return dt_s, out
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from pyactivestorage_amd import _lib, engine
+    from pyactivestorage_amd.batch import ReductionPlan
+    from pyactivestorage_amd.device import get_context
+    from pyactivestorage_amd.synthetic import chunk_major_device
+
+    cfg = CONFIGS[args.config]
+    dt = np.dtype(cfg["dtype"])
+    ctx = get_context(local)
+    if args.tile_bytes:
+        ctx.set_tile_bytes(args.tile_bytes)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    # weak scaling: each rank owns its own slab of the variable (dim 0)
+    origin = (rank * cfg["shape"][0], 0, 0)
+    data, offsets, n_fill = chunk_major_device(
+        torch, cfg["shape"], cfg["chunks"], dt, dev, origin=origin,
+        n_formula=cfg["shape"][0] * world,
+        fill=FILL if cfg["masked"] else None, fill_frac=0.01 if cfg["masked"] else 0.0,
+        seed=rank, shuffle=cfg["shuffle"])
+    torch.cuda.synchronize()
+    missing = ((dt.type(FILL), None, dt.type(VMIN), dt.type(VMAX)) if cfg["masked"]
+               else (None, None, None, None))
+    sels = chunk_selections(cfg, origin)
+    plan = ReductionPlan(ctx, dt, cfg["chunks"], data.data_ptr(), offsets,
+                         shuffle=dt.itemsize if cfg["shuffle"] else 0, selections=sels,
+                         missing=missing, round_to_var=True, stream=stream)
+    n_chunks = plan.n_chunks
+    sel_elems = (n_chunks * int(np.prod(cfg["chunks"])) if sels is None
+                 else sum(s.n_selected for s in sels))
+    bytes_per_launch = sel_elems * dt.itemsize
+
+    gathered = torch.zeros(world * _lib.PARTIAL_NBYTES, dtype=torch.uint8, device=dev)
+    final = torch.zeros(_lib.PARTIAL_NBYTES, dtype=torch.uint8, device=dev)
+    # zero-copy torch view of the plan's 32-byte device total, for RCCL
+    total_t = _tensor_from_ptr(torch, plan.total.ptr, _lib.PARTIAL_NBYTES, dev)
+
+    def step():
+        plan.launch(stream, chunk_partials=False)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, total_t)
+            engine.combine_partials(ctx, dt, gathered.data_ptr(), world, final.data_ptr(), False,
+                                    stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.check(ctx.lib.pyas_timing_enable(ctx.handle, args.steps), "timing_enable")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    import ctypes
+    ms = (ctypes.c_float * args.steps)()
+    nrec = ctypes.c_int32(0)
+    _lib.check(ctx.lib.pyas_timing_read(ctx.handle, ms, args.steps, ctypes.byref(nrec)), "timing_read")
+    kern_ms = float(np.mean(np.array(ms[: nrec.value]))) if nrec.value else float("nan")
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms_max = float(t[0]), float(t[1])
+    else:
+        kern_ms_max = kern_ms
+
+    # result check against an independent torch computation on the device
+    tot = plan.read_total(stream)[0]
+    result = {"sum": float(tot["sum"]), "count": int(tot["count"]), "min": float(tot["min"]),
+              "max": float(tot["max"])}
+    if world > 1:
+        fin = np.frombuffer(final.cpu().numpy().tobytes(), dtype=engine.partial_dtype(dt))[0]
+        result = {"sum": float(fin["sum"]), "count": int(fin["count"]), "min": float(fin["min"]),
+                  "max": float(fin["max"])}
+
+    ms_per_step = elapsed / args.steps * 1e3
+    total_bytes = bytes_per_launch * world
+    value = total_bytes / (elapsed / args.steps) / 1e9
+    chunks_per_s = n_chunks * world / (elapsed / args.steps)
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(args.traffic_file) as f:
+            tr = json.load(f)
+        if tr.get("config") == args.config:
+            traffic = tr.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_chunks > 0:
+        nc = min(args.cpu_chunks, n_chunks)
+        cb = int(np.prod(cfg["chunks"])) * dt.itemsize
+        host = data[: nc * cb].cpu().numpy()
+        secs, _ = cpu_baseline(cfg, host, nc, missing, args.cpu_threads)
+        ncores = len(os.sched_getaffinity(0))
+        cpu = {"value": round(nc * cb / secs / 1e9, 4), "unit": "GB/s",
+               "cores": min(args.cpu_threads, ncores), "kind": "port",
+               "sample": f"{nc} of {n_chunks} chunks ({nc * cb / 2**20:.0f} MiB) of the same "
+                         f"workload, oracle storage_ref.reduce_chunk per chunk from a page-cache-hot "
+                         f"file on a {args.cpu_threads}-thread pool (active.py:557), "
+                         f"{secs:.2f} s, host has {ncores} usable cores",
+               "chunks_per_s": round(nc / secs, 1)}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64" if dt.itemsize == 8 else "f32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: {cfg['desc']}", "variable_per_gpu": list(cfg["shape"]),
+                       "chunk_shape": list(cfg["chunks"]), "chunks_per_gpu": n_chunks,
+                       "bytes_per_gpu": bytes_per_launch, "parallelism": f"chunk-shard x{world}",
+                       "methods": "sum,count,min,max in one pass (mean = sum/count)"},
+            "chunks_per_s": round(chunks_per_s, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel": "pyas::k_reduce",
+                         "kernel_ms_avg": round(kern_ms, 5), "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
+                         "bytes_per_launch": bytes_per_launch},
+            "cpu_baseline": cpu,
+            "result": result,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _tensor_from_ptr(torch, ptr, nbytes, dev):
+    """Zero-copy torch view of a device allocation made by the C library."""
+    class _Holder:
+        __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                    "version": 3, "strides": None}
+    return torch.as_tensor(_Holder(), device=dev)
+
+
+if __name__ == "__main__":
+    main()

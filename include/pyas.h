@@ -1,0 +1,212 @@
+/*
+ * pyas.h — C ABI of the MI355X (gfx950) chunk-reduction backend.
+ *
+ * Drop-in boundary for PyActiveStorage's local chunk reducer.  Every entry
+ * point below names the reference interface it replaces (paths relative to
+ * the NCAS-CMS/PyActiveStorage repository):
+ *
+ *   reference                                       | replaced by
+ *   ------------------------------------------------+---------------------------
+ *   activestorage/storage.py:8-104  reduce_chunk    | pyas_reduce_chunks (batch,
+ *     (one call per chunk, NumPy)                   |   method != None)
+ *   activestorage/storage.py:95-96  chunk[sel] +    | pyas_select_chunks
+ *     mask_missing  (method=None branch, :102-103)  |
+ *   activestorage/storage.py:98-100 np.ma.count +   | pyas_reduce_axes (partial
+ *     method(axis=..., keepdims=True), axis ⊂ dims  |   axis reductions)
+ *   activestorage/storage.py:107-123 filter_pipeline| fused into the kernels
+ *     + numcodecs.Shuffle.decode (hdf2numcodec:37)  |   (pyas_batch.shuffle) and
+ *                                                   |   pyas_unshuffle
+ *   activestorage/storage.py:126-153 mask_missing   | pyas_mask (thresholds are
+ *                                                   |   pre-compiled on the host)
+ *   activestorage/active.py:557-598 thread-pool     | pyas_reduce_chunks with a
+ *     fan-out + out[...] assembly + method(out)     |   `total` output, and
+ *                                                   |   pyas_combine_partials
+ *
+ * Conventions
+ *   - Plain C types only; every pointer documented as "device" must be a HIP
+ *     device (or managed) pointer on the context's device.  `stream` is a
+ *     hipStream_t passed as void* (NULL = the null stream).
+ *   - Every function returns a pyas_status; on failure pyas_last_error()
+ *     returns a thread-local message.  Launch functions do not synchronise
+ *     and allocate nothing after the first call with a given geometry, so a
+ *     caller may capture them into a hipGraph after one warm call.
+ *   - Results are deterministic: no floating-point atomics anywhere; partials
+ *     are combined in a fixed order.
+ */
+#ifndef PYAS_H
+#define PYAS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PYAS_ABI_VERSION 1
+#define PYAS_MAX_DIMS 8
+
+typedef enum {
+    PYAS_OK = 0,
+    PYAS_EINVAL = 1,      /* bad argument (reference: ValueError)            */
+    PYAS_ENOTSUP = 2,     /* unsupported dtype/filter (NotImplementedError)  */
+    PYAS_EDEVICE = 3,     /* HIP runtime / launch failure                    */
+    PYAS_ENOMEM = 4,      /* device allocation failed                        */
+    PYAS_EINDEX = 5       /* selection out of the chunk (IndexError)         */
+} pyas_status;
+
+/* netCDF-4 numeric types (the 10 the format defines) */
+typedef enum {
+    PYAS_I8 = 0, PYAS_U8 = 1, PYAS_I16 = 2, PYAS_U16 = 3, PYAS_I32 = 4,
+    PYAS_U32 = 5, PYAS_I64 = 6, PYAS_U64 = 7, PYAS_F32 = 8, PYAS_F64 = 9
+} pyas_dtype;
+
+/* One 8-byte value in the data's class: f for floats, i for signed, u for
+ * unsigned integers.  Float data values (f32 too) are carried exactly as f64. */
+typedef union {
+    double f;
+    int64_t i;
+    uint64_t u;
+} pyas_scalar;
+
+/* Partial result of a masked reduction over a set of elements (32 bytes).
+ * sum  : floats accumulate in f64; signed ints in int64, unsigned in uint64,
+ *        both wrapping modulo 2^64 exactly as NumPy's int64/uint64 sums do.
+ * count: unmasked elements (np.ma.count, storage.py:98).
+ * min/max: NaN-propagating like np.ma.min/max; meaningless when count == 0
+ *        (the reference returns `masked` there, storage.py:99-100). */
+typedef struct {
+    pyas_scalar sum;
+    int64_t count;
+    pyas_scalar min;
+    pyas_scalar max;
+} pyas_partial;
+
+/* Compiled form of mask_missing (storage.py:126-153).  All thresholds are
+ * values OF THE DATA TYPE (already converted by the host so that the device
+ * comparison in the data type is exactly NumPy's comparison in the promoted
+ * type).  An element x is masked iff
+ *     (eq_lo[0] <= x <= eq_hi[0]) || (eq_lo[1] <= x <= eq_hi[1])
+ *  || x > gt || x < lt  || (vector tables, below).
+ * Disabled rules use neutral values (empty interval lo > hi; gt = +inf or
+ * type max; lt = -inf or type min) and their bit is clear in `flags`.
+ * Vector _FillValue / missing_value (storage.py:133-143, broadcast equality)
+ * use device tables of intervals indexed by sum_d idx_d * tab_stride[k][d],
+ * idx_d = position inside the chunk's selection along chunk dim d. */
+#define PYAS_MASK_EQ0 1u
+#define PYAS_MASK_EQ1 2u
+#define PYAS_MASK_GT 4u
+#define PYAS_MASK_LT 8u
+#define PYAS_MASK_TAB0 16u
+#define PYAS_MASK_TAB1 32u
+
+typedef struct {
+    uint32_t flags;
+    int32_t tab_len[2];
+    pyas_scalar eq_lo[2];
+    pyas_scalar eq_hi[2];
+    pyas_scalar gt;
+    pyas_scalar lt;
+    const pyas_scalar *tab_lo[2];           /* device, tab_len[k] entries */
+    const pyas_scalar *tab_hi[2];
+    int64_t tab_stride[2][PYAS_MAX_DIMS];
+} pyas_mask;
+
+/* A batch of chunks of ONE variable resident in device memory.
+ * Chunk c occupies bytes [offsets[c], offsets[c] + chunk_nbytes) of `data`
+ * (uncompressed; byte-shuffled when `shuffle` > 1; big-endian when
+ * `byteswap`).  offsets[c] must be a multiple of the element size.
+ * Selection (storage.py:95 chunk[chunk_selection]) per chunk and chunk dim:
+ *   sel[(c*PYAS_MAX_DIMS + d)*3 + {0,1,2}] = {start, step, count}
+ *   step != 0 : indices start + k*step, k < count   (slices; step may be < 0)
+ *   step == 0 : indices index_pool[start + k], k < count (integer lists)
+ * sel == NULL selects every chunk completely. */
+typedef struct {
+    int32_t dtype;                     /* pyas_dtype */
+    int32_t byteswap;                  /* 1: stored non-native (big-endian) */
+    int32_t shuffle;                   /* HDF5 shuffle element size, 0/1 = off */
+    int32_t ndim;                      /* chunk rank, 1..PYAS_MAX_DIMS */
+    int64_t chunk_shape[PYAS_MAX_DIMS];
+    int64_t n_chunks;
+    const void *data;                  /* device */
+    const int64_t *offsets;            /* device [n_chunks] */
+    const int32_t *sel;                /* device [n_chunks*PYAS_MAX_DIMS*3] or NULL */
+    const int32_t *index_pool;         /* device, used by step == 0 dims */
+} pyas_batch;
+
+/* combine flags */
+#define PYAS_COMBINE_ROUND_TO_VAR 1u   /* round each input sum to the variable
+                                          dtype first (Active stores partials in
+                                          an `out` array of the var dtype,
+                                          active.py:512,585) */
+
+typedef struct pyas_ctx pyas_ctx;
+
+/* ---- library / context -------------------------------------------------- */
+int pyas_abi_version(void);
+const char *pyas_last_error(void);
+int pyas_device_count(int *count);
+int pyas_ctx_create(int device, pyas_ctx **out);
+int pyas_ctx_destroy(pyas_ctx *ctx);
+/* Tile size (bytes of selected data per workgroup); 0 restores the default. */
+int pyas_ctx_set_tile_bytes(pyas_ctx *ctx, int64_t tile_bytes);
+
+/* ---- memory helpers (so a non-torch host can drive the ABI) ------------- */
+int pyas_malloc(pyas_ctx *ctx, size_t nbytes, void **dptr);
+int pyas_free(pyas_ctx *ctx, void *dptr);
+int pyas_memcpy_h2d(pyas_ctx *ctx, void *dst, const void *src, size_t n, void *stream);
+int pyas_memcpy_d2h(pyas_ctx *ctx, void *dst, const void *src, size_t n, void *stream);
+int pyas_stream_create(pyas_ctx *ctx, void **stream);
+int pyas_stream_destroy(pyas_ctx *ctx, void *stream);
+int pyas_stream_synchronize(pyas_ctx *ctx, void *stream);
+
+/* ---- hot path ------------------------------------------------------------ */
+/* Fused un-shuffle -> byte-swap -> select -> mask -> sum/count/min/max for
+ * every chunk of the batch.  chunk_out (device, n_chunks entries, may be
+ * NULL) receives one partial per chunk (storage.py:98-100 with axis = all
+ * dims); total (device, 1 entry, may be NULL) receives the combine of all
+ * chunk partials under `combine_flags` (active.py:594-598). */
+int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch,
+                       const pyas_mask *mask, pyas_partial *chunk_out,
+                       pyas_partial *total, uint32_t combine_flags,
+                       void *stream);
+
+/* Partial-axis reduction: for chunk c the selected block is reduced over the
+ * chunk dims whose bit is set in axes_mask; outputs (row-major over the
+ * remaining selected dims, keepdims) start at out[out_offsets[c]]. */
+int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch,
+                     const pyas_mask *mask, uint32_t axes_mask,
+                     const int64_t *out_offsets, pyas_partial *out,
+                     void *stream);
+
+/* method=None: decode + select + mask into dense row-major outputs.
+ * values (device) receives native-endian elements, mask_out (device, may be
+ * NULL) one byte per element (1 = masked); chunk c starts at element
+ * out_offsets[c]. */
+int pyas_select_chunks(pyas_ctx *ctx, const pyas_batch *batch,
+                       const pyas_mask *mask, const int64_t *out_offsets,
+                       void *values, uint8_t *mask_out, void *stream);
+
+/* Fixed-order combine of n partials (device) into *out (device).  Used for
+ * the per-chunk -> total step and for the cross-GPU combine of per-rank
+ * partials after an RCCL all-gather. */
+int pyas_combine_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
+                          int64_t n, uint32_t combine_flags, pyas_partial *out,
+                          void *stream);
+
+/* Standalone HDF5/numcodecs byte un-shuffle (storage.py:121-122), device to
+ * device; n_bytes % elementsize trailing bytes are copied through. */
+int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes,
+                   int32_t elementsize, void *stream);
+
+/* ---- measurement ---------------------------------------------------------- */
+/* When enabled, the main reduce kernel of each pyas_reduce_chunks call is
+ * bracketed by HIP events on the launch stream (up to max_launches calls). */
+int pyas_timing_enable(pyas_ctx *ctx, int32_t max_launches);
+/* Synchronises the recorded events; writes up to cap durations (ms). */
+int pyas_timing_read(pyas_ctx *ctx, float *ms, int32_t cap, int32_t *n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PYAS_H */

@@ -1,0 +1,145 @@
+"""ctypes binding of the C ABI in ``include/pyas.h`` (``lib/libpyas_hip.so``).
+
+This is the only place Python touches the native library.  The product path
+has no CPU fallback: if the shared library is missing or the HIP runtime has
+no device, calls raise ``RuntimeError`` instead of silently computing on the
+host.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+MAX_DIMS = 8
+ABI_VERSION = 1
+
+# pyas_status
+OK, EINVAL, ENOTSUP, EDEVICE, ENOMEM, EINDEX = range(6)
+# pyas_dtype
+I8, U8, I16, U16, I32, U32, I64, U64, F32, F64 = range(10)
+# mask flags
+MASK_EQ0, MASK_EQ1, MASK_GT, MASK_LT, MASK_TAB0, MASK_TAB1 = 1, 2, 4, 8, 16, 32
+COMBINE_ROUND_TO_VAR = 1
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libpyas_hip.so")
+
+
+class Scalar(ctypes.Union):
+    _fields_ = [("f", ctypes.c_double), ("i", ctypes.c_int64), ("u", ctypes.c_uint64)]
+
+
+class Partial(ctypes.Structure):
+    _fields_ = [("sum", Scalar), ("count", ctypes.c_int64), ("min", Scalar), ("max", Scalar)]
+
+
+class Mask(ctypes.Structure):
+    _fields_ = [
+        ("flags", ctypes.c_uint32),
+        ("tab_len", ctypes.c_int32 * 2),
+        ("eq_lo", Scalar * 2),
+        ("eq_hi", Scalar * 2),
+        ("gt", Scalar),
+        ("lt", Scalar),
+        ("tab_lo", ctypes.c_void_p * 2),
+        ("tab_hi", ctypes.c_void_p * 2),
+        ("tab_stride", (ctypes.c_int64 * MAX_DIMS) * 2),
+    ]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int32),
+        ("byteswap", ctypes.c_int32),
+        ("shuffle", ctypes.c_int32),
+        ("ndim", ctypes.c_int32),
+        ("chunk_shape", ctypes.c_int64 * MAX_DIMS),
+        ("n_chunks", ctypes.c_int64),
+        ("data", ctypes.c_void_p),
+        ("offsets", ctypes.c_void_p),
+        ("sel", ctypes.c_void_p),
+        ("index_pool", ctypes.c_void_p),
+    ]
+
+
+PARTIAL_NBYTES = ctypes.sizeof(Partial)
+assert PARTIAL_NBYTES == 32
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_u32 = ctypes.c_uint32
+_sz = ctypes.c_size_t
+
+# name -> argtypes (restype is always c_int except the two noted)
+SIGNATURES = {
+    "pyas_abi_version": [],
+    "pyas_last_error": [],
+    "pyas_device_count": [ctypes.POINTER(ctypes.c_int)],
+    "pyas_ctx_create": [ctypes.c_int, ctypes.POINTER(_vp)],
+    "pyas_ctx_destroy": [_vp],
+    "pyas_ctx_set_tile_bytes": [_vp, _i64],
+    "pyas_malloc": [_vp, _sz, ctypes.POINTER(_vp)],
+    "pyas_free": [_vp, _vp],
+    "pyas_memcpy_h2d": [_vp, _vp, _vp, _sz, _vp],
+    "pyas_memcpy_d2h": [_vp, _vp, _vp, _sz, _vp],
+    "pyas_stream_create": [_vp, ctypes.POINTER(_vp)],
+    "pyas_stream_destroy": [_vp, _vp],
+    "pyas_stream_synchronize": [_vp, _vp],
+    "pyas_reduce_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _u32, _vp],
+    "pyas_reduce_axes": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _u32, _vp, _vp, _vp],
+    "pyas_select_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _vp, _vp],
+    "pyas_combine_partials": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
+    "pyas_unshuffle": [_vp, _vp, _vp, _i64, _i32, _vp],
+    "pyas_timing_enable": [_vp, _i32],
+    "pyas_timing_read": [_vp, ctypes.POINTER(ctypes.c_float), _i32, ctypes.POINTER(_i32)],
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes library handle.
+
+    Raises ``RuntimeError`` if the library has not been built: there is no
+    host fallback for the reduction path.
+    """
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(
+                f"pyactivestorage_amd: HIP library not found at {p}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C "
+                "pyactivestorage_amd/csrc). There is no CPU fallback.")
+        lib = ctypes.CDLL(p)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_char_p if name == "pyas_last_error" else ctypes.c_int
+        if lib.pyas_abi_version() != ABI_VERSION:
+            raise RuntimeError("pyactivestorage_amd: ABI version mismatch with " + p)
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    """Map a pyas_status to the exception type the reference raises."""
+    if rc == OK:
+        return
+    msg = (load().pyas_last_error() or b"").decode(errors="replace")
+    text = f"{what}: {msg}" if what else msg
+    if rc == EINVAL:
+        raise ValueError(text)
+    if rc == ENOTSUP:
+        raise NotImplementedError(text)
+    if rc == EINDEX:
+        raise IndexError(text)
+    if rc == ENOMEM:
+        raise MemoryError(text)
+    raise RuntimeError(text)

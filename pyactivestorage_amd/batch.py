@@ -1,0 +1,127 @@
+"""Batched, device-resident chunk reduction — the throughput path.
+
+A :class:`ReductionPlan` is everything one ``Active.__getitem__`` needs on
+the device (``activestorage/active.py:476-598``): the chunk byte offsets
+inside a device buffer, the per-chunk hyperslab selections, the compiled
+mask, and output space for one partial per chunk plus the combined total.
+Planning (host) happens once; :meth:`ReductionPlan.launch` only enqueues the
+kernel chain on a stream (no host synchronisation, no allocation), so it can
+be timed or captured.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib, engine, selection
+from .device import Context, DeviceBuffer
+from .dtypes import native
+from .masking import compile_missing
+
+
+class ReductionPlan:
+    """Reduce every listed chunk of one variable, fully on the device.
+
+    Parameters
+    ----------
+    ctx: device context.
+    dtype, chunk_shape, shuffle: the variable's storage layout.
+    data_ptr: device pointer of the buffer holding the (uncompressed) chunks.
+    offsets: int64 byte offsets of the chunks inside that buffer.
+    selections: None (every chunk fully selected) or a list of
+        :class:`selection.ChunkSel` (one per chunk, same order as offsets).
+    missing: the ``(fill, missing, valid_min, valid_max)`` tuple.
+    round_to_var: store per-chunk sums in the variable dtype before the
+        combine, as ``Active`` does (``active.py:512,585``).
+    """
+
+    def __init__(self, ctx: Context, dtype, chunk_shape, data_ptr, offsets, *, shuffle=0,
+                 selections=None, missing=None, round_to_var=True, stream=None):
+        self.ctx = ctx
+        self.dtype = np.dtype(dtype)
+        self.chunk_shape = tuple(int(s) for s in chunk_shape)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        self.n_chunks = int(offsets.size)
+        es = self.dtype.itemsize
+        if (offsets % es).any():
+            raise ValueError("chunk offsets must be multiples of the element size")
+        self.round_to_var = bool(round_to_var)
+        self.cm = compile_missing(missing, self.dtype)
+        self._bufs = []
+        st = stream
+        self.offsets_buf = self._upload(offsets, st)
+        sel_ptr = pool_ptr = None
+        sel_shape, kept = self.chunk_shape, tuple(range(len(self.chunk_shape)))
+        if selections is not None:
+            if len(selections) != self.n_chunks:
+                raise ValueError("one selection per chunk is required")
+            table, pool = selection.pack(selections, len(self.chunk_shape))
+            sel_ptr = self._upload(table, st).ptr
+            pool_ptr = self._upload(pool, st).ptr
+            shapes = {s.shape for s in selections}
+            if (self.cm.tables[0] is not None or self.cm.tables[1] is not None) and len(shapes) > 1:
+                raise NotImplementedError("vector fill/missing values need equal selection shapes")
+            if selections:
+                sel_shape, kept = selections[0].shape, selections[0].kept
+        self.layout = engine.Layout(self.dtype, self.chunk_shape,
+                                    shuffle if (shuffle and shuffle > 1 and es > 1) else 0)
+        self.batch = self.layout.batch_struct(self.n_chunks, data_ptr, self.offsets_buf.ptr,
+                                              sel_ptr, pool_ptr)
+        self.mask_up = engine.MaskUpload(ctx, self.cm, sel_shape, kept, st)
+        self.chunk_partials = DeviceBuffer(ctx, max(self.n_chunks, 1) * _lib.PARTIAL_NBYTES)
+        self.total = DeviceBuffer(ctx, _lib.PARTIAL_NBYTES)
+
+    def _upload(self, arr, stream):
+        arr = np.ascontiguousarray(arr)
+        buf = DeviceBuffer(self.ctx, max(arr.nbytes, 16))
+        self.ctx.h2d(buf.ptr, arr, stream)
+        self.ctx.synchronize(stream)
+        self._bufs.append(buf)
+        return buf
+
+    # ------------------------------------------------------------------
+    def launch(self, stream=None, chunk_partials=True) -> None:
+        """Enqueue: fused reduce of every chunk -> per-chunk partials ->
+        fixed-order combine into ``self.total``."""
+        engine.reduce_chunks(self.ctx, self.batch, self.mask_up.struct,
+                             self.chunk_partials.ptr if chunk_partials else None, self.total.ptr,
+                             self.round_to_var, stream)
+
+    def read_total(self, stream=None) -> np.ndarray:
+        host = np.zeros(1, dtype=engine.partial_dtype(self.dtype))
+        self.ctx.d2h(host, self.total.ptr, stream)
+        self.ctx.synchronize(stream)
+        return host
+
+    def read_chunk_partials(self, stream=None) -> np.ndarray:
+        host = np.zeros(self.n_chunks, dtype=engine.partial_dtype(self.dtype))
+        if self.n_chunks:
+            self.ctx.d2h(host, self.chunk_partials.ptr, stream)
+        self.ctx.synchronize(stream)
+        return host
+
+
+def finalize(total: np.ndarray, method: str, dtype, components=False, ndim=1, masked=None):
+    """Host formatting of a combined partial into ``Active``'s return value
+    (``active.py:591-630``): sum/min/max as the variable's reduction dtype,
+    mean = sum / n (float64), or the components dict."""
+    from .dtypes import sum_dtype
+    dt = np.dtype(dtype)
+    t = total.reshape(-1)[0]
+    n = np.full((1,) * ndim, int(t["count"]), dtype=np.int64)
+    shape = (1,) * ndim
+    if method in ("sum", "mean"):
+        # out[] holds per-chunk sums in the variable dtype, np.ma.sum(out) keeps it
+        # for floats; integer out[] sums widen to int64/uint64 (active.py:594)
+        rdt = native(dt) if dt.kind == "f" else sum_dtype(dt)
+        val = np.full(shape, t["sum"]).astype(rdt)
+    else:
+        val = np.full(shape, t[method]).astype(native(dt))
+    out = np.ma.MaskedArray(val, mask=np.full(shape, int(t["count"]) == 0))
+    if components:
+        key = "sum" if method == "mean" else method
+        return {key: out, "n": n}
+    if method == "mean":
+        return out / n
+    return out

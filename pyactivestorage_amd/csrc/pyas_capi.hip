@@ -1,0 +1,461 @@
+// pyas_capi.hip — the extern "C" boundary declared in include/pyas.h.
+//
+// Host-side responsibilities: argument validation (mirroring the reference's
+// error behaviour: ValueError -> PYAS_EINVAL, NotImplementedError ->
+// PYAS_ENOTSUP), geometry (tiles per chunk), per-stream scratch for tile
+// partials, launching the kernel chain on the caller's stream, and optional
+// HIP-event timing of the hot kernel for bench.py.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "pyas.h"
+#include "pyas_internal.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(e == hipErrorOutOfMemory ? PYAS_ENOMEM : PYAS_EDEVICE, "%s: %s", what,
+                hipGetErrorString(e));
+}
+
+#define PYAS_HIP(call)                                  \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #call); \
+    } while (0)
+
+constexpr int64_t kDefaultTileBytes = 256 * 1024;
+
+int elem_size(int dtype) {
+    switch (dtype) {
+        case PYAS_I8: case PYAS_U8: return 1;
+        case PYAS_I16: case PYAS_U16: return 2;
+        case PYAS_I32: case PYAS_U32: case PYAS_F32: return 4;
+        case PYAS_I64: case PYAS_U64: case PYAS_F64: return 8;
+        default: return 0;
+    }
+}
+
+struct Scratch {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct pyas_ctx {
+    int device = 0;
+    int64_t tile_bytes = kDefaultTileBytes;
+    std::mutex mu;
+    std::unordered_map<void *, Scratch> scratch;  // keyed by stream
+    // timing
+    std::vector<hipEvent_t> ev0, ev1;
+    int32_t timing_n = 0;
+};
+
+namespace {
+
+int ensure_scratch(pyas_ctx *ctx, void *stream, size_t bytes, void **out) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Scratch &s = ctx->scratch[stream];
+    if (s.bytes < bytes) {
+        if (s.ptr) {
+            // the stream may still use the old buffer
+            PYAS_HIP(hipStreamSynchronize((hipStream_t)stream));
+            PYAS_HIP(hipFree(s.ptr));
+            s.ptr = nullptr;
+            s.bytes = 0;
+        }
+        const size_t want = bytes < 4096 ? 4096 : bytes;
+        PYAS_HIP(hipMalloc(&s.ptr, want));
+        s.bytes = want;
+    }
+    *out = s.ptr;
+    return PYAS_OK;
+}
+
+// Validate the batch and fill the kernel argument block.
+int prepare(const pyas_ctx *ctx, const pyas_batch *b, const pyas_mask *m, pyas::ReduceArgs &a,
+            int &es, bool &shuf, bool &bsw, bool &masked) {
+    if (!b) return fail(PYAS_EINVAL, "batch is NULL");
+    es = elem_size(b->dtype);
+    if (es == 0) return fail(PYAS_ENOTSUP, "unsupported dtype code %d", b->dtype);
+    if (b->ndim < 1 || b->ndim > PYAS_MAX_DIMS)
+        return fail(PYAS_EINVAL, "chunk rank %d outside 1..%d", b->ndim, PYAS_MAX_DIMS);
+    if (b->n_chunks < 0) return fail(PYAS_EINVAL, "negative chunk count");
+    int64_t elems = 1;
+    for (int d = 0; d < b->ndim; ++d) {
+        if (b->chunk_shape[d] <= 0) return fail(PYAS_EINVAL, "chunk_shape[%d] = %lld", d, (long long)b->chunk_shape[d]);
+        elems *= b->chunk_shape[d];
+        if (elems >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "chunk has >= 2^31 elements");
+    }
+    if (b->shuffle > 1 && b->shuffle != es)
+        return fail(PYAS_ENOTSUP, "shuffle elementsize %d != dtype itemsize %d", b->shuffle, es);
+    if (b->n_chunks > 0 && (!b->data || !b->offsets))
+        return fail(PYAS_EINVAL, "data/offsets pointer is NULL");
+    shuf = b->shuffle > 1 && es > 1;
+    bsw = b->byteswap != 0 && es > 1;
+    std::memset(&a, 0, sizeof(a));
+    a.data = (const uint8_t *)b->data;
+    a.offsets = b->offsets;
+    a.sel = b->sel;
+    a.pool = b->index_pool;
+    a.ndim = b->ndim;
+    a.chunk_elems = elems;
+    int64_t stride = 1;
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+        if (d < b->ndim) {
+            a.shape[d] = b->chunk_shape[d];
+            a.cstride[d] = stride;
+            stride *= b->chunk_shape[d];
+        } else {
+            a.shape[d] = 1;
+            a.cstride[d] = 0;
+        }
+    }
+    masked = false;
+    if (m) {
+        a.mask = *m;
+        const uint32_t known = PYAS_MASK_EQ0 | PYAS_MASK_EQ1 | PYAS_MASK_GT | PYAS_MASK_LT |
+                               PYAS_MASK_TAB0 | PYAS_MASK_TAB1;
+        if (m->flags & ~known) return fail(PYAS_EINVAL, "unknown mask flags 0x%x", m->flags);
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t bit = k == 0 ? PYAS_MASK_TAB0 : PYAS_MASK_TAB1;
+            if (m->flags & bit) {
+                if (!m->tab_lo[k] || !m->tab_hi[k] || m->tab_len[k] <= 0)
+                    return fail(PYAS_EINVAL, "mask table %d enabled but empty", k);
+                a.tab.on[k] = true;
+                a.tab.lo[k] = m->tab_lo[k];
+                a.tab.hi[k] = m->tab_hi[k];
+                for (int d = 0; d < PYAS_MAX_DIMS; ++d) a.tab.stride[k][d] = m->tab_stride[k][d];
+            }
+        }
+        masked = m->flags != 0;
+    }
+    (void)ctx;
+    return PYAS_OK;
+}
+
+int64_t tiles_per_chunk(const pyas_ctx *ctx, int64_t chunk_bytes) {
+    const int64_t tb = ctx->tile_bytes > 0 ? ctx->tile_bytes : kDefaultTileBytes;
+    int64_t t = (chunk_bytes + tb - 1) / tb;
+    return t < 1 ? 1 : t;
+}
+
+// Fixed-order combine of n partials into out[0]; may use scratch at `tmp`
+// (room for n / kSeg + 1 partials).
+constexpr int64_t kSeg = 2048;
+
+int combine_into(int dtype, const pyas_partial *in, int64_t n, uint32_t flags, pyas_partial *tmp,
+                 pyas_partial *out, hipStream_t st) {
+    if (n <= 0) {
+        PYAS_HIP(hipMemsetAsync(out, 0, sizeof(pyas_partial), st));
+        return PYAS_OK;
+    }
+    const int64_t nblocks = (n + kSeg - 1) / kSeg;
+    if (nblocks == 1) {
+        PYAS_HIP(pyas::launch_combine(dtype, in, n, kSeg, 1, flags, out, st));
+        return PYAS_OK;
+    }
+    PYAS_HIP(pyas::launch_combine(dtype, in, n, kSeg, nblocks, flags, tmp, st));
+    PYAS_HIP(pyas::launch_combine(dtype, tmp, nblocks, nblocks, 1, 0u, out, st));
+    return PYAS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pyas_abi_version(void) { return PYAS_ABI_VERSION; }
+
+const char *pyas_last_error(void) { return g_err.c_str(); }
+
+int pyas_device_count(int *count) {
+    if (!count) return fail(PYAS_EINVAL, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return hip_fail(e, "hipGetDeviceCount");
+    }
+    *count = n;
+    return PYAS_OK;
+}
+
+int pyas_ctx_create(int device, pyas_ctx **out) {
+    if (!out) return fail(PYAS_EINVAL, "out is NULL");
+    int n = 0;
+    PYAS_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(PYAS_EINVAL, "device %d not in [0, %d)", device, n);
+    PYAS_HIP(hipSetDevice(device));
+    pyas_ctx *c = new pyas_ctx();
+    c->device = device;
+    *out = c;
+    return PYAS_OK;
+}
+
+int pyas_ctx_destroy(pyas_ctx *ctx) {
+    if (!ctx) return PYAS_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    for (auto &kv : ctx->scratch)
+        if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+    for (auto e : ctx->ev0) (void)hipEventDestroy(e);
+    for (auto e : ctx->ev1) (void)hipEventDestroy(e);
+    delete ctx;
+    return PYAS_OK;
+}
+
+int pyas_ctx_set_tile_bytes(pyas_ctx *ctx, int64_t tile_bytes) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (tile_bytes < 0) return fail(PYAS_EINVAL, "tile_bytes < 0");
+    ctx->tile_bytes = tile_bytes == 0 ? kDefaultTileBytes : tile_bytes;
+    return PYAS_OK;
+}
+
+int pyas_malloc(pyas_ctx *ctx, size_t nbytes, void **dptr) {
+    if (!ctx || !dptr) return fail(PYAS_EINVAL, "NULL argument");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    *dptr = nullptr;
+    PYAS_HIP(hipMalloc(dptr, nbytes ? nbytes : 1));
+    return PYAS_OK;
+}
+
+int pyas_free(pyas_ctx *ctx, void *dptr) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!dptr) return PYAS_OK;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(hipFree(dptr));
+    return PYAS_OK;
+}
+
+int pyas_memcpy_h2d(pyas_ctx *ctx, void *dst, const void *src, size_t n, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (n == 0) return PYAS_OK;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
+int pyas_memcpy_d2h(pyas_ctx *ctx, void *dst, const void *src, size_t n, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (n == 0) return PYAS_OK;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
+int pyas_stream_create(pyas_ctx *ctx, void **stream) {
+    if (!ctx || !stream) return fail(PYAS_EINVAL, "NULL argument");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    hipStream_t s;
+    PYAS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = (void *)s;
+    return PYAS_OK;
+}
+
+int pyas_stream_destroy(pyas_ctx *ctx, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!stream) return PYAS_OK;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(hipStreamSynchronize((hipStream_t)stream));
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        auto it = ctx->scratch.find(stream);
+        if (it != ctx->scratch.end()) {
+            if (it->second.ptr) (void)hipFree(it->second.ptr);
+            ctx->scratch.erase(it);
+        }
+    }
+    PYAS_HIP(hipStreamDestroy((hipStream_t)stream));
+    return PYAS_OK;
+}
+
+int pyas_stream_synchronize(pyas_ctx *ctx, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return PYAS_OK;
+}
+
+int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                       pyas_partial *chunk_out, pyas_partial *total, uint32_t combine_flags,
+                       void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!chunk_out && !total) return fail(PYAS_EINVAL, "neither chunk_out nor total given");
+    if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
+        return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
+    pyas::ReduceArgs a;
+    int es;
+    bool shuf, bsw, masked;
+    int rc = prepare(ctx, batch, mask, a, es, shuf, bsw, masked);
+    if (rc) return rc;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t n = batch->n_chunks;
+    if (n == 0) {
+        if (total) PYAS_HIP(hipMemsetAsync(total, 0, sizeof(pyas_partial), st));
+        return PYAS_OK;
+    }
+    const int64_t tpc = tiles_per_chunk(ctx, a.chunk_elems * es);
+    const int64_t grid = n * tpc;
+    if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid of %lld workgroups", (long long)grid);
+    a.tpc = tpc;
+    // scratch layout: [tiles (tpc>1)] [chunk partials (if chunk_out NULL)] [combine tmp]
+    const size_t tiles_b = tpc > 1 ? (size_t)grid * sizeof(pyas_partial) : 0;
+    const size_t chunks_b = chunk_out ? 0 : (size_t)n * sizeof(pyas_partial);
+    const size_t tmp_b = ((size_t)(n / kSeg) + 2) * sizeof(pyas_partial);
+    void *scr = nullptr;
+    rc = ensure_scratch(ctx, stream, tiles_b + chunks_b + tmp_b, &scr);
+    if (rc) return rc;
+    pyas_partial *tiles = (pyas_partial *)scr;
+    pyas_partial *chunks = chunk_out ? chunk_out : (pyas_partial *)((char *)scr + tiles_b);
+    pyas_partial *tmp = (pyas_partial *)((char *)scr + tiles_b + chunks_b);
+    a.out = tpc > 1 ? tiles : chunks;
+
+    const bool timed = ctx->timing_n < (int32_t)ctx->ev0.size();
+    if (timed) PYAS_HIP(hipEventRecord(ctx->ev0[ctx->timing_n], st));
+    PYAS_HIP(pyas::launch_reduce(batch->dtype, a, shuf, bsw, masked, grid, st));
+    if (timed) {
+        PYAS_HIP(hipEventRecord(ctx->ev1[ctx->timing_n], st));
+        ctx->timing_n++;
+    }
+    if (tpc > 1) PYAS_HIP(pyas::launch_tiles_to_chunks(batch->dtype, tiles, tpc, n, chunks, st));
+    if (total) {
+        rc = combine_into(batch->dtype, chunks, n, combine_flags, tmp, total, st);
+        if (rc) return rc;
+    }
+    return PYAS_OK;
+}
+
+int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                     uint32_t axes_mask, const int64_t *out_offsets, pyas_partial *out,
+                     void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    pyas::AxesArgs x;
+    std::memset(&x, 0, sizeof(x));
+    int es;
+    bool shuf, bsw, masked;
+    int rc = prepare(ctx, batch, mask, x.r, es, shuf, bsw, masked);
+    if (rc) return rc;
+    if (axes_mask >> batch->ndim) return fail(PYAS_EINVAL, "axes mask 0x%x beyond rank %d", axes_mask, batch->ndim);
+    if (batch->n_chunks == 0) return PYAS_OK;
+    if (!out_offsets || !out) return fail(PYAS_EINVAL, "out/out_offsets is NULL");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    int64_t keep_elems = 1;
+    for (int d = 0; d < batch->ndim; ++d)
+        if (!((axes_mask >> d) & 1u)) keep_elems *= batch->chunk_shape[d];
+    int64_t bpc = (keep_elems + pyas::kBlock - 1) / pyas::kBlock;
+    if (bpc > 64) bpc = 64;
+    x.axes = axes_mask;
+    x.bpc = bpc;
+    x.out_offsets = out_offsets;
+    x.out = out;
+    x.shuf = shuf;
+    x.bswap = bsw;
+    const int64_t grid = batch->n_chunks * bpc;
+    if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
+    PYAS_HIP(pyas::launch_reduce_axes(batch->dtype, x, grid, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
+int pyas_select_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                       const int64_t *out_offsets, void *values, uint8_t *mask_out,
+                       void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    pyas::SelectArgs x;
+    std::memset(&x, 0, sizeof(x));
+    int es;
+    bool shuf, bsw, masked;
+    int rc = prepare(ctx, batch, mask, x.r, es, shuf, bsw, masked);
+    if (rc) return rc;
+    if (batch->n_chunks == 0) return PYAS_OK;
+    if (!out_offsets || !values) return fail(PYAS_EINVAL, "values/out_offsets is NULL");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    int64_t bpc = (x.r.chunk_elems + pyas::kBlock - 1) / pyas::kBlock;
+    if (bpc > 64) bpc = 64;
+    x.bpc = bpc;
+    x.out_offsets = out_offsets;
+    x.values = values;
+    x.mask_out = mask_out;
+    x.shuf = shuf;
+    x.bswap = bsw;
+    const int64_t grid = batch->n_chunks * bpc;
+    if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
+    PYAS_HIP(pyas::launch_select(batch->dtype, x, grid, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
+int pyas_combine_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, int64_t n,
+                          uint32_t combine_flags, pyas_partial *out, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (elem_size(dtype) == 0) return fail(PYAS_ENOTSUP, "unsupported dtype code %d", dtype);
+    if (!out || (n > 0 && !in)) return fail(PYAS_EINVAL, "NULL partials");
+    if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
+        return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
+    PYAS_HIP(hipSetDevice(ctx->device));
+    void *scr = nullptr;
+    int rc = ensure_scratch(ctx, stream, ((size_t)(n / kSeg) + 2) * sizeof(pyas_partial), &scr);
+    if (rc) return rc;
+    return combine_into(dtype, in, n, combine_flags, (pyas_partial *)scr, out, (hipStream_t)stream);
+}
+
+int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes, int32_t elementsize,
+                   void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (n_bytes < 0 || elementsize < 1) return fail(PYAS_EINVAL, "bad size/elementsize");
+    if (n_bytes == 0) return PYAS_OK;
+    if (!src || !dst) return fail(PYAS_EINVAL, "NULL buffer");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(pyas::launch_unshuffle(src, dst, n_bytes, elementsize, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
+int pyas_timing_enable(pyas_ctx *ctx, int32_t max_launches) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (max_launches < 0) return fail(PYAS_EINVAL, "max_launches < 0");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    for (auto e : ctx->ev0) (void)hipEventDestroy(e);
+    for (auto e : ctx->ev1) (void)hipEventDestroy(e);
+    ctx->ev0.assign(max_launches, nullptr);
+    ctx->ev1.assign(max_launches, nullptr);
+    for (int i = 0; i < max_launches; ++i) {
+        PYAS_HIP(hipEventCreate(&ctx->ev0[i]));
+        PYAS_HIP(hipEventCreate(&ctx->ev1[i]));
+    }
+    ctx->timing_n = 0;
+    return PYAS_OK;
+}
+
+int pyas_timing_read(pyas_ctx *ctx, float *ms, int32_t cap, int32_t *n) {
+    if (!ctx || !n) return fail(PYAS_EINVAL, "NULL argument");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    const int32_t m = ctx->timing_n < cap ? ctx->timing_n : cap;
+    for (int i = 0; i < m; ++i) {
+        PYAS_HIP(hipEventSynchronize(ctx->ev1[i]));
+        PYAS_HIP(hipEventElapsedTime(&ms[i], ctx->ev0[i], ctx->ev1[i]));
+    }
+    *n = m;
+    return PYAS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// pyas_internal.hpp — kernel argument blocks and launcher prototypes shared by
+// pyas_kernels.hip (device code) and pyas_capi.hip (the extern "C" boundary).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pyas.h"
+#include "pyas_device.hpp"
+
+namespace pyas {
+
+// Passed by value in the kernarg segment (a few hundred bytes).
+struct ReduceArgs {
+    const uint8_t *data;
+    const int64_t *offsets;
+    const int32_t *sel;
+    const int32_t *pool;
+    int64_t shape[PYAS_MAX_DIMS];
+    int64_t cstride[PYAS_MAX_DIMS];   // row-major element strides of a chunk
+    int64_t chunk_elems;
+    int64_t tpc;                      // tiles (workgroups) per chunk
+    int32_t ndim;
+    pyas_mask mask;
+    MaskTab tab;
+    pyas_partial *out;
+};
+
+struct AxesArgs {
+    ReduceArgs r;
+    uint32_t axes;
+    int64_t bpc;                      // workgroups per chunk
+    const int64_t *out_offsets;
+    pyas_partial *out;
+    bool shuf, bswap;
+};
+
+struct SelectArgs {
+    ReduceArgs r;
+    int64_t bpc;
+    const int64_t *out_offsets;
+    void *values;
+    uint8_t *mask_out;
+    bool shuf, bswap;
+};
+
+hipError_t launch_reduce(int dtype, const ReduceArgs &a, bool shuf, bool bsw, bool masked,
+                         int64_t grid, hipStream_t st);
+hipError_t launch_tiles_to_chunks(int dtype, const pyas_partial *tiles, int64_t tpc,
+                                  int64_t n_chunks, pyas_partial *out, hipStream_t st);
+hipError_t launch_combine(int dtype, const pyas_partial *in, int64_t n, int64_t seg,
+                          int64_t nblocks, uint32_t flags, pyas_partial *out, hipStream_t st);
+hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st);
+hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
+hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es,
+                            hipStream_t st);
+
+}  // namespace pyas

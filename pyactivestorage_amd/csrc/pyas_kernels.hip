@@ -1,0 +1,469 @@
+// pyas_kernels.hip — gfx950 kernels of the chunk-reduction backend.
+//
+// k_reduce        : the hot path.  One workgroup per (chunk, tile); streams the
+//                   chunk's selected bytes from HBM with 16-B loads, undoes the
+//                   HDF5 shuffle in registers (v_perm byte transposes), swaps
+//                   byte order, applies the compiled mask and reduces to
+//                   {sum, count, min, max}.  Replaces storage.py:51-100 per chunk.
+// k_tiles_to_chunks / k_combine : fixed-order combine of partials
+//                   (active.py:575-598), no atomics => deterministic.
+// k_reduce_axes   : partial-axis reduction (storage.py:98-100, axis ⊂ dims).
+// k_select        : method=None path (storage.py:95-96, returns data + mask).
+// k_unshuffle     : standalone filter reversal (storage.py:121-122).
+#include <hip/hip_runtime.h>
+
+#include "pyas_device.hpp"
+#include "pyas_internal.hpp"
+
+namespace pyas {
+
+// ---------------------------------------------------------------------------
+// vector un-shuffle: 16 consecutive elements from ES byte planes
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__device__ __forceinline__ uint32_t word(const uint4 &v, int j) {
+    return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
+}
+// a,b,c,d hold byte 0,1,2,3 of four consecutive elements; returns the four
+// little-endian 32-bit words (8 v_perm_b32).
+__device__ __forceinline__ void transpose4(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                           uint32_t e[4]) {
+    const uint32_t t0 = perm(b, a, 0x05010400u), t1 = perm(b, a, 0x07030602u);
+    const uint32_t u0 = perm(d, c, 0x05010400u), u1 = perm(d, c, 0x07030602u);
+    e[0] = perm(u0, t0, 0x05040100u);
+    e[1] = perm(u0, t0, 0x07060302u);
+    e[2] = perm(u1, t1, 0x05040100u);
+    e[3] = perm(u1, t1, 0x07060302u);
+}
+
+template <typename T, bool BSWAP>
+__device__ __forceinline__ void unshuffle16(const uint4 *pl, T out[16]) {
+    constexpr int ES = sizeof(T);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if constexpr (ES == 2) {
+            const uint32_t a = word(pl[BSWAP ? 1 : 0], j), b = word(pl[BSWAP ? 0 : 1], j);
+            const uint32_t w0 = perm(b, a, 0x05010400u), w1 = perm(b, a, 0x07030602u);
+            out[4 * j + 0] = bits_to<T>((uint16_t)(w0 & 0xffffu));
+            out[4 * j + 1] = bits_to<T>((uint16_t)(w0 >> 16));
+            out[4 * j + 2] = bits_to<T>((uint16_t)(w1 & 0xffffu));
+            out[4 * j + 3] = bits_to<T>((uint16_t)(w1 >> 16));
+        } else if constexpr (ES == 4) {
+            uint32_t e[4];
+            if (BSWAP) transpose4(word(pl[3], j), word(pl[2], j), word(pl[1], j), word(pl[0], j), e);
+            else transpose4(word(pl[0], j), word(pl[1], j), word(pl[2], j), word(pl[3], j), e);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) out[4 * j + k] = bits_to<T>(e[k]);
+        } else if constexpr (ES == 8) {
+            uint32_t lo[4], hi[4];
+            if (BSWAP) {
+                transpose4(word(pl[7], j), word(pl[6], j), word(pl[5], j), word(pl[4], j), lo);
+                transpose4(word(pl[3], j), word(pl[2], j), word(pl[1], j), word(pl[0], j), hi);
+            } else {
+                transpose4(word(pl[0], j), word(pl[1], j), word(pl[2], j), word(pl[3], j), lo);
+                transpose4(word(pl[4], j), word(pl[5], j), word(pl[6], j), word(pl[7], j), hi);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                out[4 * j + k] = bits_to<T>(((uint64_t)hi[k] << 32) | (uint64_t)lo[k]);
+        }
+    }
+}
+
+// Raw 16 bytes of the plain layout -> 16/ES values
+template <typename T, bool BSWAP, bool MASKED>
+__device__ __forceinline__ void consume16(const uint4 &r, Acc<T> &acc, const MaskT<T> &mk) {
+    using U = typename TT<T>::U;
+    constexpr int N = 16 / sizeof(T);
+    U w[N];
+    __builtin_memcpy(w, &r, 16);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        U u = w[k];
+        if (BSWAP) u = bswap(u);
+        acc.template add<MASKED>(bits_to<T>(u), mk);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// contiguous runs
+// ---------------------------------------------------------------------------
+// Plain layout, memory elements [m0, m1) of the chunk at `base`.
+template <typename T, bool BSWAP, bool MASKED>
+__device__ void run_plain(const uint8_t *base, int64_t m0, int64_t m1, Acc<T> &acc,
+                          const MaskT<T> &mk) {
+    constexpr int ES = sizeof(T);
+    const int tid = threadIdx.x;
+    const uintptr_t p0 = (uintptr_t)(base + m0 * ES), p1 = (uintptr_t)(base + m1 * ES);
+    const uintptr_t a0 = (p0 + 15) & ~(uintptr_t)15, a1 = p1 & ~(uintptr_t)15;
+    if (a0 >= a1) {
+        for (int64_t i = m0 + tid; i < m1; i += kBlock)
+            acc.template add<MASKED>(load_plain<T, BSWAP>(base, i), mk);
+        return;
+    }
+    const int64_t nhead = (int64_t)(a0 - p0) / ES, ntail = (int64_t)(p1 - a1) / ES;
+    if (tid < nhead) acc.template add<MASKED>(load_plain<T, BSWAP>(base, m0 + tid), mk);
+    if (tid < ntail) acc.template add<MASKED>(load_plain<T, BSWAP>(base, m1 - ntail + tid), mk);
+    const uint4 *v = reinterpret_cast<const uint4 *>(a0);
+    const int64_t nvec = (int64_t)(a1 - a0) / 16;
+    constexpr int U = 4;
+    const int64_t nfull = nvec / (U * kBlock) * (U * kBlock);
+    for (int64_t k = tid; k < nfull; k += U * kBlock) {
+        uint4 r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = v[k + u * kBlock];
+#pragma unroll
+        for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED>(r[u], acc, mk);
+    }
+    for (int64_t k = nfull + tid; k < nvec; k += kBlock) consume16<T, BSWAP, MASKED>(v[k], acc, mk);
+}
+
+// Shuffled layout, chunk elements [i0, i1); n = elements in the chunk.
+template <typename T, bool BSWAP, bool MASKED>
+__device__ void run_shuffled(const uint8_t *base, int64_t n, int64_t i0, int64_t i1,
+                             Acc<T> &acc, const MaskT<T> &mk) {
+    constexpr int ES = sizeof(T);
+    const int tid = threadIdx.x;
+    const bool vec_ok = (((uintptr_t)base & 15) == 0) && ((n & 15) == 0);
+    int64_t g0 = (i0 + 15) & ~(int64_t)15, g1 = i1 & ~(int64_t)15;
+    if (!vec_ok || g0 >= g1) {
+        for (int64_t i = i0 + tid; i < i1; i += kBlock)
+            acc.template add<MASKED>(load_shuffled<T, BSWAP>(base, n, i), mk);
+        return;
+    }
+    if (tid < g0 - i0) acc.template add<MASKED>(load_shuffled<T, BSWAP>(base, n, i0 + tid), mk);
+    if (tid < i1 - g1) acc.template add<MASKED>(load_shuffled<T, BSWAP>(base, n, g1 + tid), mk);
+    const int64_t ng = (g1 - g0) / 16;
+    for (int64_t g = tid; g < ng; g += kBlock) {
+        const int64_t i = g0 + g * 16;
+        uint4 pl[ES];
+#pragma unroll
+        for (int b = 0; b < ES; ++b) pl[b] = *reinterpret_cast<const uint4 *>(base + (int64_t)b * n + i);
+        T x[16];
+        unshuffle16<T, BSWAP>(pl, x);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc.template add<MASKED>(x[k], mk);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// generic (strided / listed / table-masked) selections
+// ---------------------------------------------------------------------------
+struct Decomp {
+    int64_t mem;
+    int64_t v[2];
+};
+
+// Decompose position e (row-major over the dims whose bit is in dmask) into
+// chunk memory index and table indices.
+__device__ __forceinline__ void decompose(const Sel &s, const int32_t *pool, const int64_t *cstride,
+                                          const MaskTab &tab, int ndim, uint32_t dmask,
+                                          int64_t e, Decomp &o) {
+#pragma unroll
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+        if (d < ndim && ((dmask >> d) & 1u)) {
+            const int64_t cd = s.cnt[d];
+            const int64_t q = e / cd, k = e - q * cd;
+            e = q;
+            o.mem += sel_index(s, pool, d, k) * cstride[d];
+            o.v[0] += k * tab.stride[0][d];
+            o.v[1] += k * tab.stride[1][d];
+        }
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ bool all_masked(const MaskT<T> &mk, const MaskTab &tab, const Decomp &o, T x) {
+    bool m = mk.masked(x);
+    if (tab.on[0]) m |= tab_masked<T>(tab, 0, o.v[0], x);
+    if (tab.on[1]) m |= tab_masked<T>(tab, 1, o.v[1], x);
+    return m;
+}
+
+template <typename T, bool SHUF, bool BSWAP, bool MASKED>
+__device__ void run_generic(const ReduceArgs &a, const uint8_t *base, const Sel &s, int64_t e0,
+                            int64_t e1, Acc<T> &acc, const MaskT<T> &mk) {
+    const uint32_t all = (1u << a.ndim) - 1u;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
+        Decomp o{0, {0, 0}};
+        decompose(s, a.pool, a.cstride, a.tab, a.ndim, all, e, o);
+        const T x = load_elem<T, SHUF, BSWAP>(base, a.chunk_elems, o.mem);
+        if constexpr (MASKED) acc.add_flag(x, all_masked(mk, a.tab, o, x));
+        else acc.add_valid(x);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the hot kernel
+// ---------------------------------------------------------------------------
+template <typename T, bool SHUF, bool BSWAP, bool MASKED>
+__global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
+    const int64_t b = blockIdx.x;
+    const int64_t c = b / a.tpc;
+    const int64_t t = b - c * a.tpc;
+    const uint8_t *base = a.data + a.offsets[c];
+    MaskT<T> mk;
+    if constexpr (MASKED) mk.init(a.mask);
+    Acc<T> acc;
+    acc.init();
+    Sel s;
+    load_sel(s, a.sel, c, a.ndim, a.shape);
+    int64_t total = 1;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) total *= (int64_t)s.cnt[d];
+    int64_t per = (total + a.tpc - 1) / a.tpc;
+    per = (per + 63) & ~(int64_t)63;
+    const int64_t e0 = t * per, e1 = e0 + per < total ? e0 + per : total;
+    if (e0 < e1) {
+        // Is the selection one contiguous run of chunk memory?  (innermost
+        // non-full dim has unit step; every dim outside it picks one index)
+        bool contig = !(a.tab.on[0] || a.tab.on[1]);
+        bool seen_partial = false;
+        int64_t m0 = 0;
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            if (d < a.ndim) {
+                const bool full = s.step[d] == 1 && s.start[d] == 0 && (int64_t)s.cnt[d] == a.shape[d];
+                if (seen_partial) {
+                    if (s.cnt[d] > 1) contig = false;
+                } else if (!full) {
+                    seen_partial = true;
+                    if (s.cnt[d] > 1 && s.step[d] != 1) contig = false;
+                }
+                if (s.cnt[d] > 0) m0 += sel_index(s, a.pool, d, 0) * a.cstride[d];
+            }
+        }
+        if (contig) {
+            if constexpr (SHUF && sizeof(T) > 1)
+                run_shuffled<T, BSWAP, MASKED>(base, a.chunk_elems, m0 + e0, m0 + e1, acc, mk);
+            else
+                run_plain<T, BSWAP, MASKED>(base, m0 + e0, m0 + e1, acc, mk);
+        } else {
+            run_generic<T, SHUF, BSWAP, MASKED>(a, base, s, e0, e1, acc, mk);
+        }
+    }
+    block_reduce(acc);
+    if (threadIdx.x == 0) store_partial(a.out + b, acc);
+}
+
+// ---------------------------------------------------------------------------
+// combines (fixed order)
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ typename TT<T>::Acc sum_of(const pyas_scalar &s, bool round) {
+    using A = typename TT<T>::Acc;
+    if constexpr (TT<T>::kind == 0) return round ? (A)(T)s.f : (A)s.f;
+    else if constexpr (TT<T>::kind == 1) return round ? (A)(T)s.i : (A)s.i;
+    else return round ? (A)(T)s.u : (A)s.u;
+}
+
+template <typename T>
+__device__ __forceinline__ void merge(WAcc<T> &acc, const pyas_partial &p, bool round) {
+    acc.sum += sum_of<T>(p.sum, round);
+    if (p.count > 0) {
+        acc.count += p.count;
+        acc.mn = pmin(acc.mn, TT<T>::from(p.min));
+        acc.mx = pmax(acc.mx, TT<T>::from(p.max));
+    }
+}
+
+// tiles -> chunks: one wave per chunk
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_tiles_to_chunks(const pyas_partial *tiles, int64_t tpc,
+                                                            int64_t n_chunks, pyas_partial *out) {
+    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    if (c >= n_chunks) return;  // wave-uniform
+    WAcc<T> acc;
+    acc.init();
+    for (int64_t t = lane; t < tpc; t += kWave) merge(acc, tiles[c * tpc + t], false);
+    wave_reduce(acc);
+    if (lane == 0) store_wpartial(out + c, acc);
+}
+
+// n partials -> one per block (contiguous segments), fixed order
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_combine(const pyas_partial *in, int64_t n, int64_t seg,
+                                                    uint32_t flags, pyas_partial *out) {
+    const int64_t lo = (int64_t)blockIdx.x * seg;
+    const int64_t hi = lo + seg < n ? lo + seg : n;
+    const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
+    WAcc<T> acc;
+    acc.init();
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) merge(acc, in[i], round);
+    block_reduce_w(acc);
+    if (threadIdx.x == 0) store_wpartial(out + blockIdx.x, acc);
+}
+
+// ---------------------------------------------------------------------------
+// partial-axis reduction (axis ⊂ dims), one thread per output element
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_reduce_axes(AxesArgs a) {
+    const int64_t c = blockIdx.x / a.bpc;
+    const int64_t j = blockIdx.x - c * a.bpc;
+    const ReduceArgs &r = a.r;
+    const uint8_t *base = r.data + r.offsets[c];
+    MaskT<T> mk;
+    mk.init(r.mask);
+    Sel s;
+    load_sel(s, r.sel, c, r.ndim, r.shape);
+    const uint32_t all = (1u << r.ndim) - 1u;
+    const uint32_t red = a.axes & all, keep = all & ~red;
+    int64_t n_out = 1, n_red = 1;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+        if (d < r.ndim) {
+            if ((red >> d) & 1u) n_red *= s.cnt[d];
+            else n_out *= s.cnt[d];
+        }
+    }
+    for (int64_t o = j * kBlock + threadIdx.x; o < n_out; o += a.bpc * kBlock) {
+        Decomp ok{0, {0, 0}};
+        decompose(s, r.pool, r.cstride, r.tab, r.ndim, keep, o, ok);
+        WAcc<T> acc;
+        acc.init();
+        for (int64_t q = 0; q < n_red; ++q) {
+            Decomp od = ok;
+            decompose(s, r.pool, r.cstride, r.tab, r.ndim, red, q, od);
+            const T x = load_elem_rt<T>(base, r.chunk_elems, od.mem, a.shuf, a.bswap);
+            if (!all_masked(mk, r.tab, od, x)) {
+                acc.sum += (typename TT<T>::Acc)x;
+                acc.count += 1;
+                acc.mn = pmin(acc.mn, x);
+                acc.mx = pmax(acc.mx, x);
+            }
+        }
+        store_wpartial(a.out + a.out_offsets[c] + o, acc);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// method=None: select + mask into dense outputs
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_select(SelectArgs a) {
+    const int64_t c = blockIdx.x / a.bpc;
+    const int64_t j = blockIdx.x - c * a.bpc;
+    const ReduceArgs &r = a.r;
+    const uint8_t *base = r.data + r.offsets[c];
+    MaskT<T> mk;
+    mk.init(r.mask);
+    Sel s;
+    load_sel(s, r.sel, c, r.ndim, r.shape);
+    int64_t total = 1;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) total *= s.cnt[d];
+    const uint32_t all = (1u << r.ndim) - 1u;
+    T *vals = reinterpret_cast<T *>(a.values) + a.out_offsets[c];
+    uint8_t *msk = a.mask_out ? a.mask_out + a.out_offsets[c] : nullptr;
+    for (int64_t e = j * kBlock + threadIdx.x; e < total; e += a.bpc * kBlock) {
+        Decomp o{0, {0, 0}};
+        decompose(s, r.pool, r.cstride, r.tab, r.ndim, all, e, o);
+        const T x = load_elem_rt<T>(base, r.chunk_elems, o.mem, a.shuf, a.bswap);
+        vals[e] = x;
+        if (msk) msk[e] = all_masked(mk, r.tab, o, x) ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_unshuffle(const uint8_t *src, uint8_t *dst, int64_t nbytes,
+                                                      int64_t es) {
+    const int64_t n = nbytes / es;
+    const int64_t body = n * es;
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nbytes;
+         q += (int64_t)gridDim.x * kBlock) {
+        if (q < body) {
+            const int64_t i = q / es, b = q - i * es;
+            dst[q] = src[b * n + i];
+        } else {
+            dst[q] = src[q];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <typename T>
+static hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool masked,
+                                  int64_t grid, hipStream_t st) {
+    const dim3 g((unsigned)grid), blk(kBlock);
+#define PYAS_L(S, B, M) hipLaunchKernelGGL((k_reduce<T, S, B, M>), g, blk, 0, st, a)
+    if constexpr (sizeof(T) == 1) {
+        if (masked) PYAS_L(false, false, true);
+        else PYAS_L(false, false, false);
+    } else {
+        if (shuf) {
+            if (bsw) { if (masked) PYAS_L(true, true, true); else PYAS_L(true, true, false); }
+            else { if (masked) PYAS_L(true, false, true); else PYAS_L(true, false, false); }
+        } else {
+            if (bsw) { if (masked) PYAS_L(false, true, true); else PYAS_L(false, true, false); }
+            else { if (masked) PYAS_L(false, false, true); else PYAS_L(false, false, false); }
+        }
+    }
+#undef PYAS_L
+    return hipGetLastError();
+}
+
+#define PYAS_DISPATCH_T(DT, CALL)                                  \
+    switch (DT) {                                                  \
+        case PYAS_I8: { using T = int8_t; CALL; } break;           \
+        case PYAS_U8: { using T = uint8_t; CALL; } break;          \
+        case PYAS_I16: { using T = int16_t; CALL; } break;         \
+        case PYAS_U16: { using T = uint16_t; CALL; } break;        \
+        case PYAS_I32: { using T = int32_t; CALL; } break;         \
+        case PYAS_U32: { using T = uint32_t; CALL; } break;        \
+        case PYAS_I64: { using T = int64_t; CALL; } break;         \
+        case PYAS_U64: { using T = uint64_t; CALL; } break;        \
+        case PYAS_F32: { using T = float; CALL; } break;           \
+        case PYAS_F64: { using T = double; CALL; } break;          \
+        default: return hipErrorInvalidValue;                      \
+    }
+
+hipError_t launch_reduce(int dtype, const ReduceArgs &a, bool shuf, bool bsw, bool masked,
+                         int64_t grid, hipStream_t st) {
+    hipError_t e = hipSuccess;
+    PYAS_DISPATCH_T(dtype, e = launch_reduce_t<T>(a, shuf, bsw, masked, grid, st));
+    return e;
+}
+
+hipError_t launch_tiles_to_chunks(int dtype, const pyas_partial *tiles, int64_t tpc, int64_t n_chunks,
+                                  pyas_partial *out, hipStream_t st) {
+    const int per_block = kBlock / kWave;
+    const dim3 g((unsigned)((n_chunks + per_block - 1) / per_block)), blk(kBlock);
+    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_tiles_to_chunks<T>), g, blk, 0, st, tiles, tpc,
+                                              n_chunks, out));
+    return hipGetLastError();
+}
+
+hipError_t launch_combine(int dtype, const pyas_partial *in, int64_t n, int64_t seg, int64_t nblocks,
+                          uint32_t flags, pyas_partial *out, hipStream_t st) {
+    const dim3 g((unsigned)nblocks), blk(kBlock);
+    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_combine<T>), g, blk, 0, st, in, n, seg, flags, out));
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st) {
+    const dim3 g((unsigned)grid), blk(kBlock);
+    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_reduce_axes<T>), g, blk, 0, st, a));
+    return hipGetLastError();
+}
+
+hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st) {
+    const dim3 g((unsigned)grid), blk(kBlock);
+    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_select<T>), g, blk, 0, st, a));
+    return hipGetLastError();
+}
+
+hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es, hipStream_t st) {
+    int64_t blocks = (nbytes + kBlock - 1) / kBlock;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_unshuffle, dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                       (const uint8_t *)src, (uint8_t *)dst, nbytes, es);
+    return hipGetLastError();
+}
+
+}  // namespace pyas

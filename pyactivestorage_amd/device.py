@@ -1,0 +1,114 @@
+"""Device context, streams and device buffers over the C ABI.
+
+One ``Context`` per GPU (process-wide, created lazily).  Every calling thread
+gets its own HIP stream so that concurrent ``reduce_chunk`` calls from the
+reference's 30-thread pool (``activestorage/active.py:557-572``) never share
+scratch memory; the C library keys its scratch by stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib
+
+_ctx_lock = threading.Lock()
+_contexts: dict[int, "Context"] = {}
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _lib.check(_lib.load().pyas_device_count(ctypes.byref(n)), "pyas_device_count")
+    return n.value
+
+
+class DeviceBuffer:
+    """Owning device allocation made through ``pyas_malloc``."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        _lib.check(ctx.lib.pyas_malloc(ctx.handle, max(self.nbytes, 1), ctypes.byref(p)),
+                   "pyas_malloc")
+        self.ptr = p.value
+
+    def free(self):
+        if self.ptr:
+            self.ctx.lib.pyas_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    """A ``pyas_ctx`` bound to one device."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.pyas_ctx_create(self.device, ctypes.byref(h)), "pyas_ctx_create")
+        self.handle = h.value
+        self._tls = threading.local()
+
+    # -- streams -------------------------------------------------------------
+    def thread_stream(self) -> int:
+        s = getattr(self._tls, "stream", None)
+        if s is None:
+            p = ctypes.c_void_p()
+            _lib.check(self.lib.pyas_stream_create(self.handle, ctypes.byref(p)),
+                       "pyas_stream_create")
+            s = self._tls.stream = p.value
+        return s
+
+    def synchronize(self, stream: int | None) -> None:
+        _lib.check(self.lib.pyas_stream_synchronize(self.handle, stream), "pyas_stream_synchronize")
+        self._tls.pending = []
+
+    # -- per-thread growable scratch buffers ---------------------------------
+    def thread_buffer(self, slot: str, nbytes: int) -> DeviceBuffer:
+        bufs = getattr(self._tls, "bufs", None)
+        if bufs is None:
+            bufs = self._tls.bufs = {}
+        b = bufs.get(slot)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                self.synchronize(self.thread_stream())
+                b.free()
+            b = bufs[slot] = DeviceBuffer(self, max(int(nbytes), 256))
+        return b
+
+    # -- copies --------------------------------------------------------------
+    def h2d(self, dst_ptr: int, host: np.ndarray, stream: int | None) -> None:
+        """Async copy; the host array is kept alive until the next
+        ``synchronize`` of this thread (HIP may read pageable memory late)."""
+        host = np.ascontiguousarray(host)
+        _lib.check(self.lib.pyas_memcpy_h2d(self.handle, dst_ptr, host.ctypes.data, host.nbytes, stream),
+                   "pyas_memcpy_h2d")
+        pending = getattr(self._tls, "pending", None)
+        if pending is None:
+            pending = self._tls.pending = []
+        pending.append(host)
+
+    def d2h(self, host: np.ndarray, src_ptr: int, stream: int | None) -> None:
+        assert host.flags.c_contiguous
+        _lib.check(self.lib.pyas_memcpy_d2h(self.handle, host.ctypes.data, src_ptr, host.nbytes, stream),
+                   "pyas_memcpy_d2h")
+
+    def set_tile_bytes(self, nbytes: int) -> None:
+        _lib.check(self.lib.pyas_ctx_set_tile_bytes(self.handle, int(nbytes)), "set_tile_bytes")
+
+
+def get_context(device: int = 0) -> Context:
+    with _ctx_lock:
+        c = _contexts.get(device)
+        if c is None:
+            c = _contexts[device] = Context(device)
+        return c

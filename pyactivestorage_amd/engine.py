@@ -1,0 +1,111 @@
+"""Batch engine: drives the HIP kernels over chunks already in device memory.
+
+This is the MI355X replacement for the reference's per-chunk loop
+(``activestorage/active.py:557-598``): instead of one ``reduce_chunk`` call
+per chunk on a 30-thread pool, one launch covers every chunk of a query.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .device import Context, DeviceBuffer
+from .dtypes import dtype_code, native, needs_byteswap, value_class
+from .masking import CompiledMask, table_layout
+
+_CLASS_DT = {"f": "<f8", "i": "<i8", "u": "<u8"}
+
+
+def partial_dtype(dt) -> np.dtype:
+    """Host view of ``pyas_partial`` for storage dtype dt."""
+    c = _CLASS_DT[value_class(dt)]
+    return np.dtype([("sum", c), ("count", "<i8"), ("min", c), ("max", c)])
+
+
+@dataclass
+class Layout:
+    """What every chunk of one variable shares."""
+    dtype: np.dtype
+    chunk_shape: tuple
+    shuffle: int = 0          # fused HDF5 shuffle element size (0 = none)
+
+    def batch_struct(self, n_chunks, data_ptr, offsets_ptr, sel_ptr=None, pool_ptr=None):
+        b = _lib.Batch()
+        b.dtype = dtype_code(self.dtype)
+        b.byteswap = 1 if needs_byteswap(self.dtype) else 0
+        b.shuffle = int(self.shuffle)
+        b.ndim = len(self.chunk_shape)
+        if not 1 <= b.ndim <= _lib.MAX_DIMS:
+            raise NotImplementedError(f"chunk rank {b.ndim} outside 1..{_lib.MAX_DIMS}")
+        for d, n in enumerate(self.chunk_shape):
+            b.chunk_shape[d] = int(n)
+        b.n_chunks = int(n_chunks)
+        b.data = data_ptr
+        b.offsets = offsets_ptr
+        b.sel = sel_ptr
+        b.index_pool = pool_ptr
+        return b
+
+
+class MaskUpload:
+    """Device copy of a CompiledMask's vector tables for one selected shape."""
+
+    def __init__(self, ctx: Context, cm: CompiledMask, sel_shape, kept, stream):
+        self.struct = cm.to_struct()
+        self._bufs = []
+        for k, which in ((0, "_FillValue"), (1, "missing_value")):
+            if cm.tables[k] is None:
+                continue
+            strides = table_layout(cm, k, sel_shape, "missing_value" if k == 1 else "fill")
+            lo, hi, _ = cm.tables[k]
+            nd = native(cm.dt)
+            host = np.zeros((2, lo.size), dtype=_CLASS_DT[value_class(nd)])
+            host[0] = lo
+            host[1] = hi
+            buf = DeviceBuffer(ctx, host.nbytes)
+            ctx.h2d(buf.ptr, host, stream)
+            self._bufs.append(buf)
+            self.struct.tab_len[k] = lo.size
+            self.struct.tab_lo[k] = buf.ptr
+            self.struct.tab_hi[k] = buf.ptr + lo.size * 8
+            for j, d in enumerate(kept):
+                self.struct.tab_stride[k][d] = int(strides[j])
+
+    def keepalive(self):
+        return self._bufs
+
+
+def reduce_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, chunk_out_ptr, total_ptr,
+                  round_to_var: bool, stream) -> None:
+    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
+    _lib.check(ctx.lib.pyas_reduce_chunks(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
+                                          chunk_out_ptr, total_ptr, flags, stream),
+               "pyas_reduce_chunks")
+
+
+def reduce_axes(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, axes_mask: int, out_offsets_ptr,
+                out_ptr, stream) -> None:
+    _lib.check(ctx.lib.pyas_reduce_axes(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
+                                        int(axes_mask), out_offsets_ptr, out_ptr, stream),
+               "pyas_reduce_axes")
+
+
+def select_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, out_offsets_ptr, values_ptr,
+                  mask_out_ptr, stream) -> None:
+    _lib.check(ctx.lib.pyas_select_chunks(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
+                                          out_offsets_ptr, values_ptr, mask_out_ptr, stream),
+               "pyas_select_chunks")
+
+
+def combine_partials(ctx: Context, dt, in_ptr, n, out_ptr, round_to_var: bool, stream) -> None:
+    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
+    _lib.check(ctx.lib.pyas_combine_partials(ctx.handle, dtype_code(dt), in_ptr, int(n), flags,
+                                             out_ptr, stream), "pyas_combine_partials")
+
+
+def unshuffle(ctx: Context, src_ptr, dst_ptr, nbytes, elementsize, stream) -> None:
+    _lib.check(ctx.lib.pyas_unshuffle(ctx.handle, src_ptr, dst_ptr, int(nbytes), int(elementsize),
+                                      stream), "pyas_unshuffle")
