@@ -17,6 +17,29 @@ namespace pyas {
 constexpr int kBlock = 256;   // 4 wave64 per workgroup
 constexpr int kWave = 64;
 
+// Type-generic lane exchange: moves the bits as 32-bit words (ds_swizzle /
+// DPP under the hood), so 1/2/4/8-byte values all take the same path.
+template <typename V>
+__device__ __forceinline__ V shfl_xor(V v, int m) {
+    if constexpr (sizeof(V) <= 4) {
+        uint32_t w = 0;
+        __builtin_memcpy(&w, &v, sizeof(V));
+        w = (uint32_t)__shfl_xor((int)w, m, kWave);
+        V r;
+        __builtin_memcpy(&r, &w, sizeof(V));
+        return r;
+    } else {
+        uint32_t w[2];
+        __builtin_memcpy(w, &v, 8);
+        w[0] = (uint32_t)__shfl_xor((int)w[0], m, kWave);
+        w[1] = (uint32_t)__shfl_xor((int)w[1], m, kWave);
+        V r;
+        __builtin_memcpy(&r, w, 8);
+        return r;
+    }
+}
+
+
 // ---------------------------------------------------------------------------
 // dtype traits
 // ---------------------------------------------------------------------------
@@ -209,25 +232,140 @@ template <typename T, typename C> struct AccT {
 template <typename T> using Acc = AccT<T, uint32_t>;
 template <typename T> using WAcc = AccT<T, int64_t>;
 
-// Type-generic lane exchange: moves the bits as 32-bit words (ds_swizzle /
-// DPP under the hood), so 1/2/4/8-byte values all take the same path.
-template <typename V>
-__device__ __forceinline__ V shfl_xor(V v, int m) {
-    if constexpr (sizeof(V) <= 4) {
-        uint32_t w = 0;
-        __builtin_memcpy(&w, &v, sizeof(V));
-        w = (uint32_t)__shfl_xor((int)w, m, kWave);
-        V r;
-        __builtin_memcpy(&r, &w, sizeof(V));
-        return r;
-    } else {
-        uint32_t w[2];
-        __builtin_memcpy(w, &v, 8);
-        w[0] = (uint32_t)__shfl_xor((int)w[0], m, kWave);
-        w[1] = (uint32_t)__shfl_xor((int)w[1], m, kWave);
-        V r;
-        __builtin_memcpy(&r, w, 8);
-        return r;
+// ---------------------------------------------------------------------------
+// Streaming-kernel accumulator.  Per lane: sum, NaN-free min/max (native
+// v_min/v_max; a NaN is remembered in `nan` and forces min = max = NaN at
+// the end, exactly np.ma.min/max's NaN propagation), count.  In converged
+// code (every lane runs the same trip count) counts come from a 64-lane
+// ballot popcount on the scalar unit (`ucount`, wave-uniform).
+// ---------------------------------------------------------------------------
+template <typename T> __device__ __forceinline__ T tmin(T a, T b) {
+    if constexpr (TT<T>::kind == 0) return __builtin_fmin(a, b);
+    else return b < a ? b : a;
+}
+template <> __device__ __forceinline__ float tmin<float>(float a, float b) { return __builtin_fminf(a, b); }
+template <typename T> __device__ __forceinline__ T tmax(T a, T b) {
+    if constexpr (TT<T>::kind == 0) return __builtin_fmax(a, b);
+    else return b > a ? b : a;
+}
+template <> __device__ __forceinline__ float tmax<float>(float a, float b) { return __builtin_fmaxf(a, b); }
+
+// Type used to sum one 16-byte group before widening (exact for ints: at
+// most 16 int8 / 8 int16 values; float32 groups of 4 add one f32 rounding
+// per group, far inside the 1e-6 parity bound).
+template <typename T> struct GroupSum { using type = typename TT<T>::Acc; };
+template <> struct GroupSum<float> { using type = float; };
+template <> struct GroupSum<int8_t> { using type = int32_t; };
+template <> struct GroupSum<uint8_t> { using type = uint32_t; };
+template <> struct GroupSum<int16_t> { using type = int32_t; };
+template <> struct GroupSum<uint16_t> { using type = uint32_t; };
+
+template <typename T> struct TileAcc {
+    using S = typename TT<T>::Acc;
+    S sum;
+    T mn, mx;
+    uint32_t count, ucount;
+    bool nan;
+    __device__ void init() {
+        sum = 0;
+        mn = TT<T>::highest();
+        mx = TT<T>::lowest();
+        count = 0;
+        ucount = 0;
+        nan = false;
+    }
+    // N values; CONV: all 64 lanes execute this call (uniform trip count).
+    template <int N, bool MASKED, bool CONV>
+    __device__ __forceinline__ void add_n(const T *x, const MaskT<T> &mk) {
+        using G = typename GroupSum<T>::type;
+        G g = 0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const T v = x[k];
+            if constexpr (TT<T>::kind == 0) nan |= (v != v);
+            if constexpr (MASKED) {
+                const bool ok = !mk.masked(v);
+                if constexpr (TT<T>::kind == 0) {
+                    const T y = ok ? v : (T)__builtin_nan("");  // v_min/v_max skip NaN
+                    mn = tmin(mn, y);
+                    mx = tmax(mx, y);
+                } else {
+                    mn = tmin(mn, ok ? v : TT<T>::highest());
+                    mx = tmax(mx, ok ? v : TT<T>::lowest());
+                }
+                g += ok ? (G)v : (G)0;
+                if constexpr (CONV) ucount += (uint32_t)__builtin_popcountll(__ballot(ok));
+                else count += ok ? 1u : 0u;
+            } else {
+                mn = tmin(mn, v);
+                mx = tmax(mx, v);
+                g += (G)v;
+            }
+        }
+        sum += (S)g;
+    }
+    // one element with an externally computed mask bit (generic path)
+    __device__ __forceinline__ void add_one(T v, bool is_masked) {
+        if constexpr (TT<T>::kind == 0) nan |= (v != v);
+        const bool ok = !is_masked;
+        if constexpr (TT<T>::kind == 0) {
+            const T y = ok ? v : (T)__builtin_nan("");
+            mn = tmin(mn, y);
+            mx = tmax(mx, y);
+        } else {
+            mn = tmin(mn, ok ? v : TT<T>::highest());
+            mx = tmax(mx, ok ? v : TT<T>::lowest());
+        }
+        sum += ok ? (S)v : (S)0;
+        count += ok ? 1u : 0u;
+    }
+};
+
+// Block reduction of TileAcc -> one pyas_partial (thread 0 stores).
+// `extra_count` is added once (unmasked tiles: the element count).
+template <typename T>
+__device__ void tile_finish(TileAcc<T> &a, uint64_t extra_count, pyas_partial *out) {
+    using S = typename TT<T>::Acc;
+    const int lane = threadIdx.x & (kWave - 1);
+    uint64_t c = (uint64_t)a.count + (lane == 0 ? (uint64_t)a.ucount : 0u);
+    uint32_t nan = a.nan ? 1u : 0u;
+#pragma unroll
+    for (int m = kWave / 2; m >= 1; m >>= 1) {
+        a.sum += shfl_xor(a.sum, m);
+        c += shfl_xor(c, m);
+        a.mn = tmin(a.mn, shfl_xor(a.mn, m));
+        a.mx = tmax(a.mx, shfl_xor(a.mx, m));
+        nan |= shfl_xor(nan, m);
+    }
+    __shared__ S s_sum[kBlock / kWave];
+    __shared__ uint64_t s_cnt[kBlock / kWave];
+    __shared__ T s_mn[kBlock / kWave];
+    __shared__ T s_mx[kBlock / kWave];
+    __shared__ uint32_t s_nan[kBlock / kWave];
+    const int w = threadIdx.x / kWave;
+    if (lane == 0) {
+        s_sum[w] = a.sum; s_cnt[w] = c; s_mn[w] = a.mn; s_mx[w] = a.mx; s_nan[w] = nan;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 1; k < kBlock / kWave; ++k) {
+            a.sum += s_sum[k];
+            c += s_cnt[k];
+            a.mn = tmin(a.mn, s_mn[k]);
+            a.mx = tmax(a.mx, s_mx[k]);
+            nan |= s_nan[k];
+        }
+        c += extra_count;
+        pyas_partial p;
+        TT<T>::put_acc(p.sum, a.sum);
+        p.count = (int64_t)c;
+        if constexpr (TT<T>::kind == 0) {
+            if (nan) { a.mn = (T)__builtin_nan(""); a.mx = a.mn; }
+        }
+        TT<T>::put(p.min, a.mn);
+        TT<T>::put(p.max, a.mx);
+        *out = p;
     }
 }
 

@@ -73,69 +73,105 @@ __device__ __forceinline__ void unshuffle16(const uint4 *pl, T out[16]) {
 }
 
 // Raw 16 bytes of the plain layout -> 16/ES values
-template <typename T, bool BSWAP, bool MASKED>
-__device__ __forceinline__ void consume16(const uint4 &r, Acc<T> &acc, const MaskT<T> &mk) {
+template <typename T, bool BSWAP>
+__device__ __forceinline__ void unpack16(const uint4 &r, T *x) {
     using U = typename TT<T>::U;
     constexpr int N = 16 / sizeof(T);
     U w[N];
     __builtin_memcpy(w, &r, 16);
 #pragma unroll
-    for (int k = 0; k < N; ++k) {
-        U u = w[k];
-        if (BSWAP) u = bswap(u);
-        acc.template add<MASKED>(bits_to<T>(u), mk);
-    }
+    for (int k = 0; k < N; ++k) x[k] = bits_to<T>(BSWAP ? bswap(w[k]) : w[k]);
+}
+
+template <typename T, bool BSWAP, bool MASKED, bool CONV>
+__device__ __forceinline__ void consume16(const uint4 &r, TileAcc<T> &acc, const MaskT<T> &mk) {
+    constexpr int N = 16 / sizeof(T);
+    T x[N];
+    unpack16<T, BSWAP>(r, x);
+    acc.template add_n<N, MASKED, CONV>(x, mk);
 }
 
 // ---------------------------------------------------------------------------
 // contiguous runs
 // ---------------------------------------------------------------------------
-// Plain layout, memory elements [m0, m1) of the chunk at `base`.
+// Plain layout, memory elements [m0, m1) of the chunk at `base`.  The body is
+// 16-B global loads, U per lane per step, register double-buffered so the
+// next step's loads are in flight while the current step is reduced.
 template <typename T, bool BSWAP, bool MASKED>
-__device__ void run_plain(const uint8_t *base, int64_t m0, int64_t m1, Acc<T> &acc,
+__device__ void run_plain(const uint8_t *base, int64_t m0, int64_t m1, TileAcc<T> &acc,
                           const MaskT<T> &mk) {
     constexpr int ES = sizeof(T);
     const int tid = threadIdx.x;
-    const uintptr_t p0 = (uintptr_t)(base + m0 * ES), p1 = (uintptr_t)(base + m1 * ES);
-    const uintptr_t a0 = (p0 + 15) & ~(uintptr_t)15, a1 = p1 & ~(uintptr_t)15;
+    const int64_t b0 = m0 * ES, b1 = m1 * ES;               // byte range in the chunk
+    const int64_t mis = (int64_t)((uintptr_t)base & 15);
+    const int64_t a0 = ((b0 + mis + 15) & ~(int64_t)15) - mis;  // first 16-B aligned byte
+    const int64_t a1 = ((b1 + mis) & ~(int64_t)15) - mis;
     if (a0 >= a1) {
-        for (int64_t i = m0 + tid; i < m1; i += kBlock)
-            acc.template add<MASKED>(load_plain<T, BSWAP>(base, i), mk);
+        for (int64_t i = m0 + tid; i < m1; i += kBlock) {
+            const T v = load_plain<T, BSWAP>(base, i);
+            acc.template add_n<1, MASKED, false>(&v, mk);
+        }
+        if (!MASKED) {} // counts of unmasked tiles are added by the caller
         return;
     }
-    const int64_t nhead = (int64_t)(a0 - p0) / ES, ntail = (int64_t)(p1 - a1) / ES;
-    if (tid < nhead) acc.template add<MASKED>(load_plain<T, BSWAP>(base, m0 + tid), mk);
-    if (tid < ntail) acc.template add<MASKED>(load_plain<T, BSWAP>(base, m1 - ntail + tid), mk);
-    const uint4 *v = reinterpret_cast<const uint4 *>(a0);
-    const int64_t nvec = (int64_t)(a1 - a0) / 16;
-    constexpr int U = 4;
-    const int64_t nfull = nvec / (U * kBlock) * (U * kBlock);
-    for (int64_t k = tid; k < nfull; k += U * kBlock) {
-        uint4 r[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) r[u] = v[k + u * kBlock];
-#pragma unroll
-        for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED>(r[u], acc, mk);
+    const int64_t nhead = (a0 - b0) / ES, ntail = (b1 - a1) / ES;
+    if (tid < nhead) {
+        const T v = load_plain<T, BSWAP>(base, m0 + tid);
+        acc.template add_n<1, MASKED, false>(&v, mk);
     }
-    for (int64_t k = nfull + tid; k < nvec; k += kBlock) consume16<T, BSWAP, MASKED>(v[k], acc, mk);
+    if (tid < ntail) {
+        const T v = load_plain<T, BSWAP>(base, m1 - ntail + tid);
+        acc.template add_n<1, MASKED, false>(&v, mk);
+    }
+    const uint4 *v = reinterpret_cast<const uint4 *>(base + a0);  // keeps global provenance
+    const int64_t nvec = (a1 - a0) / 16;
+    constexpr int U = 4;
+    constexpr int64_t STEP = (int64_t)U * kBlock;
+    const int64_t nsteps = nvec / STEP;
+    if (nsteps > 0) {
+        uint4 cur[U], nxt[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = v[tid + u * kBlock];
+        for (int64_t s = 0; s < nsteps; ++s) {
+            // prefetch the next step (clamped: the last step re-reads itself)
+            const int64_t ns = s + 1 < nsteps ? s + 1 : s;
+#pragma unroll
+            for (int u = 0; u < U; ++u) nxt[u] = v[ns * STEP + tid + u * kBlock];
+#pragma unroll
+            for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED, true>(cur[u], acc, mk);
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+    }
+    for (int64_t k = nsteps * STEP + tid; k < nvec; k += kBlock)
+        consume16<T, BSWAP, MASKED, false>(v[k], acc, mk);
 }
 
 // Shuffled layout, chunk elements [i0, i1); n = elements in the chunk.
 template <typename T, bool BSWAP, bool MASKED>
 __device__ void run_shuffled(const uint8_t *base, int64_t n, int64_t i0, int64_t i1,
-                             Acc<T> &acc, const MaskT<T> &mk) {
+                             TileAcc<T> &acc, const MaskT<T> &mk) {
     constexpr int ES = sizeof(T);
     const int tid = threadIdx.x;
     const bool vec_ok = (((uintptr_t)base & 15) == 0) && ((n & 15) == 0);
-    int64_t g0 = (i0 + 15) & ~(int64_t)15, g1 = i1 & ~(int64_t)15;
+    const int64_t g0 = (i0 + 15) & ~(int64_t)15, g1 = i1 & ~(int64_t)15;
     if (!vec_ok || g0 >= g1) {
-        for (int64_t i = i0 + tid; i < i1; i += kBlock)
-            acc.template add<MASKED>(load_shuffled<T, BSWAP>(base, n, i), mk);
+        for (int64_t i = i0 + tid; i < i1; i += kBlock) {
+            const T v = load_shuffled<T, BSWAP>(base, n, i);
+            acc.template add_n<1, MASKED, false>(&v, mk);
+        }
         return;
     }
-    if (tid < g0 - i0) acc.template add<MASKED>(load_shuffled<T, BSWAP>(base, n, i0 + tid), mk);
-    if (tid < i1 - g1) acc.template add<MASKED>(load_shuffled<T, BSWAP>(base, n, g1 + tid), mk);
+    if (tid < g0 - i0) {
+        const T v = load_shuffled<T, BSWAP>(base, n, i0 + tid);
+        acc.template add_n<1, MASKED, false>(&v, mk);
+    }
+    if (tid < i1 - g1) {
+        const T v = load_shuffled<T, BSWAP>(base, n, g1 + tid);
+        acc.template add_n<1, MASKED, false>(&v, mk);
+    }
     const int64_t ng = (g1 - g0) / 16;
+    const int64_t nfull = ng / kBlock * kBlock;
     for (int64_t g = tid; g < ng; g += kBlock) {
         const int64_t i = g0 + g * 16;
         uint4 pl[ES];
@@ -143,8 +179,8 @@ __device__ void run_shuffled(const uint8_t *base, int64_t n, int64_t i0, int64_t
         for (int b = 0; b < ES; ++b) pl[b] = *reinterpret_cast<const uint4 *>(base + (int64_t)b * n + i);
         T x[16];
         unshuffle16<T, BSWAP>(pl, x);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) acc.template add<MASKED>(x[k], mk);
+        if (g < nfull) acc.template add_n<16, MASKED, false>(x, mk);
+        else acc.template add_n<16, MASKED, false>(x, mk);
     }
 }
 
@@ -184,14 +220,13 @@ __device__ __forceinline__ bool all_masked(const MaskT<T> &mk, const MaskTab &ta
 
 template <typename T, bool SHUF, bool BSWAP, bool MASKED>
 __device__ void run_generic(const ReduceArgs &a, const uint8_t *base, const Sel &s, int64_t e0,
-                            int64_t e1, Acc<T> &acc, const MaskT<T> &mk) {
+                            int64_t e1, TileAcc<T> &acc, const MaskT<T> &mk) {
     const uint32_t all = (1u << a.ndim) - 1u;
     for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
         Decomp o{0, {0, 0}};
         decompose(s, a.pool, a.cstride, a.tab, a.ndim, all, e, o);
         const T x = load_elem<T, SHUF, BSWAP>(base, a.chunk_elems, o.mem);
-        if constexpr (MASKED) acc.add_flag(x, all_masked(mk, a.tab, o, x));
-        else acc.add_valid(x);
+        acc.add_one(x, MASKED ? all_masked(mk, a.tab, o, x) : false);
     }
 }
 
@@ -206,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     const uint8_t *base = a.data + a.offsets[c];
     MaskT<T> mk;
     if constexpr (MASKED) mk.init(a.mask);
-    Acc<T> acc;
+    TileAcc<T> acc;
     acc.init();
     Sel s;
     load_sel(s, a.sel, c, a.ndim, a.shape);
@@ -216,6 +251,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     int64_t per = (total + a.tpc - 1) / a.tpc;
     per = (per + 63) & ~(int64_t)63;
     const int64_t e0 = t * per, e1 = e0 + per < total ? e0 + per : total;
+    bool generic = false;
     if (e0 < e1) {
         // Is the selection one contiguous run of chunk memory?  (innermost
         // non-full dim has unit step; every dim outside it picks one index)
@@ -241,11 +277,13 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
             else
                 run_plain<T, BSWAP, MASKED>(base, m0 + e0, m0 + e1, acc, mk);
         } else {
+            generic = true;
             run_generic<T, SHUF, BSWAP, MASKED>(a, base, s, e0, e1, acc, mk);
         }
     }
-    block_reduce(acc);
-    if (threadIdx.x == 0) store_partial(a.out + b, acc);
+    // unmasked contiguous tiles count every element; the generic path counts itself
+    const uint64_t extra = (!MASKED && !generic && e0 < e1) ? (uint64_t)(e1 - e0) : 0u;
+    tile_finish(acc, extra, a.out + b);
 }
 
 // ---------------------------------------------------------------------------
