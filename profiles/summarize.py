@@ -1,0 +1,87 @@
+"""Summarise rocprofv3 CSV output into committed evidence.
+
+    python profiles/summarize.py --trace DIR/run_kernel_stats.csv \
+        --pmc DIR/run_counter_collection.csv --config c3 --bytes 4294967296 \
+        --out profiles/r01_c3_summary.json [--traffic profiles/traffic.json]
+
+* kernel stats: average duration of every pyas kernel (ns) from
+  ``--kernel-trace --stats``;
+* HBM traffic: FETCH_SIZE (KiB) of each ``pyas::k_reduce`` dispatch from a
+  separate ``--pmc FETCH_SIZE`` pass, corrected per MI355X_MICROARCH.md §HBM:
+  on gfx950 FETCH_SIZE reports exactly half of the bytes of a wide coalesced
+  streaming read (16 B/lane global_load), so bytes = FETCH_SIZE * 1024 * 2.
+"""
+import argparse
+import csv
+import json
+import statistics
+
+
+def kernel_stats(path):
+    out = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            name = row["Name"]
+            if "pyas::" not in name:
+                continue
+            out[name] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
+                         "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"]),
+                         "pct": float(row["Percentage"])}
+    return out
+
+
+def pmc(path, counter="FETCH_SIZE", kernel="pyas::k_reduce"):
+    vals, durs = [], []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                vals.append(float(row["Counter_Value"]))
+                durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    return vals, durs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace")
+    ap.add_argument("--pmc")
+    ap.add_argument("--pmc-write")
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--bytes", type=int, required=True, help="algorithmic bytes per k_reduce launch")
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--traffic")
+    a = ap.parse_args()
+    summary = {"config": a.config, "algorithmic_bytes_per_launch": a.bytes}
+    if a.trace:
+        ks = kernel_stats(a.trace)
+        summary["kernels"] = ks
+        red = [v for k, v in ks.items() if "k_reduce<" in k]
+        if red:
+            avg = sum(v["avg_ns"] * v["calls"] for v in red) / sum(v["calls"] for v in red)
+            summary["k_reduce_avg_ns"] = avg
+            summary["k_reduce_achieved_GBps"] = a.bytes / avg
+    if a.pmc:
+        vals, durs = pmc(a.pmc)
+        if vals:
+            kib = statistics.median(vals)
+            hbm = kib * 1024 * 2
+            summary["pmc"] = {"counter": "FETCH_SIZE", "dispatches": len(vals), "median_kib": kib,
+                              "correction": "x2 (gfx950 FETCH_SIZE counts half of 16B/lane streams)",
+                              "hbm_read_bytes_per_launch": hbm,
+                              "ratio_to_algorithmic": hbm / a.bytes}
+    if a.pmc_write:
+        vals, _ = pmc(a.pmc_write, counter="WRITE_SIZE")
+        if vals:
+            summary.setdefault("pmc", {})["write_bytes_per_launch"] = statistics.median(vals) * 1024
+    with open(a.out, "w") as f:
+        json.dump(summary, f, indent=1)
+    if a.traffic and "pmc" in summary:
+        with open(a.traffic, "w") as f:
+            json.dump({"config": a.config,
+                       "hbm_bytes_per_launch": summary["pmc"]["hbm_read_bytes_per_launch"]
+                       + summary["pmc"].get("write_bytes_per_launch", 0.0),
+                       "source": a.out}, f, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+"""Loader for the golden vectors produced by tests/golden/make_golden.py
+(outputs of the reference's own storage.py) and tests/golden/extract_h5.py
+(libhdf5's own decode of the reference's test files)."""
+import functools
+import json
+import os
+
+import numpy as np
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+METHODS = {"ma.sum": np.ma.sum, "ma.min": np.ma.min, "ma.max": np.ma.max, "ma.mean": np.ma.mean,
+           "sum": np.sum, "min": np.min, "max": np.max, "mean": np.mean, "none": None}
+
+
+def dec_value(e):
+    if e is None:
+        return None
+    k = e["kind"]
+    if k == "ndarray":
+        return np.array(e["v"], dtype=e["dtype"]).reshape(e["shape"])
+    if k == "list":
+        return list(e["v"])
+    if k == "np":
+        return np.dtype(e["dtype"]).type(e["v"])
+    if k == "int":
+        return int(e["v"])
+    return float(e["v"])
+
+
+def dec_sel(e):
+    def one(d):
+        if "slice" in d:
+            return slice(*d["slice"])
+        if "ellipsis" in d:
+            return Ellipsis
+        if "list" in d:
+            return list(d["list"])
+        return d["int"]
+    if "tuple" in e:
+        return tuple(one(d) for d in e["tuple"])
+    return one(e)
+
+
+@functools.lru_cache(maxsize=1)
+def cases():
+    with open(os.path.join(HERE, "reference_cases.json")) as f:
+        return json.load(f)["cases"]
+
+
+@functools.lru_cache(maxsize=1)
+def arrays():
+    return dict(np.load(os.path.join(HERE, "reference_outputs.npz")))
+
+
+@functools.lru_cache(maxsize=1)
+def h5_meta():
+    with open(os.path.join(HERE, "h5_vars.json")) as f:
+        return json.load(f)
+
+
+@functools.lru_cache(maxsize=1)
+def h5_blobs():
+    return dict(np.load(os.path.join(HERE, "h5_chunks.npz")))
+
+
+def args_of(i, zlib_cls, shuffle_cls):
+    """Replay arguments of golden case i for a reduce_chunk_bytes-like call."""
+    c = cases()[i]
+    raw = arrays()[c["input"]].tobytes()
+    comp = zlib_cls() if c["codecs"].get("zlib") else None
+    filters = [shuffle_cls(c["codecs"]["shuffle"])] if c["codecs"].get("shuffle") else None
+    missing = tuple(dec_value(v) for v in c["missing"])
+    axis = tuple(c["axis"]) if c["axis"] is not None else None
+    return dict(raw=raw, compression=comp, filters=filters, missing=missing, dtype=c["dtype"],
+                shape=tuple(c["shape"]), order=c["order"], chunk_selection=dec_sel(c["sel"]),
+                axis=axis, method=METHODS[c["method"]])
+
+
+def expected(i):
+    """(expect-dict, data, mask, count) of golden case i (or raises name)."""
+    c = cases()[i]
+    if "raises" in c:
+        return c["raises"], None, None, None
+    a = arrays()
+    return c["expect"], a[f"data{i}"], a[f"mask{i}"], a.get(f"count{i}")
+
+
+def check(i, tmp, n, rel=1e-6):
+    """Assert (tmp, n) reproduces golden case i.  Float sums/means: rel
+    tolerance (or scaled by sum |x| via rel*... not needed: exact when the
+    computation is the oracle's own NumPy)."""
+    exp, data, mask, count = expected(i)
+    assert type(tmp).__name__ == exp["type"], (i, type(tmp), exp)
+    assert np.asarray(tmp).dtype.str == exp["dtype"] or np.dtype(exp["dtype"]) == tmp.dtype, (i, tmp.dtype, exp)
+    assert list(np.shape(tmp)) == exp["shape"], (i, np.shape(tmp), exp)
+    if exp["type"] == "MaskedArray":
+        assert (np.ma.getmask(tmp) is np.ma.nomask) == exp["nomask"], (i, "nomask", exp)
+    gm = np.ma.getmaskarray(tmp)
+    assert np.array_equal(gm, mask), (i, gm, mask)
+    gd = np.asarray(np.ma.getdata(tmp))[~mask]
+    wd = data[~mask]
+    if wd.dtype.kind == "f" and rel:
+        w, g = wd.astype(np.float64), gd.astype(np.float64)
+        ok = (np.isnan(w) & np.isnan(g)) | (w == g) | (np.abs(w - g) <= rel * np.abs(w))
+        assert ok.all(), (i, gd, wd)
+    else:
+        assert np.array_equal(gd, wd, equal_nan=wd.dtype.kind == "f"), (i, gd, wd)
+    if count is None:
+        assert n is None, i
+    else:
+        assert n.dtype == count.dtype and np.array_equal(n, count), (i, n, count)

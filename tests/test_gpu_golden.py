@@ -1,0 +1,55 @@
+"""GPU path vs the reference's own outputs (golden vectors).
+
+Every case of tests/golden/reference_cases.json — produced by running the
+reference's ``activestorage/storage.py`` on the reference's own test inputs
+(cesm2/daily_data/zero_chunked byte ranges of tests/unit/test_storage.py,
+every chunk of test1.nc with zlib+shuffle, cesm2 chunks) and on a synthetic
+sweep — is replayed through the HIP drop-in ``reduce_chunk_bytes``.  Same
+container type, dtype, shape, nomask-ness, mask and count; values bit-exact
+except float sums/means (<= 1e-6 relative).  Cases where the reference
+raises must raise the same exception type.
+"""
+import numpy as np
+import pytest
+
+from pyactivestorage_amd import storage as pas
+from tests import _golden as G
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("block", range(0, 3205, 400))
+def test_gpu_reproduces_reference_outputs(gpu, block):
+    cases = G.cases()
+    for i in range(block, min(block + 400, len(cases))):
+        a = G.args_of(i, pas.Zlib, pas.Shuffle)
+        exp = G.expected(i)
+        call = lambda: pas.reduce_chunk_bytes(a["raw"], a["compression"], a["filters"], a["missing"],  # noqa
+                                              a["dtype"], a["shape"], a["order"], a["chunk_selection"],
+                                              a["axis"], a["method"])
+        if isinstance(exp[0], str):
+            with pytest.raises(Exception) as ei:
+                call()
+            assert type(ei.value).__name__ == exp[0], (i, G.cases()[i], ei.value)
+            continue
+        tmp, n = call()
+        # float sums of signed data can cancel: allow 4e-7 * sum|x| like tests/_compare.py
+        try:
+            G.check(i, tmp, n, rel=1e-6)
+        except AssertionError:
+            c = G.cases()[i]
+            if c["method"] not in ("ma.sum", "sum", "ma.mean", "mean"):
+                raise
+            sel, _ = pas.reduce_chunk_bytes(a["raw"], a["compression"], a["filters"], a["missing"],
+                                            a["dtype"], a["shape"], a["order"], a["chunk_selection"],
+                                            None, None)
+            with np.errstate(all="ignore"):
+                scale = np.ma.sum(np.abs(np.ma.asarray(sel).astype(np.float64)), axis=a["axis"],
+                                  keepdims=True)
+            _, data, mask, count = G.expected(i)
+            g = np.asarray(np.ma.getdata(tmp), dtype=np.float64)[~mask]
+            w = data.astype(np.float64)[~mask]
+            s = np.broadcast_to(np.ma.filled(scale, 0), mask.shape)[~mask]
+            ok = (np.isnan(g) & np.isnan(w)) | (np.abs(g - w) <= np.maximum(1e-6 * np.abs(w), 4e-7 * s))
+            assert ok.all(), (i, g, w)
+            assert np.array_equal(np.ma.getmaskarray(tmp), mask) and np.array_equal(n, count), i
