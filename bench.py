@@ -38,8 +38,8 @@ CONFIGS = {
     "c4": dict(shape=(2048, 2048, 2048), chunks=(128, 128, 128), dtype="f4", shuffle=True,
                masked=True, hyperslab=None, desc="2048^3 f32, 128^3 chunks, shuffle + mask, sum"),
     "c5": dict(shape=(4096, 2048, 1024), chunks=(32, 32, 32), dtype="f8", shuffle=False,
-               masked=True, hyperslab=((16, 4080), (16, 2032), (16, 1008)),
-               desc="4096x2048x1024 f64, 32^3 chunks, hyperslab, masked mean"),
+               masked=True, hyperslab=16,
+               desc="4096x2048x1024 f64, 32^3 chunks, hyperslab [16:-16]^3, masked mean"),
 }
 FILL = -999.0
 VMIN = 1000.0
@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--tile-bytes", type=int, default=0)
+    p.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                   help="weak: each GPU adds its own slab of the variable (dim 0); "
+                        "strong: one variable of the config's shape split across GPUs")
     p.add_argument("--cpu-chunks", type=int, default=1024,
                    help="chunks in the CPU-baseline sample (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=30)
@@ -60,24 +63,27 @@ def parse():
     return p.parse_args()
 
 
-def chunk_selections(cfg, rank_origin):
-    """Per-chunk hyperslab selections for c5 (None = all chunks full)."""
-    hs = cfg["hyperslab"]
-    if hs is None:
-        return None
-    from pyactivestorage_amd import selection
-    shape, chunks = cfg["shape"], cfg["chunks"]
-    grid = [-(-s // c) for s, c in zip(shape, chunks)]
-    sels = []
-    for ci in np.ndindex(*grid):
-        dims = []
-        for d, c in enumerate(ci):
-            lo = max(hs[d][0] - c * chunks[d], 0)
-            hi = min(hs[d][1] - c * chunks[d], chunks[d])
-            cnt = max(hi - lo, 0)
-            dims.append(selection.DimSel(lo if cnt else 0, 1, cnt, False))
-        sels.append(selection.ChunkSel(dims, tuple(d.count for d in dims), (0, 1, 2)))
-    return sels
+def chunk_selections(cfg, gshape, lo, hi):
+    """Selection table (ABI layout, int32 [n, MAX_DIMS, 3]) of chunks [lo, hi)
+    for configs with a hyperslab (margin m selects [m:-m] in every dim), and
+    the selected elements per chunk.  None = every chunk fully selected."""
+    m = cfg["hyperslab"]
+    chunks = np.array(cfg["chunks"], dtype=np.int64)
+    if m is None:
+        return None, np.full(hi - lo, int(np.prod(chunks)), dtype=np.int64)
+    from pyactivestorage_amd import _lib
+    grid = np.array(gshape, dtype=np.int64) // chunks
+    cid = np.arange(lo, hi, dtype=np.int64)
+    ci = np.stack(np.unravel_index(cid, tuple(grid)), axis=1)          # (n, 3)
+    start = np.maximum(m - ci * chunks, 0)
+    stop = np.minimum(np.array(gshape) - m - ci * chunks, chunks)
+    cnt = np.maximum(stop - start, 0)
+    table = np.zeros((hi - lo, _lib.MAX_DIMS, 3), dtype=np.int32)
+    table[:, :, 1] = 1
+    table[:, :, 2] = 1
+    table[:, :3, 0] = np.where(cnt > 0, start, 0)
+    table[:, :3, 2] = cnt
+    return table, cnt.prod(axis=1)
 
 
 def cpu_baseline(cfg, host_chunks: np.ndarray, n_chunks: int, missing, threads: int):
@@ -133,6 +139,7 @@ def main():
 
     from pyactivestorage_amd import _lib, engine
     from pyactivestorage_amd.batch import ReductionPlan
+    from pyactivestorage_amd.distributed import reduce_sharded
     from pyactivestorage_amd.device import get_context
     from pyactivestorage_amd.synthetic import chunk_major_device
 
@@ -143,36 +150,46 @@ def main():
         ctx.set_tile_bytes(args.tile_bytes)
     stream = torch.cuda.current_stream().cuda_stream
 
-    # weak scaling: each rank owns its own slab of the variable (dim 0)
-    origin = (rank * cfg["shape"][0], 0, 0)
+    # the variable: weak scaling grows it along dim 0 with the GPU count
+    gshape = list(cfg["shape"])
+    if args.scaling == "weak":
+        gshape[0] *= world
+    gshape = tuple(gshape)
+    grid = [s // c for s, c in zip(gshape, cfg["chunks"])]
+    n_all = int(np.prod(grid))
+    _, weights = chunk_selections(cfg, gshape, 0, n_all)
+    from pyactivestorage_amd.distributed import shard_ranges
+    lo, hi = shard_ranges(weights, world)[rank]
     data, offsets, n_fill = chunk_major_device(
-        torch, cfg["shape"], cfg["chunks"], dt, dev, origin=origin,
-        n_formula=cfg["shape"][0] * world,
+        torch, gshape, cfg["chunks"], dt, dev, chunk_range=(lo, hi),
         fill=FILL if cfg["masked"] else None, fill_frac=0.01 if cfg["masked"] else 0.0,
         seed=rank, shuffle=cfg["shuffle"])
     torch.cuda.synchronize()
     missing = ((dt.type(FILL), None, dt.type(VMIN), dt.type(VMAX)) if cfg["masked"]
                else (None, None, None, None))
-    sels = chunk_selections(cfg, origin)
+    sels, counts = chunk_selections(cfg, gshape, lo, hi)
     plan = ReductionPlan(ctx, dt, cfg["chunks"], data.data_ptr(), offsets,
-                         shuffle=dt.itemsize if cfg["shuffle"] else 0, selections=sels,
+                         shuffle=dt.itemsize if cfg["shuffle"] else 0, sel_table=sels,
                          missing=missing, round_to_var=True, stream=stream)
     n_chunks = plan.n_chunks
-    sel_elems = (n_chunks * int(np.prod(cfg["chunks"])) if sels is None
-                 else sum(s.n_selected for s in sels))
+    sel_elems = int(counts.sum())
     bytes_per_launch = sel_elems * dt.itemsize
+    check = None
+    if not cfg["shuffle"] and sels is None:
+        # independent device check of the unmasked count with plain torch ops
+        tdt = torch.float32 if dt.itemsize == 4 else torch.float64
+        v = data[: bytes_per_launch].view(tdt)
+        ok = (v != FILL) & (v >= VMIN) & (v <= VMAX) if cfg["masked"] else torch.ones_like(v, dtype=torch.bool)
+        check = {"torch_count": int(ok.sum().item())}
+        del v, ok
 
-    gathered = torch.zeros(world * _lib.PARTIAL_NBYTES, dtype=torch.uint8, device=dev)
     final = torch.zeros(_lib.PARTIAL_NBYTES, dtype=torch.uint8, device=dev)
-    # zero-copy torch view of the plan's 32-byte device total, for RCCL
-    total_t = _tensor_from_ptr(torch, plan.total.ptr, _lib.PARTIAL_NBYTES, dev)
 
     def step():
-        plan.launch(stream, chunk_partials=False)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, total_t)
-            engine.combine_partials(ctx, dt, gathered.data_ptr(), world, final.data_ptr(), False,
-                                    stream)
+            reduce_sharded(torch, plan, ctx, stream, final)
+        else:
+            plan.launch(stream, chunk_partials=False)
 
     for _ in range(args.warmup):
         step()
@@ -200,19 +217,27 @@ def main():
     else:
         kern_ms_max = kern_ms
 
-    # result check against an independent torch computation on the device
     tot = plan.read_total(stream)[0]
-    result = {"sum": float(tot["sum"]), "count": int(tot["count"]), "min": float(tot["min"]),
-              "max": float(tot["max"])}
+    local = {"sum": float(tot["sum"]), "count": int(tot["count"]), "min": float(tot["min"]),
+             "max": float(tot["max"])}
+    if check is not None:
+        check["kernel_count"] = local["count"]
+        check["ok"] = check["torch_count"] == local["count"]
+    result = local
     if world > 1:
         fin = np.frombuffer(final.cpu().numpy().tobytes(), dtype=engine.partial_dtype(dt))[0]
         result = {"sum": float(fin["sum"]), "count": int(fin["count"]), "min": float(fin["min"]),
                   "max": float(fin["max"])}
 
     ms_per_step = elapsed / args.steps * 1e3
-    total_bytes = bytes_per_launch * world
+    if world > 1:
+        agg = torch.tensor([bytes_per_launch, n_chunks], dtype=torch.float64, device=dev)
+        dist.all_reduce(agg)
+        total_bytes, total_chunks = float(agg[0]), float(agg[1])
+    else:
+        total_bytes, total_chunks = float(bytes_per_launch), float(n_chunks)
     value = total_bytes / (elapsed / args.steps) / 1e9
-    chunks_per_s = n_chunks * world / (elapsed / args.steps)
+    chunks_per_s = total_chunks / (elapsed / args.steps)
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = None
     try:
@@ -242,11 +267,11 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": "f64" if dt.itemsize == 8 else "f32", "data": "synthetic",
-            "config": {"workload": f"{args.config}: {cfg['desc']}", "variable_per_gpu": list(cfg["shape"]),
-                       "chunk_shape": list(cfg["chunks"]), "chunks_per_gpu": n_chunks,
-                       "bytes_per_gpu": bytes_per_launch, "parallelism": f"chunk-shard x{world}",
+            "config": {"workload": f"{args.config}: {cfg['desc']}", "variable": list(gshape),
+                       "chunk_shape": list(cfg["chunks"]), "chunks_rank0": n_chunks,
+                       "bytes_rank0": bytes_per_launch, "parallelism": f"chunk-shard x{world}",
                        "methods": "sum,count,min,max in one pass (mean = sum/count)"},
             "chunks_per_s": round(chunks_per_s, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -255,20 +280,12 @@ def main():
                          "kernel_ms_avg": round(kern_ms, 5), "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                          "bytes_per_launch": bytes_per_launch},
             "cpu_baseline": cpu,
-            "result": result,
+            "result": result, "check": check,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-
-
-def _tensor_from_ptr(torch, ptr, nbytes, dev):
-    """Zero-copy torch view of a device allocation made by the C library."""
-    class _Holder:
-        __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
-                                    "version": 3, "strides": None}
-    return torch.as_tensor(_Holder(), device=dev)
 
 
 if __name__ == "__main__":

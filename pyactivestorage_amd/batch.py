@@ -37,7 +37,8 @@ class ReductionPlan:
     """
 
     def __init__(self, ctx: Context, dtype, chunk_shape, data_ptr, offsets, *, shuffle=0,
-                 selections=None, missing=None, round_to_var=True, stream=None):
+                 selections=None, sel_table=None, index_pool=None, missing=None,
+                 round_to_var=True, stream=None):
         self.ctx = ctx
         self.dtype = np.dtype(dtype)
         self.chunk_shape = tuple(int(s) for s in chunk_shape)
@@ -57,6 +58,7 @@ class ReductionPlan:
             if len(selections) != self.n_chunks:
                 raise ValueError("one selection per chunk is required")
             table, pool = selection.pack(selections, len(self.chunk_shape))
+            _check_table(table, self.chunk_shape, pool)
             sel_ptr = self._upload(table, st).ptr
             pool_ptr = self._upload(pool, st).ptr
             shapes = {s.shape for s in selections}
@@ -64,6 +66,17 @@ class ReductionPlan:
                 raise NotImplementedError("vector fill/missing values need equal selection shapes")
             if selections:
                 sel_shape, kept = selections[0].shape, selections[0].kept
+        elif sel_table is not None:
+            # pre-packed ABI table (int32 [n, MAX_DIMS, 3]) for large planned queries
+            table = np.ascontiguousarray(sel_table, dtype=np.int32)
+            if table.shape != (self.n_chunks, _lib.MAX_DIMS, 3):
+                raise ValueError("sel_table must have shape (n_chunks, MAX_DIMS, 3)")
+            _check_table(table, self.chunk_shape, index_pool)
+            if self.cm.tables[0] is not None or self.cm.tables[1] is not None:
+                raise NotImplementedError("vector fill/missing values need ChunkSel selections")
+            sel_ptr = self._upload(table, st).ptr
+            pool_ptr = self._upload(index_pool if index_pool is not None
+                                    else np.zeros(1, dtype=np.int32), st).ptr
         self.layout = engine.Layout(self.dtype, self.chunk_shape,
                                     shuffle if (shuffle and shuffle > 1 and es > 1) else 0)
         self.batch = self.layout.batch_struct(self.n_chunks, data_ptr, self.offsets_buf.ptr,
@@ -88,6 +101,15 @@ class ReductionPlan:
                              self.chunk_partials.ptr if chunk_partials else None, self.total.ptr,
                              self.round_to_var, stream)
 
+    def total_tensor(self, torch):
+        """Zero-copy torch view (32 uint8) of the device total, e.g. to hand
+        it to torch.distributed (RCCL) without a copy."""
+        t = getattr(self, "_total_t", None)
+        if t is None:
+            t = self._total_t = device_tensor(torch, self.total.ptr, _lib.PARTIAL_NBYTES,
+                                              self.ctx.device)
+        return t
+
     def read_total(self, stream=None) -> np.ndarray:
         host = np.zeros(1, dtype=engine.partial_dtype(self.dtype))
         self.ctx.d2h(host, self.total.ptr, stream)
@@ -100,6 +122,45 @@ class ReductionPlan:
             self.ctx.d2h(host, self.chunk_partials.ptr, stream)
         self.ctx.synchronize(stream)
         return host
+
+
+def _check_table(table, chunk_shape, pool):
+    """Host bounds check of a packed selection table, so the device never
+    reads outside a chunk (the C ABI trusts its caller)."""
+    nd = len(chunk_shape)
+    shape = np.array(chunk_shape + (1,) * (_lib.MAX_DIMS - nd), dtype=np.int64)
+    start = table[:, :, 0].astype(np.int64)
+    step = table[:, :, 1].astype(np.int64)
+    cnt = table[:, :, 2].astype(np.int64)
+    if (cnt < 0).any():
+        raise ValueError("negative selection count")
+    sl = (step != 0) & (cnt > 0)
+    last = start + (cnt - 1) * step
+    bad = sl & ((start < 0) | (start >= shape) | (last < 0) | (last >= shape))
+    if bad.any():
+        raise IndexError("selection table reaches outside the chunk")
+    lst = (step == 0) & (cnt > 0)
+    if lst.any():
+        if pool is None:
+            raise ValueError("listed selections need an index pool")
+        pool = np.asarray(pool, dtype=np.int64)
+        ends = start + cnt
+        if (start[lst] < 0).any() or (ends[lst] > pool.size).any():
+            raise IndexError("index pool reference out of range")
+        dims = np.nonzero(lst)
+        for c, d in zip(*dims):
+            seg = pool[start[c, d]: start[c, d] + cnt[c, d]]
+            if (seg < 0).any() or (seg >= shape[d]).any():
+                raise IndexError("listed index outside the chunk")
+
+
+def device_tensor(torch, ptr, nbytes, device):
+    """Zero-copy uint8 torch tensor over a device allocation made by the C
+    library (``__cuda_array_interface__``)."""
+    class _Holder:
+        __cuda_array_interface__ = {"shape": (int(nbytes),), "typestr": "|u1", "data": (int(ptr), False),
+                                    "version": 3, "strides": None}
+    return torch.as_tensor(_Holder(), device=torch.device("cuda", device))
 
 
 def finalize(total: np.ndarray, method: str, dtype, components=False, ndim=1, masked=None):

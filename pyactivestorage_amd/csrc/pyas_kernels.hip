@@ -218,22 +218,124 @@ __device__ __forceinline__ bool all_masked(const MaskT<T> &mk, const MaskTab &ta
     return m;
 }
 
+// Mixed-radix position counter over the selected box (innermost dim
+// fastest).  Divisions happen once per thread; every step of `stride`
+// elements is then a carry-propagating add per dim (no division).
+struct RadixCounter {
+    uint32_t idx[PYAS_MAX_DIMS], inc[PYAS_MAX_DIMS], cnt[PYAS_MAX_DIMS];
+    __device__ __forceinline__ void init(const Sel &s, int ndim, uint32_t dmask, uint64_t start,
+                                         uint64_t stride) {
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            const bool on = d < ndim && ((dmask >> d) & 1u);
+            const uint32_t c = on ? (uint32_t)s.cnt[d] : 1u;
+            cnt[d] = c;
+            idx[d] = (uint32_t)(start % c);
+            start /= c;
+            inc[d] = (uint32_t)(stride % c);
+            stride /= c;
+        }
+    }
+    __device__ __forceinline__ void advance() {
+        uint32_t carry = 0;
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            const uint32_t x = idx[d] + inc[d] + carry;
+            carry = x >= cnt[d] ? 1u : 0u;
+            idx[d] = carry ? x - cnt[d] : x;
+        }
+    }
+    __device__ __forceinline__ void locate(const Sel &s, const int32_t *pool, const int64_t *cstride,
+                                           const MaskTab &tab, int ndim, uint32_t dmask,
+                                           Decomp &o) const {
+#pragma unroll
+        for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+            if (d < ndim && ((dmask >> d) & 1u)) {
+                o.mem += sel_index(s, pool, d, idx[d]) * cstride[d];
+                o.v[0] += (int64_t)idx[d] * tab.stride[0][d];
+                o.v[1] += (int64_t)idx[d] * tab.stride[1][d];
+            }
+        }
+    }
+};
+
 template <typename T, bool SHUF, bool BSWAP, bool MASKED>
 __device__ void run_generic(const ReduceArgs &a, const uint8_t *base, const Sel &s, int64_t e0,
                             int64_t e1, TileAcc<T> &acc, const MaskT<T> &mk) {
     const uint32_t all = (1u << a.ndim) - 1u;
+    RadixCounter rc;
+    rc.init(s, a.ndim, all, (uint64_t)(e0 + threadIdx.x), (uint64_t)kBlock);
     for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
         Decomp o{0, {0, 0}};
-        decompose(s, a.pool, a.cstride, a.tab, a.ndim, all, e, o);
+        rc.locate(s, a.pool, a.cstride, a.tab, a.ndim, all, o);
         const T x = load_elem<T, SHUF, BSWAP>(base, a.chunk_elems, o.mem);
         acc.add_one(x, MASKED ? all_masked(mk, a.tab, o, x) : false);
+        rc.advance();
+    }
+}
+
+// Box-like selections whose innermost part is a contiguous run of L
+// elements (dims > k full, dim k unit step): stream each run as 16-B vectors.
+// Work items are (outer index of dims < k, vector within the run), walked by
+// a radix counter, U independent 16-B loads in flight per lane.
+template <typename T, bool BSWAP, bool MASKED>
+__device__ void run_rows(const ReduceArgs &a, const uint8_t *base, const Sel &s, int k, int64_t L,
+                         int64_t e0, int64_t e1, TileAcc<T> &acc, const MaskT<T> &mk) {
+    constexpr int N = 16 / sizeof(T);
+    const int64_t V = L / N;                       // vectors per run
+    const int64_t q0 = e0 / N, q1 = e1 / N;        // vector range of this tile
+    // radix over (dims 0..k-1, vector) with the vector as the fastest digit
+    Sel rs = s;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+        if (d == k) rs.cnt[d] = (int32_t)V;
+        else if (d > k) rs.cnt[d] = 1;
+    }
+    const uint32_t dm = (2u << k) - 1u;            // dims 0..k
+    int64_t inner0 = 0;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+        if (d == k) inner0 = (int64_t)s.start[d] * a.cstride[d];
+    RadixCounter rc;
+    rc.init(rs, a.ndim, dm, (uint64_t)(q0 + threadIdx.x), (uint64_t)kBlock);
+    auto addr = [&](const RadixCounter &r) -> const uint4 * {
+        int64_t mem = inner0;
+#pragma unroll
+        for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+            if (d < k) mem += sel_index(s, a.pool, d, r.idx[d]) * a.cstride[d];
+        uint32_t v = 0;
+#pragma unroll
+        for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+            if (d == k) v = r.idx[d];
+        return reinterpret_cast<const uint4 *>(base + (mem + (int64_t)v * N) * (int64_t)sizeof(T));
+    };
+    constexpr int U = 4;
+    int64_t q = q0 + threadIdx.x;
+    // converged part: every lane has U full items
+    const int64_t nfull = ((q1 - q0) / (U * kBlock)) * (U * kBlock);
+    for (int64_t it = 0; it < nfull; it += U * kBlock) {
+        const uint4 *p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) { p[u] = addr(rc); rc.advance(); }
+        uint4 r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = *p[u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED, true>(r[u], acc, mk);
+        q += U * kBlock;
+    }
+    for (; q < q1; q += kBlock) {
+        consume16<T, BSWAP, MASKED, false>(*addr(rc), acc, mk);
+        rc.advance();
     }
 }
 
 // ---------------------------------------------------------------------------
 // the hot kernel
 // ---------------------------------------------------------------------------
-template <typename T, bool SHUF, bool BSWAP, bool MASKED>
+// SEL = false: every chunk fully selected (batch.sel == NULL) -> a lean
+// streaming-only kernel (no selection state, high occupancy).
+template <typename T, bool SHUF, bool BSWAP, bool MASKED, bool SEL>
 __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     const int64_t b = blockIdx.x;
     const int64_t c = b / a.tpc;
@@ -243,6 +345,19 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
     if constexpr (MASKED) mk.init(a.mask);
     TileAcc<T> acc;
     acc.init();
+    if constexpr (!SEL) {
+        int64_t per = (a.chunk_elems + a.tpc - 1) / a.tpc;
+        per = (per + 63) & ~(int64_t)63;
+        const int64_t e0 = t * per, e1 = e0 + per < a.chunk_elems ? e0 + per : a.chunk_elems;
+        if (e0 < e1) {
+            if constexpr (SHUF && sizeof(T) > 1)
+                run_shuffled<T, BSWAP, MASKED>(base, a.chunk_elems, e0, e1, acc, mk);
+            else
+                run_plain<T, BSWAP, MASKED>(base, e0, e1, acc, mk);
+        }
+        tile_finish(acc, (!MASKED && e0 < e1) ? (uint64_t)(e1 - e0) : 0u, a.out + b);
+        return;
+    }
     Sel s;
     load_sel(s, a.sel, c, a.ndim, a.shape);
     int64_t total = 1;
@@ -277,8 +392,38 @@ __global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
             else
                 run_plain<T, BSWAP, MASKED>(base, m0 + e0, m0 + e1, acc, mk);
         } else {
-            generic = true;
-            run_generic<T, SHUF, BSWAP, MASKED>(a, base, s, e0, e1, acc, mk);
+            // rows of 16-B vectors?  (no shuffle/tables, unit-step innermost
+            // partial dim k, everything 16-B aligned)
+            constexpr int64_t ES = sizeof(T);
+            int k = -1;
+            int64_t L = 1;
+            bool rows = !SHUF && !(a.tab.on[0] || a.tab.on[1]) && ((uintptr_t)base & 15) == 0;
+#pragma unroll
+            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+                if (d < a.ndim) {
+                    if (k < 0) {
+                        const bool full = s.step[d] == 1 && s.start[d] == 0 &&
+                                          (int64_t)s.cnt[d] == a.shape[d];
+                        if (!full) {
+                            k = d;
+                            if (s.step[d] != 1) rows = false;
+                            if (((int64_t)s.start[d] * a.cstride[d] * ES) % 16 != 0) rows = false;
+                            L *= s.cnt[d];
+                        } else {
+                            L *= a.shape[d];
+                        }
+                    } else if ((a.cstride[d] * ES) % 16 != 0) {
+                        rows = false;  // an outer dim whose rows start unaligned
+                    }
+                }
+            }
+            if (k < 0 || (L * ES) % 16 != 0) rows = false;
+            if (rows) {
+                run_rows<T, BSWAP, MASKED>(a, base, s, k, L, e0, e1, acc, mk);
+            } else {
+                generic = true;
+                run_generic<T, SHUF, BSWAP, MASKED>(a, base, s, e0, e1, acc, mk);
+            }
         }
     }
     // unmasked contiguous tiles count every element; the generic path counts itself
@@ -424,11 +569,11 @@ __global__ __launch_bounds__(kBlock) void k_unshuffle(const uint8_t *src, uint8_
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <typename T>
-static hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool masked,
-                                  int64_t grid, hipStream_t st) {
-    const dim3 g((unsigned)grid), blk(kBlock);
-#define PYAS_L(S, B, M) hipLaunchKernelGGL((k_reduce<T, S, B, M>), g, blk, 0, st, a)
+template <typename T, bool SEL>
+static void launch_reduce_ts(const ReduceArgs &a, bool shuf, bool bsw, bool masked, dim3 g,
+                             hipStream_t st) {
+    const dim3 blk(kBlock);
+#define PYAS_L(S, B, M) hipLaunchKernelGGL((k_reduce<T, S, B, M, SEL>), g, blk, 0, st, a)
     if constexpr (sizeof(T) == 1) {
         if (masked) PYAS_L(false, false, true);
         else PYAS_L(false, false, false);
@@ -442,6 +587,14 @@ static hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool
         }
     }
 #undef PYAS_L
+}
+
+template <typename T>
+static hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool masked,
+                                  int64_t grid, hipStream_t st) {
+    const dim3 g((unsigned)grid);
+    if (a.sel) launch_reduce_ts<T, true>(a, shuf, bsw, masked, g, st);
+    else launch_reduce_ts<T, false>(a, shuf, bsw, masked, g, st);
     return hipGetLastError();
 }
 
