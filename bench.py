@@ -56,9 +56,11 @@ def parse():
     p.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                    help="weak: each GPU adds its own slab of the variable (dim 0); "
                         "strong: one variable of the config's shape split across GPUs")
-    p.add_argument("--cpu-chunks", type=int, default=1024,
+    p.add_argument("--cpu-chunks", type=int, default=4096,
                    help="chunks in the CPU-baseline sample (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=30)
+    p.add_argument("--host-inclusive", type=int, default=1,
+                   help="also time pinned host -> H2D -> reduce -> D2H (rank 0, N=1)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return p.parse_args()
 
@@ -119,6 +121,59 @@ def cpu_baseline(cfg, host_chunks: np.ndarray, n_chunks: int, missing, threads: 
     finally:
         os.unlink(path)
     return dt_s, out
+
+
+def host_inclusive(torch, ctx, data, cfg, dt, missing, reps=3, groups=16):
+    """Host-resident variant of the same step: the chunk bytes start in pinned
+    host memory, are copied H2D in `groups` slices on a copy stream while the
+    compute stream reduces the previous slice, and the 32-byte result is
+    copied back.  Returns (serial GB/s, overlapped GB/s)."""
+    from pyactivestorage_amd import engine
+    from pyactivestorage_amd.batch import ReductionPlan
+    nbytes = data.numel()
+    cb = int(np.prod(cfg["chunks"])) * dt.itemsize
+    n = nbytes // cb
+    host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    host.copy_(data, non_blocking=False)
+    dev = torch.empty_like(data)
+    comp = torch.cuda.current_stream()
+    copy = torch.cuda.Stream()
+    bounds = np.linspace(0, n, groups + 1).astype(np.int64)
+    plans = [ReductionPlan(ctx, dt, cfg["chunks"], dev.data_ptr() + int(a) * cb,
+                           np.arange(b - a, dtype=np.int64) * cb,
+                           shuffle=dt.itemsize if cfg["shuffle"] else 0, missing=missing,
+                           stream=comp.cuda_stream) for a, b in zip(bounds[:-1], bounds[1:])]
+    totals = torch.empty(groups * 32, dtype=torch.uint8, device=data.device)
+    final = torch.empty(32, dtype=torch.uint8, device=data.device)
+    out = torch.empty(32, dtype=torch.uint8, pin_memory=True)
+
+    def run(overlap):
+        evs = []
+        for g, (a, b) in enumerate(zip(bounds[:-1], bounds[1:])):
+            st = copy if overlap else comp
+            with torch.cuda.stream(st):
+                dev[a * cb:b * cb].copy_(host[a * cb:b * cb], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            evs.append(ev)
+        for g, p in enumerate(plans):
+            comp.wait_event(evs[g])
+            p.launch(comp.cuda_stream, chunk_partials=False)
+            totals[g * 32:(g + 1) * 32].copy_(p.total_tensor(torch))
+        engine.combine_partials(ctx, dt, totals.data_ptr(), groups, final.data_ptr(), False,
+                                comp.cuda_stream)
+        out.copy_(final, non_blocking=True)
+        torch.cuda.synchronize()
+
+    res = []
+    for overlap in (False, True):
+        run(overlap)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run(overlap)
+        res.append(nbytes / ((time.perf_counter() - t0) / reps) / 1e9)
+    del dev, host
+    return res
 
 
 def main():
@@ -263,6 +318,13 @@ def main():
                          f"{secs:.2f} s, host has {ncores} usable cores",
                "chunks_per_s": round(nc / secs, 1)}
 
+    hostinc = None
+    if rank == 0 and world == 1 and args.host_inclusive and data.numel() <= (8 << 30):
+        ser, ovl = host_inclusive(torch, ctx, data, cfg, dt, missing)
+        hostinc = {"serial_GBps": round(ser, 2), "overlapped_GBps": round(ovl, 2),
+                   "path": "pinned host -> H2D (16 slices, copy stream) -> fused reduce "
+                           "(compute stream) -> D2H 32 B"}
+
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
@@ -280,7 +342,7 @@ def main():
                          "kernel_ms_avg": round(kern_ms, 5), "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
                          "bytes_per_launch": bytes_per_launch},
             "cpu_baseline": cpu,
-            "result": result, "check": check,
+            "result": result, "check": check, "host_inclusive": hostinc,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
