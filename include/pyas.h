@@ -194,6 +194,16 @@ int pyas_combine_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
                           int64_t n, uint32_t combine_flags, pyas_partial *out,
                           void *stream);
 
+/* Segmented fixed-order combine: out[s] = fold of in[index[k]] for k in
+ * [seg_offsets[s], seg_offsets[s+1]) in order (device arrays).  This is the
+ * partial-axis form of the Active combine (active.py:575-598): `in` holds
+ * per-chunk partial arrays, each segment lists the partials that fall on one
+ * output element along the reduced axes. */
+int pyas_combine_segments(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
+                          const int64_t *index, const int64_t *seg_offsets,
+                          int64_t n_segments, uint32_t combine_flags,
+                          pyas_partial *out, void *stream);
+
 /* Standalone HDF5/numcodecs byte un-shuffle (storage.py:121-122), device to
  * device; n_bytes % elementsize trailing bytes are copied through. */
 int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes,

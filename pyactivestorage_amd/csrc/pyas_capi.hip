@@ -419,6 +419,22 @@ int pyas_combine_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, 
     return combine_into(dtype, in, n, combine_flags, (pyas_partial *)scr, out, (hipStream_t)stream);
 }
 
+int pyas_combine_segments(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
+                          const int64_t *index, const int64_t *seg_offsets, int64_t n_segments,
+                          uint32_t combine_flags, pyas_partial *out, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (elem_size(dtype) == 0) return fail(PYAS_ENOTSUP, "unsupported dtype code %d", dtype);
+    if (n_segments < 0) return fail(PYAS_EINVAL, "negative segment count");
+    if (n_segments == 0) return PYAS_OK;
+    if (!in || !index || !seg_offsets || !out) return fail(PYAS_EINVAL, "NULL argument");
+    if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
+        return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(pyas::launch_combine_segments(dtype, in, index, seg_offsets, n_segments, combine_flags,
+                                           out, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
 int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes, int32_t elementsize,
                    void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");

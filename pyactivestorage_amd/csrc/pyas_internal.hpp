@@ -50,6 +50,9 @@ hipError_t launch_tiles_to_chunks(int dtype, const pyas_partial *tiles, int64_t 
                                   int64_t n_chunks, pyas_partial *out, hipStream_t st);
 hipError_t launch_combine(int dtype, const pyas_partial *in, int64_t n, int64_t seg,
                           int64_t nblocks, uint32_t flags, pyas_partial *out, hipStream_t st);
+hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int64_t *index,
+                                   const int64_t *seg, int64_t n_seg, uint32_t flags,
+                                   pyas_partial *out, hipStream_t st);
 hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
 hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es,

@@ -480,6 +480,20 @@ __global__ __launch_bounds__(kBlock) void k_combine(const pyas_partial *in, int6
     if (threadIdx.x == 0) store_wpartial(out + blockIdx.x, acc);
 }
 
+// segmented combine: one thread per output segment, sequential fixed order
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_combine_segments(const pyas_partial *in, const int64_t *index,
+                                                             const int64_t *seg, int64_t n_seg,
+                                                             uint32_t flags, pyas_partial *out) {
+    const int64_t sidx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (sidx >= n_seg) return;
+    const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
+    WAcc<T> acc;
+    acc.init();
+    for (int64_t k = seg[sidx]; k < seg[sidx + 1]; ++k) merge(acc, in[index[k]], round);
+    store_wpartial(out + sidx, acc);
+}
+
 // ---------------------------------------------------------------------------
 // partial-axis reduction (axis ⊂ dims), one thread per output element
 // ---------------------------------------------------------------------------
@@ -633,6 +647,15 @@ hipError_t launch_combine(int dtype, const pyas_partial *in, int64_t n, int64_t 
                           uint32_t flags, pyas_partial *out, hipStream_t st) {
     const dim3 g((unsigned)nblocks), blk(kBlock);
     PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_combine<T>), g, blk, 0, st, in, n, seg, flags, out));
+    return hipGetLastError();
+}
+
+hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int64_t *index,
+                                   const int64_t *seg, int64_t n_seg, uint32_t flags,
+                                   pyas_partial *out, hipStream_t st) {
+    const dim3 g((unsigned)((n_seg + kBlock - 1) / kBlock)), blk(kBlock);
+    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_combine_segments<T>), g, blk, 0, st, in, index, seg,
+                                              n_seg, flags, out));
     return hipGetLastError();
 }
 

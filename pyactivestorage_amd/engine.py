@@ -106,6 +106,14 @@ def combine_partials(ctx: Context, dt, in_ptr, n, out_ptr, round_to_var: bool, s
                                              out_ptr, stream), "pyas_combine_partials")
 
 
+def combine_segments(ctx: Context, dt, in_ptr, index_ptr, seg_ptr, n_seg, out_ptr, round_to_var: bool,
+                     stream) -> None:
+    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
+    _lib.check(ctx.lib.pyas_combine_segments(ctx.handle, dtype_code(dt), in_ptr, index_ptr, seg_ptr,
+                                             int(n_seg), flags, out_ptr, stream),
+               "pyas_combine_segments")
+
+
 def unshuffle(ctx: Context, src_ptr, dst_ptr, nbytes, elementsize, stream) -> None:
     _lib.check(ctx.lib.pyas_unshuffle(ctx.handle, src_ptr, dst_ptr, int(nbytes), int(elementsize),
                                       stream), "pyas_unshuffle")

@@ -83,7 +83,7 @@ def normalize(chunk_selection, shape) -> ChunkSel:
         raise IndexError(f"too many indices for array: array is {ndim}-dimensional, "
                          f"but {n_real} were indexed")
     if n_ell:
-        k = sel.index(Ellipsis)
+        k = [i for i, x in enumerate(sel) if x is Ellipsis][0]
         sel = sel[:k] + (slice(None),) * (ndim - n_real) + sel[k + 1:]
     else:
         sel = sel + (slice(None),) * (ndim - n_real)
