@@ -23,7 +23,8 @@ MASK_EQ0, MASK_EQ1, MASK_GT, MASK_LT, MASK_TAB0, MASK_TAB1 = 1, 2, 4, 8, 16, 32
 COMBINE_ROUND_TO_VAR = 1
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libpyas_hip.so")
+# PYAS_LIB selects an alternative build (tuning experiments only)
+LIB_PATH = os.environ.get("PYAS_LIB") or os.path.join(LIB_DIR, "libpyas_hip.so")
 
 
 class Scalar(ctypes.Union):

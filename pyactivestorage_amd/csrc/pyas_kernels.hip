@@ -72,6 +72,23 @@ __device__ __forceinline__ void unshuffle16(const uint4 *pl, T out[16]) {
     }
 }
 
+// Streaming 16-B load; PYAS_NT=1 marks it non-temporal (read-once data).
+#ifndef PYAS_UNROLL
+#define PYAS_UNROLL 4
+#endif
+#ifndef PYAS_NT
+#define PYAS_NT 1   // measured: +7 % (C2) / +5 % (C3) over default-policy loads
+#endif
+__device__ __forceinline__ uint4 ldg16(const uint4 *p) {
+#if PYAS_NT
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(r.x, r.y, r.z, r.w);
+#else
+    return *p;
+#endif
+}
+
 // Raw 16 bytes of the plain layout -> 16/ES values
 template <typename T, bool BSWAP>
 __device__ __forceinline__ void unpack16(const uint4 &r, T *x) {
@@ -125,18 +142,18 @@ __device__ void run_plain(const uint8_t *base, int64_t m0, int64_t m1, TileAcc<T
     }
     const uint4 *v = reinterpret_cast<const uint4 *>(base + a0);  // keeps global provenance
     const int64_t nvec = (a1 - a0) / 16;
-    constexpr int U = 4;
+    constexpr int U = PYAS_UNROLL;
     constexpr int64_t STEP = (int64_t)U * kBlock;
     const int64_t nsteps = nvec / STEP;
     if (nsteps > 0) {
         uint4 cur[U], nxt[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = v[tid + u * kBlock];
+        for (int u = 0; u < U; ++u) cur[u] = ldg16(v + tid + u * kBlock);
         for (int64_t s = 0; s < nsteps; ++s) {
             // prefetch the next step (clamped: the last step re-reads itself)
             const int64_t ns = s + 1 < nsteps ? s + 1 : s;
 #pragma unroll
-            for (int u = 0; u < U; ++u) nxt[u] = v[ns * STEP + tid + u * kBlock];
+            for (int u = 0; u < U; ++u) nxt[u] = ldg16(v + ns * STEP + tid + u * kBlock);
 #pragma unroll
             for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED, true>(cur[u], acc, mk);
 #pragma unroll
@@ -144,7 +161,7 @@ __device__ void run_plain(const uint8_t *base, int64_t m0, int64_t m1, TileAcc<T
         }
     }
     for (int64_t k = nsteps * STEP + tid; k < nvec; k += kBlock)
-        consume16<T, BSWAP, MASKED, false>(v[k], acc, mk);
+        consume16<T, BSWAP, MASKED, false>(ldg16(v + k), acc, mk);
 }
 
 // Shuffled layout, chunk elements [i0, i1); n = elements in the chunk.
@@ -176,7 +193,7 @@ __device__ void run_shuffled(const uint8_t *base, int64_t n, int64_t i0, int64_t
         const int64_t i = g0 + g * 16;
         uint4 pl[ES];
 #pragma unroll
-        for (int b = 0; b < ES; ++b) pl[b] = *reinterpret_cast<const uint4 *>(base + (int64_t)b * n + i);
+        for (int b = 0; b < ES; ++b) pl[b] = ldg16(reinterpret_cast<const uint4 *>(base + (int64_t)b * n + i));
         T x[16];
         unshuffle16<T, BSWAP>(pl, x);
         if (g < nfull) acc.template add_n<16, MASKED, false>(x, mk);
@@ -319,13 +336,13 @@ __device__ void run_rows(const ReduceArgs &a, const uint8_t *base, const Sel &s,
         for (int u = 0; u < U; ++u) { p[u] = addr(rc); rc.advance(); }
         uint4 r[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) r[u] = *p[u];
+        for (int u = 0; u < U; ++u) r[u] = ldg16(p[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED, true>(r[u], acc, mk);
         q += U * kBlock;
     }
     for (; q < q1; q += kBlock) {
-        consume16<T, BSWAP, MASKED, false>(*addr(rc), acc, mk);
+        consume16<T, BSWAP, MASKED, false>(ldg16(addr(rc)), acc, mk);
         rc.advance();
     }
 }
