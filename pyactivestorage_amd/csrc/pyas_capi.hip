@@ -361,11 +361,43 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *ma
     if (batch->n_chunks == 0) return PYAS_OK;
     if (!out_offsets || !out) return fail(PYAS_EINVAL, "out/out_offsets is NULL");
     PYAS_HIP(hipSetDevice(ctx->device));
-    int64_t keep_elems = 1;
-    for (int d = 0; d < batch->ndim; ++d)
-        if (!((axes_mask >> d) & 1u)) keep_elems *= batch->chunk_shape[d];
-    int64_t bpc = (keep_elems + pyas::kBlock - 1) / pyas::kBlock;
+    // Geometry from the full chunk extents (selections only shrink them).
+    int64_t keep_elems = 1, red_elems = 1;
+    for (int d = 0; d < batch->ndim; ++d) {
+        if ((axes_mask >> d) & 1u) red_elems *= batch->chunk_shape[d];
+        else keep_elems *= batch->chunk_shape[d];
+    }
+    x.row = ((axes_mask >> (batch->ndim - 1)) & 1u) != 0;
+    // 16-B vector walks: >= 4-byte unshuffled elements, no index tables, the
+    // reduced offsets fit the LDS map and the last dim is whole 16-B vectors.
+    const int64_t last_bytes = (int64_t)batch->chunk_shape[batch->ndim - 1] * es;
+    x.vec = es >= 4 && !shuf && !x.r.tab.on[0] && !x.r.tab.on[1] && red_elems <= pyas::kAxesLds &&
+            last_bytes % 16 == 0;
+    const int64_t nv = 16 / es;   // elements per vector
+    auto pow2_floor = [](int64_t v) { int64_t p = 1; while (p * 2 <= v) p *= 2; return p; };
+    int64_t per_block, keep_items = keep_elems;
+    if (x.row) {   // about 8 reduced elements (or 4 vectors) per lane, G in [1, 64]
+        const int64_t per_lane_units = x.vec ? red_elems / nv / 4 : red_elems / 8;
+        int64_t g = pow2_floor(per_lane_units > 0 ? per_lane_units : 1);
+        x.group = (int32_t)(g > pyas::kWave ? pyas::kWave : g);
+        x.split = 1;
+        per_block = (pyas::kBlock / pyas::kWave) * (pyas::kWave / x.group);
+    } else {       // split the reduced range when a chunk has few outputs (or vectors of them)
+        if (x.vec && keep_elems % nv == 0) keep_items = keep_elems / nv;
+        else x.vec = false;
+        int64_t sp = 1;
+        while (sp < pyas::kBlock && keep_items * sp * 2 <= pyas::kBlock && red_elems / (sp * 2) >= 8) sp *= 2;
+        x.split = (int32_t)sp;
+        x.group = 1;
+        per_block = pyas::kBlock / sp;
+    }
+    // workgroups per chunk: enough to cover the outputs once, but each
+    // streaming at least ~128 KiB so the per-workgroup offset map amortises
+    int64_t bpc = (keep_items + per_block - 1) / per_block;
+    const int64_t by_bytes = (x.r.chunk_elems * es) >> 17;
+    if (bpc > by_bytes) bpc = by_bytes;
     if (bpc > 64) bpc = 64;
+    if (bpc < 1) bpc = 1;
     x.axes = axes_mask;
     x.bpc = bpc;
     x.out_offsets = out_offsets;

@@ -321,6 +321,78 @@ template <typename T> struct TileAcc {
     }
 };
 
+// One lane's TileAcc -> pyas_partial (no cross-lane work).
+template <typename T>
+__device__ __forceinline__ void tile_store_lane(const TileAcc<T> &a, pyas_partial *out) {
+    pyas_partial p;
+    TT<T>::put_acc(p.sum, a.sum);
+    p.count = (int64_t)a.count + (int64_t)a.ucount;
+    T mn = a.mn, mx = a.mx;
+    if constexpr (TT<T>::kind == 0) {
+        if (a.nan) { mn = (T)__builtin_nan(""); mx = mn; }
+    }
+    TT<T>::put(p.min, mn);
+    TT<T>::put(p.max, mx);
+    *out = p;
+}
+
+// Wave reduction of TileAcc (every lane participates) -> lane 0 stores.
+template <typename T>
+__device__ __forceinline__ void wave_finish(TileAcc<T> &a, pyas_partial *out) {
+    uint64_t c = (uint64_t)a.count;
+    uint32_t nan = a.nan ? 1u : 0u;
+#pragma unroll
+    for (int m = kWave / 2; m >= 1; m >>= 1) {
+        a.sum += shfl_xor(a.sum, m);
+        c += shfl_xor(c, m);
+        a.mn = tmin(a.mn, shfl_xor(a.mn, m));
+        a.mx = tmax(a.mx, shfl_xor(a.mx, m));
+        nan |= shfl_xor(nan, m);
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        a.count = (uint32_t)0;
+        a.ucount = 0;
+        a.nan = nan != 0;
+        pyas_partial p;
+        TT<T>::put_acc(p.sum, a.sum);
+        p.count = (int64_t)c;
+        T mn = a.mn, mx = a.mx;
+        if constexpr (TT<T>::kind == 0) {
+            if (nan) { mn = (T)__builtin_nan(""); mx = mn; }
+        }
+        TT<T>::put(p.min, mn);
+        TT<T>::put(p.max, mx);
+        *out = p;
+    }
+}
+
+// Segmented reduction over aligned groups of G lanes (G power of two <= 64);
+// the lane given a non-null `out` stores its group's partial.
+template <typename T>
+__device__ __forceinline__ void group_finish(TileAcc<T> &a, int G, pyas_partial *out) {
+    uint64_t c = (uint64_t)a.count;
+    uint32_t nan = a.nan ? 1u : 0u;
+    for (int m = G / 2; m >= 1; m >>= 1) {   // uniform trip count
+        a.sum += shfl_xor(a.sum, m);
+        c += shfl_xor(c, m);
+        a.mn = tmin(a.mn, shfl_xor(a.mn, m));
+        a.mx = tmax(a.mx, shfl_xor(a.mx, m));
+        nan |= shfl_xor(nan, m);
+    }
+    if (out) {
+        pyas_partial p;
+        TT<T>::put_acc(p.sum, a.sum);
+        p.count = (int64_t)c;
+        T mn = a.mn, mx = a.mx;
+        if constexpr (TT<T>::kind == 0) {
+            if (nan) { mn = (T)__builtin_nan(""); mx = mn; }
+        }
+        TT<T>::put(p.min, mn);
+        TT<T>::put(p.max, mx);
+        *out = p;
+    }
+}
+
 // Block reduction of TileAcc -> one pyas_partial (thread 0 stores).
 // `extra_count` is added once (unmasked tiles: the element count).
 template <typename T>

@@ -26,6 +26,8 @@ struct ReduceArgs {
     pyas_partial *out;
 };
 
+constexpr int kAxesLds = 8192;   // reduced-index offsets kept in LDS (int32, 32 KiB)
+
 struct AxesArgs {
     ReduceArgs r;
     uint32_t axes;
@@ -33,6 +35,10 @@ struct AxesArgs {
     const int64_t *out_offsets;
     pyas_partial *out;
     bool shuf, bswap;
+    bool row;                         // innermost dim reduced: G lanes per output
+    int32_t group;                    // row layout: lanes per output (power of 2)
+    int32_t split;                    // column layout: splits of the reduced range
+    bool vec;                         // geometry admits 16-B vector walks (kernel re-checks per chunk)
 };
 
 struct SelectArgs {

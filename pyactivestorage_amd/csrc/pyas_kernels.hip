@@ -514,8 +514,245 @@ __global__ __launch_bounds__(kBlock) void k_combine_segments(const pyas_partial 
 // ---------------------------------------------------------------------------
 // partial-axis reduction (axis ⊂ dims), one thread per output element
 // ---------------------------------------------------------------------------
+// Two layouts, chosen by the host:
+//  column (a.row == false; innermost selected dim kept): a workgroup holds
+//    OT = 256/S outputs x S splits of the reduced range; lanes with the same
+//    split hold consecutive outputs (consecutive addresses); the S partials of
+//    an output are folded through LDS in split order (deterministic);
+//  row (a.row; innermost dim reduced): G lanes per output (G a power of two,
+//    about 8 elements per lane), 64/G outputs per wave, lanes of a group read
+//    consecutive addresses, then a segmented shuffle reduce inside the group.
+// Both walk index spaces with radix counters (no per-element division) and
+// keep 4 independent loads in flight per lane.
+template <typename T, int U, bool SHUF, bool BSWAP>
+__device__ __forceinline__ void axes_walk(const ReduceArgs &r, const uint8_t *base, const Sel &s,
+                                          uint32_t red, const Decomp &base_o, RadixCounter &rc,
+                                          int64_t q0, int64_t n_red, int64_t stride, bool tabs,
+                                          const MaskT<T> &mk, TileAcc<T> &acc) {
+    int64_t q = q0;
+    const int64_t nfull = q0 + ((n_red - q0 + stride - 1) / stride) / U * U * stride;
+    for (; q < nfull; q += U * stride) {
+        Decomp od[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            od[u] = base_o;
+            rc.locate(s, r.pool, r.cstride, r.tab, r.ndim, red, od[u]);
+            rc.advance();
+        }
+        T x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = load_elem<T, SHUF, BSWAP>(base, r.chunk_elems, od[u].mem);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc.add_one(x[u], tabs ? all_masked(mk, r.tab, od[u], x[u]) : mk.masked(x[u]));
+    }
+    for (; q < n_red; q += stride) {
+        Decomp od = base_o;
+        rc.locate(s, r.pool, r.cstride, r.tab, r.ndim, red, od);
+        const T x = load_elem<T, SHUF, BSWAP>(base, r.chunk_elems, od.mem);
+        acc.add_one(x, tabs ? all_masked(mk, r.tab, od, x) : mk.masked(x));
+        rc.advance();
+    }
+}
+
+// Same walk with the reduced-index -> element-offset map precomputed in LDS
+// (no tables): per element one LDS read, one add, one load; U in flight.
+template <typename T, int U, bool SHUF, bool BSWAP>
+__device__ __forceinline__ void axes_walk_lds(const uint8_t *base, int64_t chunk_elems,
+                                              const int32_t *roff, int64_t base_mem, int64_t q0,
+                                              int64_t n_red, int64_t stride, const MaskT<T> &mk,
+                                              TileAcc<T> &acc) {
+    int64_t q = q0;
+    const int64_t nfull = q0 + ((n_red - q0 + stride - 1) / stride) / U * U * stride;
+    for (; q < nfull; q += U * stride) {
+        T x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            x[u] = load_elem<T, SHUF, BSWAP>(base, chunk_elems, base_mem + roff[q + u * stride]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc.add_one(x[u], mk.masked(x[u]));
+    }
+    for (; q < n_red; q += stride) {
+        const T x = load_elem<T, SHUF, BSWAP>(base, chunk_elems, base_mem + roff[q]);
+        acc.add_one(x, mk.masked(x));
+    }
+}
+
+
+// Fold the S split partials of each of OT outputs through LDS in split order
+// (deterministic); thread (ol, sp=0) ends with the folded value.
 template <typename T>
+__device__ __forceinline__ void fold_splits(TileAcc<T> &acc, int S, int OT, int ol, int sp) {
+    __shared__ typename TT<T>::Acc l_sum[kBlock];
+    __shared__ uint32_t l_cnt[kBlock];
+    __shared__ T l_mn[kBlock], l_mx[kBlock];
+    __shared__ uint8_t l_nan[kBlock];
+    const int t = threadIdx.x;
+    l_sum[t] = acc.sum; l_cnt[t] = acc.count; l_mn[t] = acc.mn; l_mx[t] = acc.mx;
+    l_nan[t] = acc.nan ? 1 : 0;
+    __syncthreads();
+    if (sp == 0) {
+        for (int k = 1; k < S; ++k) {
+            const int u = k * OT + ol;
+            acc.sum += l_sum[u];
+            acc.count += l_cnt[u];
+            acc.mn = tmin(acc.mn, l_mn[u]);
+            acc.mx = tmax(acc.mx, l_mx[u]);
+            acc.nan = acc.nan || l_nan[u];
+        }
+    }
+    __syncthreads();
+}
+
+template <typename T, bool SHUF, bool BSWAP>
+__device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
+                           const Sel &s, uint32_t red, uint32_t keep, int64_t n_out, int64_t n_red,
+                           const MaskT<T> &mk, int32_t *roff) {
+    const ReduceArgs &r = a.r;
+    constexpr int ES = sizeof(T), N = 16 / ES;
+    const bool tabs = r.tab.on[0] || r.tab.on[1];
+    const bool use_lds = !tabs && n_red <= kAxesLds;
+    // 16-B vector modes: the last chunk dim is a unit-step, 16-B aligned run
+    const int last = r.ndim - 1;
+    int64_t cnt_last = 1, start_last = 0, step_last = 1, shape_last = 1;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+        if (d == last) { cnt_last = s.cnt[d]; start_last = s.start[d]; step_last = s.step[d]; shape_last = r.shape[d]; }
+    const bool vec_ok = use_lds && !SHUF && ES >= 4 && step_last == 1 && ((uintptr_t)base & 15) == 0 &&
+                        (cnt_last * ES) % 16 == 0 && (start_last * ES) % 16 == 0 && (shape_last * ES) % 16 == 0;
+    const bool row_vec = a.row && a.vec && vec_ok;
+    const bool col_vec = !a.row && a.vec && vec_ok;
+    if (use_lds) {   // reduced-index -> element offset, once per workgroup
+        const int64_t nq = row_vec ? n_red / N : n_red;
+        const uint64_t m = row_vec ? N : 1;
+        RadixCounter t;   // one decomposition per thread, then digit adds
+        t.init(s, r.ndim, red, threadIdx.x * m, kBlock * m);
+        for (int64_t q = threadIdx.x; q < nq; q += kBlock) {
+            Decomp d{0, {0, 0}};
+            t.locate(s, r.pool, r.cstride, r.tab, r.ndim, red, d);
+            roff[q] = (int32_t)d.mem;
+            t.advance();
+        }
+        __syncthreads();
+    }
+    if (!a.row) {
+        const int S = a.split, OT = kBlock / S;
+        const int ol = threadIdx.x % OT, sp = threadIdx.x / OT;
+        const int64_t n_items = col_vec ? n_out / N : n_out;   // outputs or N-output vectors
+        const uint64_t m = col_vec ? N : 1;
+        RadixCounter ko;   // kept-index counter stepping with the loop
+        ko.init(s, r.ndim, keep, (uint64_t)(j * OT + ol) * m, (uint64_t)(a.bpc * OT) * m);
+        for (int64_t o0 = j * OT; o0 < n_items; o0 += a.bpc * OT) {   // block-uniform loop
+            const int64_t oi = o0 + ol;
+            Decomp base_o{0, {0, 0}};
+            if (oi < n_items) ko.locate(s, r.pool, r.cstride, r.tab, r.ndim, keep, base_o);
+            ko.advance();
+            if (col_vec) {
+                TileAcc<T> acc[N];
+#pragma unroll
+                for (int k = 0; k < N; ++k) acc[k].init();
+                if (oi < n_items) {
+                    const uint8_t *bo = base + base_o.mem * ES;
+                    constexpr int U = 4;
+                    int64_t q = sp;
+                    const int64_t nfull = sp + ((n_red - sp + S - 1) / S) / U * U * S;
+                    for (; q < nfull; q += U * S) {
+                        uint4 v[U];
+#pragma unroll
+                        for (int u = 0; u < U; ++u)
+                            v[u] = ldg16(reinterpret_cast<const uint4 *>(bo + (int64_t)roff[q + u * S] * ES));
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            T x[N];
+                            unpack16<T, BSWAP>(v[u], x);
+#pragma unroll
+                            for (int k = 0; k < N; ++k) acc[k].add_one(x[k], mk.masked(x[k]));
+                        }
+                    }
+                    for (; q < n_red; q += S) {
+                        T x[N];
+                        unpack16<T, BSWAP>(ldg16(reinterpret_cast<const uint4 *>(bo + (int64_t)roff[q] * ES)), x);
+#pragma unroll
+                        for (int k = 0; k < N; ++k) acc[k].add_one(x[k], mk.masked(x[k]));
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    if (S > 1) fold_splits(acc[k], S, OT, ol, sp);
+                    if (sp == 0 && oi < n_items) tile_store_lane(acc[k], a.out + a.out_offsets[c] + oi * N + k);
+                }
+                continue;
+            }
+            TileAcc<T> acc;
+            acc.init();
+            if (oi < n_items) {
+                if (use_lds) {
+                    axes_walk_lds<T, 8, SHUF, BSWAP>(base, r.chunk_elems, roff, base_o.mem, sp, n_red, S, mk, acc);
+                } else {
+                    RadixCounter rc;
+                    rc.init(s, r.ndim, red, (uint64_t)sp, (uint64_t)S);
+                    axes_walk<T, 4, SHUF, BSWAP>(r, base, s, red, base_o, rc, sp, n_red, S, tabs, mk, acc);
+                }
+            }
+            if (S > 1) fold_splits(acc, S, OT, ol, sp);
+            if (sp == 0 && oi < n_items) tile_store_lane(acc, a.out + a.out_offsets[c] + oi);
+        }
+    } else {
+        // G lanes per output (host-sized for element or 16-B vector walks)
+        const int G = a.group;
+        const int lane = threadIdx.x & (kWave - 1);
+        const int gl = lane & (G - 1);
+        const int64_t per_wave = kWave / G;
+        const int64_t wave = (int64_t)j * (kBlock / kWave) + threadIdx.x / kWave;
+        const int64_t nwaves = (int64_t)a.bpc * (kBlock / kWave);
+        RadixCounter ko;   // kept-index counter stepping with the loop
+        ko.init(s, r.ndim, keep, (uint64_t)(wave * per_wave + lane / G), (uint64_t)(nwaves * per_wave));
+        for (int64_t o0 = wave * per_wave; o0 < n_out; o0 += nwaves * per_wave) {  // wave-uniform
+            const int64_t o = o0 + lane / G;
+            TileAcc<T> acc;
+            acc.init();
+            Decomp base_o{0, {0, 0}};
+            if (o < n_out) ko.locate(s, r.pool, r.cstride, r.tab, r.ndim, keep, base_o);
+            ko.advance();
+            if (o < n_out) {
+                if (row_vec) {
+                    const uint8_t *bo = base + base_o.mem * ES;
+                    const int64_t nv = n_red / N;
+                    constexpr int U = 4;
+                    int64_t q = gl;
+                    const int64_t nfull = gl + ((nv - gl + G - 1) / G) / U * U * G;
+                    for (; q < nfull; q += U * G) {
+                        uint4 v[U];
+#pragma unroll
+                        for (int u = 0; u < U; ++u)
+                            v[u] = ldg16(reinterpret_cast<const uint4 *>(bo + (int64_t)roff[q + u * G] * ES));
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            T x[N];
+                            unpack16<T, BSWAP>(v[u], x);
+                            acc.template add_n<N, true, false>(x, mk);
+                        }
+                    }
+                    for (; q < nv; q += G) {
+                        T x[N];
+                        unpack16<T, BSWAP>(ldg16(reinterpret_cast<const uint4 *>(bo + (int64_t)roff[q] * ES)), x);
+                        acc.template add_n<N, true, false>(x, mk);
+                    }
+                } else if (use_lds) {
+                    axes_walk_lds<T, 8, SHUF, BSWAP>(base, r.chunk_elems, roff, base_o.mem, gl, n_red, G, mk, acc);
+                } else {
+                    RadixCounter rc;
+                    rc.init(s, r.ndim, red, (uint64_t)gl, (uint64_t)G);
+                    axes_walk<T, 4, SHUF, BSWAP>(r, base, s, red, base_o, rc, gl, n_red, G, tabs, mk, acc);
+                }
+            }
+            group_finish(acc, G, (o < n_out && gl == 0) ? a.out + a.out_offsets[c] + o : nullptr);
+        }
+    }
+}
+
+template <typename T, bool SHUF, bool BSWAP>
 __global__ __launch_bounds__(kBlock) void k_reduce_axes(AxesArgs a) {
+    __shared__ int32_t roff[kAxesLds];
     const int64_t c = blockIdx.x / a.bpc;
     const int64_t j = blockIdx.x - c * a.bpc;
     const ReduceArgs &r = a.r;
@@ -534,24 +771,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_axes(AxesArgs a) {
             else n_out *= s.cnt[d];
         }
     }
-    for (int64_t o = j * kBlock + threadIdx.x; o < n_out; o += a.bpc * kBlock) {
-        Decomp ok{0, {0, 0}};
-        decompose(s, r.pool, r.cstride, r.tab, r.ndim, keep, o, ok);
-        WAcc<T> acc;
-        acc.init();
-        for (int64_t q = 0; q < n_red; ++q) {
-            Decomp od = ok;
-            decompose(s, r.pool, r.cstride, r.tab, r.ndim, red, q, od);
-            const T x = load_elem_rt<T>(base, r.chunk_elems, od.mem, a.shuf, a.bswap);
-            if (!all_masked(mk, r.tab, od, x)) {
-                acc.sum += (typename TT<T>::Acc)x;
-                acc.count += 1;
-                acc.mn = pmin(acc.mn, x);
-                acc.mx = pmax(acc.mx, x);
-            }
-        }
-        store_wpartial(a.out + a.out_offsets[c] + o, acc);
-    }
+    axes_block<T, SHUF, BSWAP>(a, c, j, base, s, red, keep, n_out, n_red, mk, roff);
 }
 
 // ---------------------------------------------------------------------------
@@ -676,9 +896,22 @@ hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int6
     return hipGetLastError();
 }
 
+template <typename T>
+static void launch_axes_t(const AxesArgs &a, dim3 g, hipStream_t st) {
+    const dim3 blk(kBlock);
+    if constexpr (sizeof(T) == 1) {
+        hipLaunchKernelGGL((k_reduce_axes<T, false, false>), g, blk, 0, st, a);
+    } else {
+        if (a.shuf && a.bswap) hipLaunchKernelGGL((k_reduce_axes<T, true, true>), g, blk, 0, st, a);
+        else if (a.shuf) hipLaunchKernelGGL((k_reduce_axes<T, true, false>), g, blk, 0, st, a);
+        else if (a.bswap) hipLaunchKernelGGL((k_reduce_axes<T, false, true>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_reduce_axes<T, false, false>), g, blk, 0, st, a);
+    }
+}
+
 hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st) {
-    const dim3 g((unsigned)grid), blk(kBlock);
-    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_reduce_axes<T>), g, blk, 0, st, a));
+    const dim3 g((unsigned)grid);
+    PYAS_DISPATCH_T(dtype, launch_axes_t<T>(a, g, st));
     return hipGetLastError();
 }
 

@@ -1,0 +1,52 @@
+"""Partial-axis reduction throughput (row f1) on the C3 workload:
+1024^3 f32 in 64^3 chunks, _FillValue + valid_min/valid_max, device-resident.
+Reports GB/s of pyas_reduce_axes for several axis sets (per chunk, keepdims)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+    from pyactivestorage_amd import _lib, engine
+    from pyactivestorage_amd.batch import ReductionPlan
+    from pyactivestorage_amd.device import DeviceBuffer, get_context
+    from pyactivestorage_amd.synthetic import chunk_major_device
+    dev = torch.device("cuda", 0)
+    ctx = get_context(0)
+    st = torch.cuda.current_stream().cuda_stream
+    shape, chunks = (1024, 1024, 1024), (64, 64, 64)
+    data, offsets, _ = chunk_major_device(torch, shape, chunks, np.float32, dev, fill=-999.0, fill_frac=0.01)
+    missing = (np.float32(-999.0), None, np.float32(1000.0), np.float32(5e8))
+    plan = ReductionPlan(ctx, np.float32, chunks, data.data_ptr(), offsets, missing=missing, stream=st)
+    nbytes = data.numel()
+    res = {}
+    for axes in ((0,), (1,), (2,), (0, 1), (1, 2), (0, 2)):
+        n_out = int(np.prod([1 if d in axes else chunks[d] for d in range(3)]))
+        out = DeviceBuffer(ctx, len(offsets) * n_out * _lib.PARTIAL_NBYTES)
+        offs = torch.from_numpy(np.arange(len(offsets), dtype=np.int64) * n_out).to(dev)
+        mask = 0
+        for a in axes:
+            mask |= 1 << a
+        for _ in range(2):
+            engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, mask, offs.data_ptr(), out.ptr, st)
+        torch.cuda.synchronize()
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, mask, offs.data_ptr(), out.ptr, st)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        res[str(axes)] = {"ms": round(dt * 1e3, 3), "GBps": round(nbytes / dt / 1e9, 1),
+                          "outputs_per_chunk": n_out}
+        del out
+    print(json.dumps({"workload": "c3 partial-axis per-chunk reduce_axes", "results": res}))
+
+
+if __name__ == "__main__":
+    main()
