@@ -16,6 +16,8 @@
  *   activestorage/storage.py:107-123 filter_pipeline| fused into the kernels
  *     + numcodecs.Shuffle.decode (hdf2numcodec:37)  |   (pyas_batch.shuffle) and
  *                                                   |   pyas_unshuffle
+ *   activestorage/storage.py:119-120 compression.   | pyas_inflate (zlib streams,
+ *     decode = numcodecs.Zlib (hdf2numcodec:34-35)  |   one wave per chunk)
  *   activestorage/storage.py:126-153 mask_missing   | pyas_mask (thresholds are
  *                                                   |   pre-compiled on the host)
  *   activestorage/active.py:557-598 thread-pool     | pyas_reduce_chunks with a
@@ -208,6 +210,36 @@ int pyas_combine_segments(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
  * device; n_bytes % elementsize trailing bytes are copied through. */
 int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes,
                    int32_t elementsize, void *stream);
+
+/* ---- zlib inflate (row f3) ------------------------------------------------- */
+/* Per-stream outcome of pyas_inflate, mirroring zlib inflate()'s failures
+ * (zlib.error from zlib.decompress in the reference, storage.py:119-120). */
+typedef enum {
+    PYAS_INFLATE_OK = 0,
+    PYAS_INFLATE_BAD_HEADER = 1,    /* "incorrect header check" / bad method  */
+    PYAS_INFLATE_NEED_DICT = 2,     /* preset dictionary (FDICT)              */
+    PYAS_INFLATE_BAD_BLOCK = 3,     /* "invalid block type"                   */
+    PYAS_INFLATE_BAD_STORED = 4,    /* "invalid stored block lengths"         */
+    PYAS_INFLATE_BAD_CODE = 5,      /* invalid code lengths / tree            */
+    PYAS_INFLATE_BAD_SYMBOL = 6,    /* invalid literal/length/distance code   */
+    PYAS_INFLATE_BAD_DISTANCE = 7,  /* "invalid distance too far back"        */
+    PYAS_INFLATE_TRUNCATED = 8,     /* "incomplete or truncated stream"       */
+    PYAS_INFLATE_BAD_CHECKSUM = 9,  /* "incorrect data check" (Adler-32)      */
+    PYAS_INFLATE_OVERFLOW = 10      /* output larger than dst_capacity        */
+} pyas_inflate_status;
+
+/* Inflate n independent zlib (RFC 1950) streams, device to device
+ * (replaces numcodecs.Zlib.decode -> zlib.decompress at storage.py:119-120;
+ * built by hdf2numcodec.py:34-35).  Stream c is src[src_offsets[c] ..
+ * + src_sizes[c]) and inflates into dst[dst_offsets[c] .. + dst_capacity[c]);
+ * out_sizes[c] receives the inflated length and status[c] a
+ * pyas_inflate_status.  All arrays are device arrays.  Bytes after the
+ * Adler-32 trailer are ignored, as zlib.decompress does.  A dst offset that is
+ * 16-byte aligned gets 1 KiB coalesced writes. */
+int pyas_inflate(pyas_ctx *ctx, const uint8_t *src, const int64_t *src_offsets,
+                 const int64_t *src_sizes, int64_t n, uint8_t *dst,
+                 const int64_t *dst_offsets, const int64_t *dst_capacity,
+                 int64_t *out_sizes, int32_t *status, void *stream);
 
 /* ---- measurement ---------------------------------------------------------- */
 /* When enabled, the main reduce kernel of each pyas_reduce_chunks call is

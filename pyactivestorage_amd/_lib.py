@@ -94,6 +94,7 @@ SIGNATURES = {
     "pyas_combine_partials": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_segments": [_vp, _i32, _vp, _vp, _vp, _i64, _u32, _vp, _vp],
     "pyas_unshuffle": [_vp, _vp, _vp, _i64, _i32, _vp],
+    "pyas_inflate": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "pyas_timing_enable": [_vp, _i32],
     "pyas_timing_read": [_vp, ctypes.POINTER(ctypes.c_float), _i32, ctypes.POINTER(_i32)],
 }

@@ -478,6 +478,22 @@ int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes, i
     return PYAS_OK;
 }
 
+int pyas_inflate(pyas_ctx *ctx, const uint8_t *src, const int64_t *src_offsets,
+                 const int64_t *src_sizes, int64_t n, uint8_t *dst,
+                 const int64_t *dst_offsets, const int64_t *dst_capacity,
+                 int64_t *out_sizes, int32_t *status, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (n < 0) return fail(PYAS_EINVAL, "negative stream count");
+    if (n == 0) return PYAS_OK;
+    if (!src || !src_offsets || !src_sizes || !dst || !dst_offsets || !dst_capacity || !out_sizes || !status)
+        return fail(PYAS_EINVAL, "NULL array");
+    if (n >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "too many streams");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    pyas::InflateArgs x{src, src_offsets, src_sizes, dst, dst_offsets, dst_capacity, out_sizes, status};
+    PYAS_HIP(pyas::launch_inflate(x, n, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
 int pyas_timing_enable(pyas_ctx *ctx, int32_t max_launches) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     if (max_launches < 0) return fail(PYAS_EINVAL, "max_launches < 0");

@@ -1,0 +1,409 @@
+// pyas_inflate.hip — zlib (RFC 1950) / DEFLATE (RFC 1951) decoding on gfx950.
+//
+// Row f3 of the hot-path table: the reference inflates every compressed chunk
+// on the host, `numcodecs.Zlib.decode` -> `zlib.decompress` (built at
+// activestorage/hdf2numcodec.py:34-35, applied at activestorage/storage.py:
+// 119-120).  Here one wave64 inflates one chunk stream; a launch covers every
+// chunk of a query, so thousands of streams decode concurrently.
+//
+// Per wave:
+//   * input: 128 dwords of the stream held lane-distributed in two VGPRs and
+//     read with v_readlane (no per-symbol memory access);
+//   * Huffman decode: 10-bit literal/length and 8-bit distance lookup tables
+//     in LDS, canonical walk for longer codes;
+//   * output: the 32 KiB history window lives in LDS; a match is copied
+//     lane-parallel as out[p+i] = out[p-d+(i mod d)] (all sources precede p);
+//     the window is flushed to HBM in coalesced 1 KiB pieces, and Adler-32 is
+//     folded in per flush with a wave reduction.
+// Error behaviour follows zlib's inflate(): bad header, preset dictionary,
+// invalid block type, stored-length mismatch, over-subscribed or incomplete
+// codes, invalid symbols, distance too far back, truncated input and Adler-32
+// mismatch are all reported per stream (pyas_inflate_status in pyas.h).
+#include "pyas_internal.hpp"
+
+namespace pyas {
+namespace {
+
+constexpr uint32_t kWin = 32768, kWinMask = kWin - 1;
+constexpr int kLitBits = 10, kDistBits = 8;
+constexpr uint32_t kFlush = 1024;   // bytes per coalesced flush (16 per lane)
+
+__constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                        31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t c_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
+                                        2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t c_dist_base[30] = {1,    2,    3,    4,    5,    7,     9,     13,    17,  25,
+                                         33,   49,   65,   97,   129,  193,   257,   385,   513, 769,
+                                         1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
+                                         6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t c_clen_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct Lds {
+    alignas(16) uint8_t win[kWin];
+    uint16_t lit[1 << kLitBits];    // sym | len << 9; len 0 -> canonical walk
+    uint16_t dist[1 << kDistBits];
+    uint16_t lit_cnt[16], dist_cnt[16];
+    uint16_t lit_sym[288], dist_sym[32];
+    uint16_t code[320];             // canonical code per symbol (build scratch)
+    uint16_t offs[16], next[16];    // build scratch
+    uint8_t lens[320];              // code lengths: literal/length then distance
+};
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Lane-distributed bit reader over dword-aligned input.
+struct BitIn {
+    const uint32_t *w;
+    uint32_t nwords;   // readable dwords from w
+    uint32_t nbits;    // valid bits from w (stream end)
+    uint32_t pos;      // bit position from w
+    uint32_t base;     // dword index held by lane 0 of cur
+    uint32_t cur, nxt;
+
+    __device__ __forceinline__ uint32_t load(uint32_t k) const {
+        const uint32_t i = k + (threadIdx.x & 63);
+        return i < nwords ? __builtin_nontemporal_load(w + i) : 0u;
+    }
+    __device__ __forceinline__ void seek() {   // after a jump (stored blocks)
+        base = pos >> 5;
+        cur = load(base);
+        nxt = load(base + 64);
+    }
+    __device__ __forceinline__ uint32_t word(uint32_t k) const {
+        const uint32_t r = k - base;
+        return r < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)r)
+                      : (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)(r - 64));
+    }
+    // At least 32 valid bits starting at pos (LSB first).
+    __device__ __forceinline__ uint32_t peek() {
+        const uint32_t k = pos >> 5;
+        if (k >= base + 64) {
+            if (k >= base + 128) {
+                seek();
+            } else {
+                cur = nxt;
+                base += 64;
+                nxt = load(base + 64);
+            }
+        }
+        const uint64_t v = (uint64_t)word(k) | ((uint64_t)word(k + 1) << 32);
+        return uni((uint32_t)(v >> (pos & 31)));
+    }
+};
+
+// Canonical Huffman table for `n` code lengths in L.lens[first..first+n).
+// Returns 0, or PYAS_INFLATE_BAD_CODE for over-subscribed / disallowed
+// incomplete sets (zlib inflate_table rules: incomplete only for a single
+// length-1 code in the literal/length and distance trees).
+__device__ int build(Lds &L, int first, int n, uint16_t *cnt, uint16_t *sorted, uint16_t *tab, int P,
+                     bool code_lengths) {
+    const int lane = threadIdx.x & 63;
+    for (int k = lane; k < (1 << P); k += 64) tab[k] = 0;
+    __shared__ int s_status;
+    if (lane == 0) {
+        for (int l = 0; l < 16; ++l) cnt[l] = 0;
+        for (int s = 0; s < n; ++s) cnt[L.lens[first + s]]++;
+        cnt[0] = 0;
+        int max = 0;
+        for (int l = 1; l < 16; ++l)
+            if (cnt[l]) max = l;
+        int left = 1, status = 0;
+        for (int l = 1; l < 16; ++l) {
+            left = (left << 1) - cnt[l];
+            if (left < 0) status = PYAS_INFLATE_BAD_CODE;
+        }
+        if (left > 0 && max > 0 && (code_lengths || max != 1)) status = PYAS_INFLATE_BAD_CODE;
+        uint16_t *offs = L.offs, *next = L.next;
+        offs[1] = 0;
+        next[1] = 0;
+        for (int l = 1; l < 15; ++l) {
+            offs[l + 1] = offs[l] + cnt[l];
+            next[l + 1] = (uint16_t)((next[l] + cnt[l]) << 1);
+        }
+        for (int s = 0; s < n; ++s) {
+            const int l = L.lens[first + s];
+            if (l) {
+                sorted[offs[l]++] = (uint16_t)s;
+                L.code[s] = next[l]++;
+            }
+        }
+        s_status = status;
+    }
+    __syncthreads();
+    for (int s = lane; s < n; s += 64) {
+        const int l = L.lens[first + s];
+        if (l && l <= P) {
+            const uint32_t rc = __builtin_bitreverse32((uint32_t)L.code[s]) >> (32 - l);
+            const uint16_t e = (uint16_t)(s | (l << 9));
+            for (uint32_t k = rc; k < (1u << P); k += 1u << l) tab[k] = e;
+        }
+    }
+    __syncthreads();
+    return uni((uint32_t)s_status);
+}
+
+// Decode one symbol: table hit, else canonical walk over the peeked bits.
+// Returns sym and sets len (0 on an invalid code).
+__device__ __forceinline__ uint32_t decode(uint32_t bits, const uint16_t *tab, int P, const uint16_t *cnt,
+                                           const uint16_t *sorted, uint32_t &len) {
+    const uint32_t e = uni(tab[bits & ((1u << P) - 1)]);
+    if (e >> 9) {
+        len = e >> 9;
+        return e & 511u;
+    }
+    int code = 0, firstc = 0, index = 0;
+    for (int l = 1; l < 16; ++l) {
+        code |= (bits >> (l - 1)) & 1u;
+        const int count = cnt[l];
+        if (code - firstc < count) {
+            len = (uint32_t)l;
+            return uni(sorted[index + code - firstc]);
+        }
+        index += count;
+        firstc = (firstc + count) << 1;
+        code <<= 1;
+    }
+    len = 0;
+    return 0;
+}
+
+struct Out {
+    uint8_t *dst;
+    uint32_t cap, pos, fpos;
+    uint32_t a, b;   // Adler-32 state
+    bool aligned;
+};
+
+// Write window bytes [fpos, fpos + n) to dst, folding them into Adler-32.
+__device__ void flush(Lds &L, Out &o, uint32_t n) {
+    const int lane = threadIdx.x & 63;
+    uint32_t s = 0, t = 0;
+    if (n == kFlush && o.aligned) {   // 16 bytes per lane, 1 KiB coalesced
+        const uint32_t off = o.fpos + lane * 16;
+        const uint4 v = *reinterpret_cast<const uint4 *>(&L.win[off & kWinMask]);
+        *reinterpret_cast<uint4 *>(o.dst + off) = v;
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t byte = (w4[k >> 2] >> ((k & 3) * 8)) & 255u;
+            s += byte;
+            t += (n - (lane * 16 + k)) * byte;
+        }
+    } else {
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t byte = L.win[(o.fpos + i) & kWinMask];
+            o.dst[o.fpos + i] = (uint8_t)byte;
+            s += byte;
+            t += (n - i) * byte;
+        }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        s += (uint32_t)__shfl_xor((int)s, m, 64);
+        t += (uint32_t)__shfl_xor((int)t, m, 64);
+    }
+    s = uni(s);
+    t = uni(t);
+    // a' = a + sum b_i;  b' = b + n*a + sum (n - i) b_i   (mod 65521)
+    const uint64_t bb = (uint64_t)o.b + (uint64_t)n * o.a + t;
+    o.a = (o.a + s) % 65521u;
+    o.b = (uint32_t)(bb % 65521u);
+    o.fpos += n;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
+    __shared__ Lds L;
+    const int64_t c = blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint8_t *src = x.src + x.src_offsets[c];
+    const int64_t n_in = x.src_sizes[c];
+    const uint32_t mis = (uint32_t)((uintptr_t)src & 3);
+    BitIn in;
+    in.w = reinterpret_cast<const uint32_t *>(src - mis);
+    in.nbits = (uint32_t)((n_in + mis) * 8);
+    in.nwords = (uint32_t)((n_in + mis + 3) / 4);
+    in.pos = mis * 8;
+    in.seek();
+    Out o;
+    o.dst = x.dst + x.dst_offsets[c];
+    o.cap = (uint32_t)x.dst_capacity[c];
+    o.pos = o.fpos = 0;
+    o.a = 1;
+    o.b = 0;
+    o.aligned = (((uintptr_t)o.dst) & 15) == 0;
+    int status = PYAS_INFLATE_OK;
+
+    // zlib header (RFC 1950): CM 8, CINFO <= 7, FCHECK, no preset dictionary
+    if (n_in < 6) status = PYAS_INFLATE_TRUNCATED;
+    if (status == 0) {
+        const uint32_t h = in.peek();
+        const uint32_t cmf = h & 255u, flg = (h >> 8) & 255u;
+        if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u)
+            status = PYAS_INFLATE_BAD_HEADER;
+        else if (flg & 32u)
+            status = PYAS_INFLATE_NEED_DICT;
+        in.pos += 16;
+    }
+    bool last = false;
+    while (status == 0 && !last) {
+        uint32_t h = in.peek();
+        last = h & 1u;
+        const uint32_t type = (h >> 1) & 3u;
+        in.pos += 3;
+        if (type == 0) {   // stored
+            in.pos = (in.pos + 7) & ~7u;
+            h = in.peek();
+            const uint32_t len = h & 0xffffu, nlen = h >> 16;
+            in.pos += 32;
+            if ((len ^ 0xffffu) != nlen) { status = PYAS_INFLATE_BAD_STORED; break; }
+            if (in.pos + len * 8 > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
+            if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
+            const uint8_t *bytes = reinterpret_cast<const uint8_t *>(in.w) + (in.pos >> 3);
+            for (uint32_t done = 0; done < len;) {
+                while (o.pos - o.fpos >= kFlush) flush(L, o, kFlush);
+                const uint32_t step = min(len - done, kFlush);
+                for (uint32_t i = lane; i < step; i += 64) L.win[(o.pos + i) & kWinMask] = bytes[done + i];
+                o.pos += step;
+                done += step;
+                __syncthreads();
+            }
+            in.pos += len * 8;
+            in.seek();
+            continue;
+        }
+        const uint16_t *lit = L.lit, *dist = L.dist;
+        if (type == 1) {   // fixed codes (RFC 1951 3.2.6)
+            for (int s = lane; s < 320; s += 64)
+                L.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+            __syncthreads();
+            build(L, 0, 288, L.lit_cnt, L.lit_sym, L.lit, kLitBits, false);
+            build(L, 288, 32, L.dist_cnt, L.dist_sym, L.dist, kDistBits, false);
+        } else if (type == 2) {   // dynamic codes
+            h = in.peek();
+            const uint32_t nlen = (h & 31u) + 257, ndist = ((h >> 5) & 31u) + 1, ncode = ((h >> 10) & 15u) + 4;
+            in.pos += 14;
+            if (nlen > 286 || ndist > 30) { status = PYAS_INFLATE_BAD_CODE; break; }
+            // code-length code: 3 bits per length in c_clen_order
+            h = in.peek();
+            const uint32_t h2 = [&] { in.pos += 30; const uint32_t r = in.peek(); in.pos -= 30; return r; }();
+            for (int s = lane; s < 19; s += 64) {
+                const uint32_t bit = 3u * (uint32_t)s;
+                uint32_t v = 0;
+                if ((uint32_t)s < ncode) v = bit < 30 ? (h >> bit) & 7u : (h2 >> (bit - 30)) & 7u;
+                L.lens[c_clen_order[s]] = (uint8_t)v;
+            }
+            in.pos += 3 * ncode;
+            __syncthreads();
+            // the code-length tree uses the distance table slots (7-bit codes)
+            if (build(L, 0, 19, L.dist_cnt, L.dist_sym, L.dist, 7, true)) { status = PYAS_INFLATE_BAD_CODE; break; }
+            // code lengths for literal/length + distance, serial (<= 316)
+            uint32_t k = 0;
+            uint32_t prev = 0;
+            while (k < nlen + ndist) {
+                const uint32_t bits = in.peek();
+                uint32_t l;
+                const uint32_t sym = decode(bits, L.dist, 7, L.dist_cnt, L.dist_sym, l);
+                if (!l) { status = PYAS_INFLATE_BAD_CODE; break; }
+                in.pos += l;
+                const uint32_t more = bits >> l;
+                uint32_t rep, val;
+                if (sym < 16) {
+                    rep = 1; val = sym; prev = sym;
+                } else if (sym == 16) {
+                    if (k == 0) { status = PYAS_INFLATE_BAD_CODE; break; }
+                    rep = 3 + (more & 3u); val = prev; in.pos += 2;
+                } else if (sym == 17) {
+                    rep = 3 + (more & 7u); val = 0; in.pos += 3;
+                } else {
+                    rep = 11 + (more & 127u); val = 0; in.pos += 7;
+                }
+                if (k + rep > nlen + ndist) { status = PYAS_INFLATE_BAD_CODE; break; }
+                if (sym > 16) prev = 0;   // zlib: repeat-previous after zeros repeats zero
+                for (uint32_t i = lane; i < rep; i += 64) {
+                    const uint32_t s = k + i;
+                    L.lens[s < nlen ? s : 288 + (s - nlen)] = (uint8_t)val;
+                }
+                k += rep;
+            }
+            if (status) break;
+            for (int s = nlen + lane; s < 288; s += 64) L.lens[s] = 0;
+            for (int s = 288 + (int)ndist + lane; s < 320; s += 64) L.lens[s] = 0;
+            __syncthreads();
+            if (L.lens[256] == 0) { status = PYAS_INFLATE_BAD_CODE; break; }
+            if (build(L, 0, 288, L.lit_cnt, L.lit_sym, L.lit, kLitBits, false) ||
+                build(L, 288, 32, L.dist_cnt, L.dist_sym, L.dist, kDistBits, false)) {
+                status = PYAS_INFLATE_BAD_CODE;
+                break;
+            }
+        } else {
+            status = PYAS_INFLATE_BAD_BLOCK;
+            break;
+        }
+        // symbol loop
+        for (;;) {
+            if (o.pos - o.fpos >= kFlush) flush(L, o, kFlush);
+            if (in.pos > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
+            uint32_t bits = in.peek();
+            uint32_t l;
+            uint32_t sym = decode(bits, lit, kLitBits, L.lit_cnt, L.lit_sym, l);
+            if (!l) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
+            if (sym < 256) {
+                if (o.pos >= o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
+                if (lane == 0) L.win[o.pos & kWinMask] = (uint8_t)sym;
+                o.pos++;
+                in.pos += l;
+                continue;
+            }
+            if (sym == 256) { in.pos += l; break; }
+            sym -= 257;
+            if (sym >= 29) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
+            const uint32_t le = c_len_extra[sym];
+            const uint32_t len = c_len_base[sym] + ((bits >> l) & ((1u << le) - 1u));
+            in.pos += l + le;
+            bits = in.peek();
+            const uint32_t ds = decode(bits, dist, kDistBits, L.dist_cnt, L.dist_sym, l);
+            if (!l || ds >= 30) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
+            const uint32_t de = c_dist_extra[ds];
+            const uint32_t d = c_dist_base[ds] + ((bits >> l) & ((1u << de) - 1u));
+            in.pos += l + de;
+            if (d > o.pos) { status = PYAS_INFLATE_BAD_DISTANCE; break; }
+            if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
+            const uint32_t from = o.pos - d;
+            for (uint32_t r = 0; r < len; r += 64) {
+                const uint32_t i = r + lane;
+                if (i < len) {
+                    const uint32_t srcp = from + (d >= len ? i : i % d);
+                    L.win[(o.pos + i) & kWinMask] = L.win[srcp & kWinMask];
+                }
+            }
+            o.pos += len;
+        }
+    }
+    if (status == 0) {
+        __syncthreads();
+        while (o.pos - o.fpos >= kFlush) flush(L, o, kFlush);
+        if (o.pos > o.fpos) flush(L, o, o.pos - o.fpos);
+        in.pos = (in.pos + 7) & ~7u;
+        if (in.pos + 32 > in.nbits) {
+            status = PYAS_INFLATE_TRUNCATED;
+        } else {
+            const uint32_t v = in.peek();
+            const uint32_t want = __builtin_bswap32(v);
+            if (want != ((o.b << 16) | o.a)) status = PYAS_INFLATE_BAD_CHECKSUM;
+        }
+    }
+    if (lane == 0) {
+        x.status[c] = status;
+        x.out_sizes[c] = o.pos;
+    }
+}
+
+hipError_t launch_inflate(const InflateArgs &x, int64_t n, hipStream_t stream) {
+    hipLaunchKernelGGL(k_inflate, dim3((uint32_t)n), dim3(64), 0, stream, x);
+    return hipGetLastError();
+}
+
+}  // namespace pyas

@@ -41,6 +41,15 @@ struct AxesArgs {
     bool vec;                         // geometry admits 16-B vector walks (kernel re-checks per chunk)
 };
 
+struct InflateArgs {
+    const uint8_t *src;
+    const int64_t *src_offsets, *src_sizes;
+    uint8_t *dst;
+    const int64_t *dst_offsets, *dst_capacity;
+    int64_t *out_sizes;
+    int32_t *status;
+};
+
 struct SelectArgs {
     ReduceArgs r;
     int64_t bpc;
@@ -60,6 +69,7 @@ hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int6
                                    const int64_t *seg, int64_t n_seg, uint32_t flags,
                                    pyas_partial *out, hipStream_t st);
 hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st);
+hipError_t launch_inflate(const InflateArgs &x, int64_t n, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
 hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es,
                             hipStream_t st);

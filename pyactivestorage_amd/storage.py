@@ -26,6 +26,7 @@ import numpy as np
 from . import _lib, engine, results, selection
 from .device import get_context
 from .dtypes import native
+from .inflate import inflate_chunk, is_zlib
 from .masking import compile_missing
 
 __all__ = ["reduce_chunk", "reduce_opens3_chunk", "reduce_chunk_bytes", "filter_pipeline",
@@ -145,6 +146,13 @@ def reduce_opens3_chunk(fh, offset, size, compression, filters, missing, dtype, 
                               chunk_selection, axis, method)
 
 
+class _Sized:
+    """Size stand-in for a chunk that only exists on the device."""
+
+    def __init__(self, size):
+        self.size = int(size)
+
+
 def reduce_chunk_bytes(raw, compression, filters, missing, dtype, shape, order,
                        chunk_selection, axis, method=None, device=0):
     """The reduction of :func:`reduce_chunk` for chunk bytes already in memory."""
@@ -153,7 +161,16 @@ def reduce_chunk_bytes(raw, compression, filters, missing, dtype, shape, order,
     if order not in ("C", "F"):
         raise NotImplementedError(f"order={order!r}")
     shuffles = _shuffle_sizes(filters)
-    buf = np.frombuffer(memoryview(_decompress(raw, compression)), dtype=np.uint8)
+    ctx = get_context(device)
+    st = ctx.thread_stream()
+    n_expect = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    if is_zlib(compression):
+        # f3: upload the deflated bytes, inflate on the device (raises like zlib)
+        data = ctx.thread_buffer("data", max(n_expect, 16))
+        inflate_chunk(ctx, raw, data.ptr, n_expect, st)
+        buf = _Sized(n_expect)
+    else:
+        buf = np.frombuffer(memoryview(_decompress(raw, compression)), dtype=np.uint8)
     # .view(dtype) then .reshape(shape) errors (storage.py:59-62)
     if buf.size % dt.itemsize:
         raise ValueError("When changing to a larger dtype, its size must be a divisor of the "
@@ -168,10 +185,9 @@ def reduce_chunk_bytes(raw, compression, filters, missing, dtype, shape, order,
     dev_dims = cs.dims[::-1] if rev else cs.dims
     dev_of = (lambda d: len(shape) - 1 - d) if rev else (lambda d: d)
 
-    ctx = get_context(device)
-    st = ctx.thread_stream()
-    data = ctx.thread_buffer("data", max(buf.size, 16))
-    ctx.h2d(data.ptr, buf, st)
+    if not is_zlib(compression):
+        data = ctx.thread_buffer("data", max(buf.size, 16))
+        ctx.h2d(data.ptr, buf, st)
     # shuffle filters: fuse the last one when its element size is the dtype's;
     # any other shuffle pass runs as a standalone device un-shuffle first
     fused = 0

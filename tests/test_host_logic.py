@@ -241,3 +241,23 @@ def test_capi_errors_without_gpu_are_reported():
         _lib.check(_lib.EINVAL)
     with pytest.raises(NotImplementedError):
         _lib.check(_lib.ENOTSUP)
+
+
+def test_inflate_status_mapping_and_packing():
+    """pyas_inflate statuses map to zlib.decompress's exceptions (storage.py:119-120)."""
+    import zlib as _z
+
+    from pyactivestorage_amd.inflate import pack_streams, raise_for_status
+    cap = np.array([8, 8, 8], dtype=np.int64)
+    raise_for_status(np.zeros(3, np.int32), cap, cap)   # all OK: no exception
+    for code, text in ((1, "incorrect header check"), (8, "incomplete or truncated stream"),
+                       (9, "incorrect data check"), (7, "invalid distance too far back")):
+        with pytest.raises(_z.error, match=text):
+            raise_for_status(np.array([0, code, 0], np.int32), cap, cap)
+    with pytest.raises(_z.error, match="^Error 2 while decompressing data$"):
+        raise_for_status(np.array([2], np.int32), cap[:1], cap[:1])
+    with pytest.raises(ValueError):
+        raise_for_status(np.array([10], np.int32), cap[:1], cap[:1])
+    host, offs, sizes = pack_streams([b"abc", b"", b"defgh"], align=4)
+    assert list(offs) == [0, 4, 4] and list(sizes) == [3, 0, 5]
+    assert host[:3].tobytes() == b"abc" and host[4:9].tobytes() == b"defgh"
