@@ -152,6 +152,11 @@ int pyas_ctx_create(int device, pyas_ctx **out);
 int pyas_ctx_destroy(pyas_ctx *ctx);
 /* Tile size (bytes of selected data per workgroup); 0 restores the default. */
 int pyas_ctx_set_tile_bytes(pyas_ctx *ctx, int64_t tile_bytes);
+/* LDS history ring of pyas_inflate, 2^wbits bytes per stream, wbits in
+ * [13, 15] (default 13).  Smaller rings run more streams per CU; matches
+ * reaching past the ring read the already-written output.  Results do not
+ * depend on it. */
+int pyas_ctx_set_inflate_window_bits(pyas_ctx *ctx, int32_t wbits);
 
 /* ---- memory helpers (so a non-torch host can drive the ABI) ------------- */
 int pyas_malloc(pyas_ctx *ctx, size_t nbytes, void **dptr);

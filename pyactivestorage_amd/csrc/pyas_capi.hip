@@ -65,6 +65,7 @@ struct Scratch {
 struct pyas_ctx {
     int device = 0;
     int64_t tile_bytes = kDefaultTileBytes;
+    int32_t inflate_wbits = 13;   // LDS history ring of pyas_inflate: 2^13 B per stream
     std::mutex mu;
     std::unordered_map<void *, Scratch> scratch;  // keyed by stream
     // timing
@@ -229,6 +230,13 @@ int pyas_ctx_set_tile_bytes(pyas_ctx *ctx, int64_t tile_bytes) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     if (tile_bytes < 0) return fail(PYAS_EINVAL, "tile_bytes < 0");
     ctx->tile_bytes = tile_bytes == 0 ? kDefaultTileBytes : tile_bytes;
+    return PYAS_OK;
+}
+
+int pyas_ctx_set_inflate_window_bits(pyas_ctx *ctx, int32_t wbits) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (wbits < 13 || wbits > 15) return fail(PYAS_EINVAL, "inflate window bits %d not in [13, 15]", wbits);
+    ctx->inflate_wbits = wbits;
     return PYAS_OK;
 }
 
@@ -490,7 +498,7 @@ int pyas_inflate(pyas_ctx *ctx, const uint8_t *src, const int64_t *src_offsets,
     if (n >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "too many streams");
     PYAS_HIP(hipSetDevice(ctx->device));
     pyas::InflateArgs x{src, src_offsets, src_sizes, dst, dst_offsets, dst_capacity, out_sizes, status};
-    PYAS_HIP(pyas::launch_inflate(x, n, (hipStream_t)stream));
+    PYAS_HIP(pyas::launch_inflate(x, n, ctx->inflate_wbits, (hipStream_t)stream));
     return PYAS_OK;
 }
 

@@ -11,10 +11,15 @@
 //     read with v_readlane (no per-symbol memory access);
 //   * Huffman decode: 10-bit literal/length and 8-bit distance lookup tables
 //     in LDS, canonical walk for longer codes;
-//   * output: the 32 KiB history window lives in LDS; a match is copied
-//     lane-parallel as out[p+i] = out[p-d+(i mod d)] (all sources precede p);
-//     the window is flushed to HBM in coalesced 1 KiB pieces, and Adler-32 is
-//     folded in per flush with a wave reduction.
+//   * output: the most recent 2^WBITS bytes (8-32 KiB) live in an LDS ring; a
+//     match is copied lane-parallel as out[p+i] = out[p-d+(i mod d)] (all
+//     sources precede p); the ring is flushed to HBM in coalesced 1 KiB
+//     pieces, and Adler-32 is folded in per flush with a wave reduction;
+//   * a match reaching further back than the ring (d > 2^WBITS, up to
+//     DEFLATE's 32 KiB) reads the already-flushed output from HBM after the
+//     wave's stores have drained, with L1-bypassing (agent-scope) loads.
+//     A smaller ring is what buys occupancy: 2^13 B + tables ~= 12.5 KiB of
+//     LDS per wave -> 12 streams per CU instead of 4.
 // Error behaviour follows zlib's inflate(): bad header, preset dictionary,
 // invalid block type, stored-length mismatch, over-subscribed or incomplete
 // codes, invalid symbols, distance too far back, truncated input and Adler-32
@@ -24,7 +29,6 @@
 namespace pyas {
 namespace {
 
-constexpr uint32_t kWin = 32768, kWinMask = kWin - 1;
 constexpr int kLitBits = 10, kDistBits = 8;
 constexpr uint32_t kFlush = 1024;   // bytes per coalesced flush (16 per lane)
 
@@ -39,8 +43,9 @@ __constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 
                                          6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t c_clen_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
+// Code tables + build scratch (the history window is separate: its size is a
+// template parameter of the kernel).
 struct Lds {
-    alignas(16) uint8_t win[kWin];
     uint16_t lit[1 << kLitBits];    // sym | len << 9; len 0 -> canonical walk
     uint16_t dist[1 << kDistBits];
     uint16_t lit_cnt[16], dist_cnt[16];
@@ -175,13 +180,14 @@ struct Out {
     bool aligned;
 };
 
-// Write window bytes [fpos, fpos + n) to dst, folding them into Adler-32.
-__device__ void flush(Lds &L, Out &o, uint32_t n) {
+// Write ring bytes [fpos, fpos + n) to dst, folding them into Adler-32.
+template <uint32_t MASK>
+__device__ void flush(const uint8_t *win, Out &o, uint32_t n) {
     const int lane = threadIdx.x & 63;
     uint32_t s = 0, t = 0;
     if (n == kFlush && o.aligned) {   // 16 bytes per lane, 1 KiB coalesced
         const uint32_t off = o.fpos + lane * 16;
-        const uint4 v = *reinterpret_cast<const uint4 *>(&L.win[off & kWinMask]);
+        const uint4 v = *reinterpret_cast<const uint4 *>(&win[off & MASK]);
         *reinterpret_cast<uint4 *>(o.dst + off) = v;
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -192,7 +198,7 @@ __device__ void flush(Lds &L, Out &o, uint32_t n) {
         }
     } else {
         for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t byte = L.win[(o.fpos + i) & kWinMask];
+            const uint32_t byte = win[(o.fpos + i) & MASK];
             o.dst[o.fpos + i] = (uint8_t)byte;
             s += byte;
             t += (n - i) * byte;
@@ -214,8 +220,19 @@ __device__ void flush(Lds &L, Out &o, uint32_t n) {
 
 }  // namespace
 
+// Byte of already-flushed output, coherent with this wave's earlier stores.
+__device__ __forceinline__ uint32_t far_byte(const uint8_t *p) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)p & ~(uintptr_t)3);
+    const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (v >> (((uintptr_t)p & 3) * 8)) & 255u;
+}
+
+template <int WBITS>
 __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
+    constexpr uint32_t kWin = 1u << WBITS, kWinMask = kWin - 1;
+    static_assert(kWin >= 4096, "ring must exceed the unflushed bytes plus one match");
     __shared__ Lds L;
+    __shared__ alignas(16) uint8_t win[kWin];
     const int64_t c = blockIdx.x;
     const int lane = threadIdx.x;
     const uint8_t *src = x.src + x.src_offsets[c];
@@ -263,9 +280,9 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
             if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
             const uint8_t *bytes = reinterpret_cast<const uint8_t *>(in.w) + (in.pos >> 3);
             for (uint32_t done = 0; done < len;) {
-                while (o.pos - o.fpos >= kFlush) flush(L, o, kFlush);
+                while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
                 const uint32_t step = min(len - done, kFlush);
-                for (uint32_t i = lane; i < step; i += 64) L.win[(o.pos + i) & kWinMask] = bytes[done + i];
+                for (uint32_t i = lane; i < step; i += 64) win[(o.pos + i) & kWinMask] = bytes[done + i];
                 o.pos += step;
                 done += step;
                 __syncthreads();
@@ -344,7 +361,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
         }
         // symbol loop
         for (;;) {
-            if (o.pos - o.fpos >= kFlush) flush(L, o, kFlush);
+            if (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
             if (in.pos > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
             uint32_t bits = in.peek();
             uint32_t l;
@@ -352,7 +369,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
             if (!l) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
             if (sym < 256) {
                 if (o.pos >= o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
-                if (lane == 0) L.win[o.pos & kWinMask] = (uint8_t)sym;
+                if (lane == 0) win[o.pos & kWinMask] = (uint8_t)sym;
                 o.pos++;
                 in.pos += l;
                 continue;
@@ -372,11 +389,20 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
             if (d > o.pos) { status = PYAS_INFLATE_BAD_DISTANCE; break; }
             if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
             const uint32_t from = o.pos - d;
+            if (d > kWin) {   // beyond the ring: every source byte is already in dst
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                for (uint32_t r = 0; r < len; r += 64) {
+                    const uint32_t i = r + lane;
+                    if (i < len) win[(o.pos + i) & kWinMask] = (uint8_t)far_byte(o.dst + from + i);
+                }
+                o.pos += len;
+                continue;
+            }
             for (uint32_t r = 0; r < len; r += 64) {
                 const uint32_t i = r + lane;
                 if (i < len) {
                     const uint32_t srcp = from + (d >= len ? i : i % d);
-                    L.win[(o.pos + i) & kWinMask] = L.win[srcp & kWinMask];
+                    win[(o.pos + i) & kWinMask] = win[srcp & kWinMask];
                 }
             }
             o.pos += len;
@@ -384,8 +410,8 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
     }
     if (status == 0) {
         __syncthreads();
-        while (o.pos - o.fpos >= kFlush) flush(L, o, kFlush);
-        if (o.pos > o.fpos) flush(L, o, o.pos - o.fpos);
+        while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
+        if (o.pos > o.fpos) flush<kWinMask>(win, o, o.pos - o.fpos);
         in.pos = (in.pos + 7) & ~7u;
         if (in.pos + 32 > in.nbits) {
             status = PYAS_INFLATE_TRUNCATED;
@@ -401,8 +427,12 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
     }
 }
 
-hipError_t launch_inflate(const InflateArgs &x, int64_t n, hipStream_t stream) {
-    hipLaunchKernelGGL(k_inflate, dim3((uint32_t)n), dim3(64), 0, stream, x);
+hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t stream) {
+    switch (wbits) {
+    case 15: hipLaunchKernelGGL(k_inflate<15>, dim3((uint32_t)n), dim3(64), 0, stream, x); break;
+    case 14: hipLaunchKernelGGL(k_inflate<14>, dim3((uint32_t)n), dim3(64), 0, stream, x); break;
+    default: hipLaunchKernelGGL(k_inflate<13>, dim3((uint32_t)n), dim3(64), 0, stream, x); break;
+    }
     return hipGetLastError();
 }
 

@@ -69,7 +69,7 @@ hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int6
                                    const int64_t *seg, int64_t n_seg, uint32_t flags,
                                    pyas_partial *out, hipStream_t st);
 hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st);
-hipError_t launch_inflate(const InflateArgs &x, int64_t n, hipStream_t st);
+hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
 hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es,
                             hipStream_t st);

@@ -50,7 +50,10 @@ def _cases():
         "empty": b"",
         "k1023": rng.integers(0, 4, 1023, dtype=np.uint8).tobytes(),
         "k1025": rng.integers(0, 4, 1025, dtype=np.uint8).tobytes(),
-        "far": rng.integers(0, 256, 40_000, dtype=np.uint8).tobytes() * 2,   # 32 KiB+ distances
+        "far": rng.integers(0, 256, 40_000, dtype=np.uint8).tobytes() * 2,   # beyond the 32 KiB window
+        "d12k": rng.integers(0, 256, 12_000, dtype=np.uint8).tobytes() * 3,   # matches past an 8 KiB ring
+        "d20k": rng.integers(0, 256, 20_000, dtype=np.uint8).tobytes() * 3,   # ... and past 16 KiB
+        "d32k": rng.integers(0, 256, 32_768, dtype=np.uint8).tobytes() * 2,   # the maximum distance
     }
     out = []
     for name, p in payloads.items():
@@ -83,6 +86,20 @@ def test_inflate_matches_zlib_all_cases(gpu):
     for (name, plain, comp), g in zip(CASES, got):
         assert zlib.decompress(comp) == plain, name
         assert g == plain, name
+
+
+@pytest.mark.parametrize("wbits", [13, 14, 15])
+def test_inflate_every_ring_size(gpu, wbits):
+    """The LDS ring size is a per-context launch choice; each variant is exact."""
+    sel = [c for c in CASES if c[0].startswith(("d12k", "d20k", "d32k", "text", "field_shuffled"))]
+    fn = gpu.lib.pyas_ctx_set_inflate_window_bits
+    assert fn(gpu.handle, wbits) == 0
+    try:
+        got = inflate_many(gpu, [c[2] for c in sel], [max(len(c[1]), 1) for c in sel])
+    finally:
+        fn(gpu.handle, 13)
+    for (name, plain, _), g in zip(sel, got):
+        assert g == plain, (name, wbits)
 
 
 def test_inflate_trailing_bytes_ignored(gpu):
