@@ -298,8 +298,9 @@ def main():
     try:
         with open(args.traffic_file) as f:
             tr = json.load(f)
-        if tr.get("config") == args.config:
-            traffic = tr.get("hbm_bytes_per_launch")
+        ent = tr.get(args.config) if "config" not in tr else (tr if tr["config"] == args.config else None)
+        if ent:
+            traffic = ent.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
 

@@ -157,6 +157,11 @@ int pyas_ctx_set_tile_bytes(pyas_ctx *ctx, int64_t tile_bytes);
  * reaching past the ring read the already-written output.  Results do not
  * depend on it. */
 int pyas_ctx_set_inflate_window_bits(pyas_ctx *ctx, int32_t wbits);
+/* on != 0 (default): pyas_reduce_chunks folds tiles -> chunks -> groups ->
+ * total in one finishing launch (the last group to finish folds the total,
+ * in group order); 0: the total is folded by a second launch.  Results are
+ * bit-identical either way. */
+int pyas_ctx_set_chained_combine(pyas_ctx *ctx, int32_t on);
 
 /* ---- memory helpers (so a non-torch host can drive the ABI) ------------- */
 int pyas_malloc(pyas_ctx *ctx, size_t nbytes, void **dptr);

@@ -14,6 +14,7 @@
 import argparse
 import csv
 import json
+import os
 import statistics
 
 
@@ -54,7 +55,7 @@ def main():
     if a.trace:
         ks = kernel_stats(a.trace)
         summary["kernels"] = ks
-        red = [v for k, v in ks.items() if "k_reduce<" in k]
+        red = [v for k, v in ks.items() if "k_reduce<" in k or "k_reduce_u<" in k]
         if red:
             avg = sum(v["avg_ns"] * v["calls"] for v in red) / sum(v["calls"] for v in red)
             summary["k_reduce_avg_ns"] = avg
@@ -75,11 +76,19 @@ def main():
     with open(a.out, "w") as f:
         json.dump(summary, f, indent=1)
     if a.traffic and "pmc" in summary:
+        # {config: {...}}: one entry per bench config, merged into the file
+        try:
+            with open(a.traffic) as f:
+                tr = json.load(f)
+        except (OSError, ValueError):
+            tr = {}
+        if "config" in tr:   # old single-config layout
+            tr = {tr["config"]: tr}
+        tr[a.config] = {"hbm_bytes_per_launch": summary["pmc"]["hbm_read_bytes_per_launch"]
+                        + summary["pmc"].get("write_bytes_per_launch", 0.0),
+                        "source": os.path.relpath(a.out, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))}
         with open(a.traffic, "w") as f:
-            json.dump({"config": a.config,
-                       "hbm_bytes_per_launch": summary["pmc"]["hbm_read_bytes_per_launch"]
-                       + summary["pmc"].get("write_bytes_per_launch", 0.0),
-                       "source": a.out}, f, indent=1)
+            json.dump(tr, f, indent=1)
     print(json.dumps(summary, indent=1))
 
 

@@ -82,6 +82,7 @@ SIGNATURES = {
     "pyas_ctx_destroy": [_vp],
     "pyas_ctx_set_tile_bytes": [_vp, _i64],
     "pyas_ctx_set_inflate_window_bits": [_vp, _i32],
+    "pyas_ctx_set_chained_combine": [_vp, _i32],
     "pyas_malloc": [_vp, _sz, ctypes.POINTER(_vp)],
     "pyas_free": [_vp, _vp],
     "pyas_memcpy_h2d": [_vp, _vp, _vp, _sz, _vp],

@@ -58,6 +58,8 @@ int elem_size(int dtype) {
 struct Scratch {
     void *ptr = nullptr;
     size_t bytes = 0;
+    uint32_t *cnt = nullptr;   // chained-combine arrival counters, zero between launches
+    int64_t n_cnt = 0;
 };
 
 }  // namespace
@@ -66,6 +68,7 @@ struct pyas_ctx {
     int device = 0;
     int64_t tile_bytes = kDefaultTileBytes;
     int32_t inflate_wbits = 13;   // LDS history ring of pyas_inflate: 2^13 B per stream
+    bool chained = true;          // k_finish folds the total itself (arrival counter)
     std::mutex mu;
     std::unordered_map<void *, Scratch> scratch;  // keyed by stream
     // timing
@@ -91,6 +94,27 @@ int ensure_scratch(pyas_ctx *ctx, void *stream, size_t bytes, void **out) {
         s.bytes = want;
     }
     *out = s.ptr;
+    return PYAS_OK;
+}
+
+// Zeroed arrival counters of the chained combine for `stream` (the kernel
+// leaves them zero again, so only a new allocation is cleared).
+int ensure_counters(pyas_ctx *ctx, void *stream, int64_t n, uint32_t **out) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Scratch &s = ctx->scratch[stream];
+    if (s.n_cnt < n) {
+        if (s.cnt) {
+            PYAS_HIP(hipStreamSynchronize((hipStream_t)stream));
+            PYAS_HIP(hipFree(s.cnt));
+            s.cnt = nullptr;
+            s.n_cnt = 0;
+        }
+        const int64_t want = n < 1024 ? 1024 : n;
+        PYAS_HIP(hipMalloc((void **)&s.cnt, (size_t)want * sizeof(uint32_t)));
+        PYAS_HIP(hipMemsetAsync(s.cnt, 0, (size_t)want * sizeof(uint32_t), (hipStream_t)stream));
+        s.n_cnt = want;
+    }
+    *out = s.cnt;
     return PYAS_OK;
 }
 
@@ -164,7 +188,7 @@ int64_t tiles_per_chunk(const pyas_ctx *ctx, int64_t chunk_bytes) {
 
 // Fixed-order combine of n partials into out[0]; may use scratch at `tmp`
 // (room for n / kSeg + 1 partials).
-constexpr int64_t kSeg = 2048;
+constexpr int64_t kSeg = pyas::kCombineSeg;
 
 int combine_into(int dtype, const pyas_partial *in, int64_t n, uint32_t flags, pyas_partial *tmp,
                  pyas_partial *out, hipStream_t st) {
@@ -219,7 +243,10 @@ int pyas_ctx_destroy(pyas_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     for (auto &kv : ctx->scratch)
+    {
         if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+        if (kv.second.cnt) (void)hipFree(kv.second.cnt);
+    }
     for (auto e : ctx->ev0) (void)hipEventDestroy(e);
     for (auto e : ctx->ev1) (void)hipEventDestroy(e);
     delete ctx;
@@ -230,6 +257,12 @@ int pyas_ctx_set_tile_bytes(pyas_ctx *ctx, int64_t tile_bytes) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     if (tile_bytes < 0) return fail(PYAS_EINVAL, "tile_bytes < 0");
     ctx->tile_bytes = tile_bytes == 0 ? kDefaultTileBytes : tile_bytes;
+    return PYAS_OK;
+}
+
+int pyas_ctx_set_chained_combine(pyas_ctx *ctx, int32_t on) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    ctx->chained = on != 0;
     return PYAS_OK;
 }
 
@@ -328,17 +361,31 @@ int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *
     const int64_t grid = n * tpc;
     if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid of %lld workgroups", (long long)grid);
     a.tpc = tpc;
-    // scratch layout: [tiles (tpc>1)] [chunk partials (if chunk_out NULL)] [combine tmp]
-    const size_t tiles_b = tpc > 1 ? (size_t)grid * sizeof(pyas_partial) : 0;
-    const size_t chunks_b = chunk_out ? 0 : (size_t)n * sizeof(pyas_partial);
-    const size_t tmp_b = ((size_t)(n / kSeg) + 2) * sizeof(pyas_partial);
+    // k_reduce writes one partial per workgroup: straight into chunk_out when a
+    // chunk is one tile, else into scratch; k_finish folds tiles -> chunks ->
+    // groups -> total in one launch.
+    // scratch layout: [tile partials (unless they go to chunk_out)] [group partials]
+    const bool direct = tpc == 1 && chunk_out;
+    const size_t tiles_b = direct ? 0 : (size_t)grid * sizeof(pyas_partial);
+    const int64_t ng = (n + kSeg - 1) / kSeg;
+    const size_t tmp_b = (size_t)(ng + 1) * sizeof(pyas_partial);
     void *scr = nullptr;
-    rc = ensure_scratch(ctx, stream, tiles_b + chunks_b + tmp_b, &scr);
+    rc = ensure_scratch(ctx, stream, tiles_b + tmp_b, &scr);
     if (rc) return rc;
-    pyas_partial *tiles = (pyas_partial *)scr;
-    pyas_partial *chunks = chunk_out ? chunk_out : (pyas_partial *)((char *)scr + tiles_b);
-    pyas_partial *tmp = (pyas_partial *)((char *)scr + tiles_b + chunks_b);
-    a.out = tpc > 1 ? tiles : chunks;
+    a.out = direct ? chunk_out : (pyas_partial *)scr;
+    pyas::FinishArgs f;
+    f.tiles = a.out;
+    f.tpc = tpc;
+    f.n_chunks = n;
+    f.chunk_out = direct ? nullptr : chunk_out;
+    f.gtmp = (pyas_partial *)((char *)scr + tiles_b);
+    f.total = total;
+    f.cnt = nullptr;
+    f.flags = combine_flags;
+    if (total && ctx->chained) {
+        rc = ensure_counters(ctx, stream, 1, &f.cnt);
+        if (rc) return rc;
+    }
 
     const bool timed = ctx->timing_n < (int32_t)ctx->ev0.size();
     if (timed) PYAS_HIP(hipEventRecord(ctx->ev0[ctx->timing_n], st));
@@ -347,11 +394,10 @@ int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *
         PYAS_HIP(hipEventRecord(ctx->ev1[ctx->timing_n], st));
         ctx->timing_n++;
     }
-    if (tpc > 1) PYAS_HIP(pyas::launch_tiles_to_chunks(batch->dtype, tiles, tpc, n, chunks, st));
-    if (total) {
-        rc = combine_into(batch->dtype, chunks, n, combine_flags, tmp, total, st);
-        if (rc) return rc;
-    }
+    if (direct && !total) return PYAS_OK;
+    PYAS_HIP(pyas::launch_finish(batch->dtype, f, st));
+    if (total && !f.cnt)   // unchained: fold the group partials in a second launch
+        PYAS_HIP(pyas::launch_combine(batch->dtype, f.gtmp, ng, ng, 1, 0u, total, st));
     return PYAS_OK;
 }
 

@@ -393,6 +393,28 @@ __device__ __forceinline__ void group_finish(TileAcc<T> &a, int G, pyas_partial 
     }
 }
 
+// Partials handed between workgroups of ONE launch (the chained combine) are
+// written and read with agent-scope relaxed atomics: on gfx950 these are
+// sc1 accesses at the device-coherent level, so no agent-scope fence (a whole
+// L2 write-back / invalidate per XCD) is needed to publish or observe them.
+__device__ __forceinline__ void store_partial_agent(pyas_partial *out, const pyas_partial &p) {
+    uint64_t w[4];
+    __builtin_memcpy(w, &p, sizeof(w));
+    uint64_t *o = reinterpret_cast<uint64_t *>(out);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) __hip_atomic_store(o + k, w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ pyas_partial load_partial_agent(const pyas_partial *in) {
+    uint64_t w[4];
+    const uint64_t *i = reinterpret_cast<const uint64_t *>(in);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        w[k] = __hip_atomic_load(const_cast<uint64_t *>(i + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pyas_partial p;
+    __builtin_memcpy(&p, w, sizeof(w));
+    return p;
+}
+
 // Block reduction of TileAcc -> one pyas_partial (thread 0 stores).
 // `extra_count` is added once (unmasked tiles: the element count).
 template <typename T>
@@ -491,6 +513,15 @@ __device__ __forceinline__ void store_partial(pyas_partial *out, const AccT<T, C
 }
 template <typename T>
 __device__ __forceinline__ void store_wpartial(pyas_partial *out, const WAcc<T> &a) { store_partial(out, a); }
+template <typename T>
+__device__ __forceinline__ void store_wpartial_agent(pyas_partial *out, const WAcc<T> &a) {
+    pyas_partial p;
+    TT<T>::put_acc(p.sum, a.sum);
+    p.count = (int64_t)a.count;
+    TT<T>::put(p.min, a.mn);
+    TT<T>::put(p.max, a.mx);
+    store_partial_agent(out, p);
+}
 
 // ---------------------------------------------------------------------------
 // selection of one chunk (storage.py:95 chunk[chunk_selection])

@@ -23,7 +23,22 @@ struct ReduceArgs {
     int32_t ndim;
     pyas_mask mask;
     MaskTab tab;
-    pyas_partial *out;
+    pyas_partial *out;                // one partial per workgroup (tile)
+};
+
+// Chunks per first-level combine group: one k_finish block, one thread per
+// chunk (k_combine uses the same segments, so both orders agree).
+constexpr int64_t kCombineSeg = kBlock;
+
+// k_finish: tile partials -> chunk partials -> group partials -> total
+struct FinishArgs {
+    const pyas_partial *tiles;        // n_chunks * tpc, chunk-major
+    int64_t tpc, n_chunks;
+    pyas_partial *chunk_out;          // may be NULL
+    pyas_partial *gtmp;               // n_chunks / kCombineSeg + 1 group partials
+    pyas_partial *total;              // may be NULL (chunk partials only)
+    uint32_t *cnt;                    // zeroed arrival counter; NULL: the host folds gtmp
+    uint32_t flags;                   // PYAS_COMBINE_*
 };
 
 constexpr int kAxesLds = 8192;   // reduced-index offsets kept in LDS (int32, 32 KiB)
@@ -59,10 +74,29 @@ struct SelectArgs {
     bool shuf, bswap;
 };
 
+// Per-dtype launchers: defined in pyas_kernels.hpp, instantiated per dtype by
+// pyas_inst.hip.
+template <typename T>
+hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool masked, int64_t grid,
+                           hipStream_t st);
+template <typename T>
+hipError_t launch_finish_t(const FinishArgs &f, hipStream_t st);
+template <typename T>
+hipError_t launch_combine_t(const pyas_partial *in, int64_t n, int64_t seg, int64_t nblocks,
+                            uint32_t flags, pyas_partial *out, hipStream_t st);
+template <typename T>
+hipError_t launch_combine_segments_t(const pyas_partial *in, const int64_t *index,
+                                     const int64_t *seg, int64_t n_seg, uint32_t flags,
+                                     pyas_partial *out, hipStream_t st);
+template <typename T>
+hipError_t launch_axes_t(const AxesArgs &a, int64_t grid, hipStream_t st);
+template <typename T>
+hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st);
+
+// dtype dispatch (pyas_kernels.hip)
 hipError_t launch_reduce(int dtype, const ReduceArgs &a, bool shuf, bool bsw, bool masked,
                          int64_t grid, hipStream_t st);
-hipError_t launch_tiles_to_chunks(int dtype, const pyas_partial *tiles, int64_t tpc,
-                                  int64_t n_chunks, pyas_partial *out, hipStream_t st);
+hipError_t launch_finish(int dtype, const FinishArgs &f, hipStream_t st);
 hipError_t launch_combine(int dtype, const pyas_partial *in, int64_t n, int64_t seg,
                           int64_t nblocks, uint32_t flags, pyas_partial *out, hipStream_t st);
 hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int64_t *index,

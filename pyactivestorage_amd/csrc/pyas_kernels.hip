@@ -1,806 +1,12 @@
-// pyas_kernels.hip — gfx950 kernels of the chunk-reduction backend.
-//
-// k_reduce        : the hot path.  One workgroup per (chunk, tile); streams the
-//                   chunk's selected bytes from HBM with 16-B loads, undoes the
-//                   HDF5 shuffle in registers (v_perm byte transposes), swaps
-//                   byte order, applies the compiled mask and reduces to
-//                   {sum, count, min, max}.  Replaces storage.py:51-100 per chunk.
-// k_tiles_to_chunks / k_combine : fixed-order combine of partials
-//                   (active.py:575-598), no atomics => deterministic.
-// k_reduce_axes   : partial-axis reduction (storage.py:98-100, axis ⊂ dims).
-// k_select        : method=None path (storage.py:95-96, returns data + mask).
-// k_unshuffle     : standalone filter reversal (storage.py:121-122).
+// pyas_kernels.hip — dtype dispatch of the kernel launchers, and the
+// standalone un-shuffle kernel.  The kernel templates are in pyas_kernels.hpp
+// and are instantiated per dtype by pyas_inst.hip.
 #include <hip/hip_runtime.h>
 
 #include "pyas_device.hpp"
 #include "pyas_internal.hpp"
 
 namespace pyas {
-
-// ---------------------------------------------------------------------------
-// vector un-shuffle: 16 consecutive elements from ES byte planes
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-    return __builtin_amdgcn_perm(hi, lo, sel);
-}
-__device__ __forceinline__ uint32_t word(const uint4 &v, int j) {
-    return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
-}
-// a,b,c,d hold byte 0,1,2,3 of four consecutive elements; returns the four
-// little-endian 32-bit words (8 v_perm_b32).
-__device__ __forceinline__ void transpose4(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
-                                           uint32_t e[4]) {
-    const uint32_t t0 = perm(b, a, 0x05010400u), t1 = perm(b, a, 0x07030602u);
-    const uint32_t u0 = perm(d, c, 0x05010400u), u1 = perm(d, c, 0x07030602u);
-    e[0] = perm(u0, t0, 0x05040100u);
-    e[1] = perm(u0, t0, 0x07060302u);
-    e[2] = perm(u1, t1, 0x05040100u);
-    e[3] = perm(u1, t1, 0x07060302u);
-}
-
-template <typename T, bool BSWAP>
-__device__ __forceinline__ void unshuffle16(const uint4 *pl, T out[16]) {
-    constexpr int ES = sizeof(T);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if constexpr (ES == 2) {
-            const uint32_t a = word(pl[BSWAP ? 1 : 0], j), b = word(pl[BSWAP ? 0 : 1], j);
-            const uint32_t w0 = perm(b, a, 0x05010400u), w1 = perm(b, a, 0x07030602u);
-            out[4 * j + 0] = bits_to<T>((uint16_t)(w0 & 0xffffu));
-            out[4 * j + 1] = bits_to<T>((uint16_t)(w0 >> 16));
-            out[4 * j + 2] = bits_to<T>((uint16_t)(w1 & 0xffffu));
-            out[4 * j + 3] = bits_to<T>((uint16_t)(w1 >> 16));
-        } else if constexpr (ES == 4) {
-            uint32_t e[4];
-            if (BSWAP) transpose4(word(pl[3], j), word(pl[2], j), word(pl[1], j), word(pl[0], j), e);
-            else transpose4(word(pl[0], j), word(pl[1], j), word(pl[2], j), word(pl[3], j), e);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) out[4 * j + k] = bits_to<T>(e[k]);
-        } else if constexpr (ES == 8) {
-            uint32_t lo[4], hi[4];
-            if (BSWAP) {
-                transpose4(word(pl[7], j), word(pl[6], j), word(pl[5], j), word(pl[4], j), lo);
-                transpose4(word(pl[3], j), word(pl[2], j), word(pl[1], j), word(pl[0], j), hi);
-            } else {
-                transpose4(word(pl[0], j), word(pl[1], j), word(pl[2], j), word(pl[3], j), lo);
-                transpose4(word(pl[4], j), word(pl[5], j), word(pl[6], j), word(pl[7], j), hi);
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                out[4 * j + k] = bits_to<T>(((uint64_t)hi[k] << 32) | (uint64_t)lo[k]);
-        }
-    }
-}
-
-// Streaming 16-B load; PYAS_NT=1 marks it non-temporal (read-once data).
-#ifndef PYAS_UNROLL
-#define PYAS_UNROLL 4
-#endif
-#ifndef PYAS_NT
-#define PYAS_NT 1   // measured: +7 % (C2) / +5 % (C3) over default-policy loads
-#endif
-__device__ __forceinline__ uint4 ldg16(const uint4 *p) {
-#if PYAS_NT
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-    return make_uint4(r.x, r.y, r.z, r.w);
-#else
-    return *p;
-#endif
-}
-
-// Raw 16 bytes of the plain layout -> 16/ES values
-template <typename T, bool BSWAP>
-__device__ __forceinline__ void unpack16(const uint4 &r, T *x) {
-    using U = typename TT<T>::U;
-    constexpr int N = 16 / sizeof(T);
-    U w[N];
-    __builtin_memcpy(w, &r, 16);
-#pragma unroll
-    for (int k = 0; k < N; ++k) x[k] = bits_to<T>(BSWAP ? bswap(w[k]) : w[k]);
-}
-
-template <typename T, bool BSWAP, bool MASKED, bool CONV>
-__device__ __forceinline__ void consume16(const uint4 &r, TileAcc<T> &acc, const MaskT<T> &mk) {
-    constexpr int N = 16 / sizeof(T);
-    T x[N];
-    unpack16<T, BSWAP>(r, x);
-    acc.template add_n<N, MASKED, CONV>(x, mk);
-}
-
-// ---------------------------------------------------------------------------
-// contiguous runs
-// ---------------------------------------------------------------------------
-// Plain layout, memory elements [m0, m1) of the chunk at `base`.  The body is
-// 16-B global loads, U per lane per step, register double-buffered so the
-// next step's loads are in flight while the current step is reduced.
-template <typename T, bool BSWAP, bool MASKED>
-__device__ void run_plain(const uint8_t *base, int64_t m0, int64_t m1, TileAcc<T> &acc,
-                          const MaskT<T> &mk) {
-    constexpr int ES = sizeof(T);
-    const int tid = threadIdx.x;
-    const int64_t b0 = m0 * ES, b1 = m1 * ES;               // byte range in the chunk
-    const int64_t mis = (int64_t)((uintptr_t)base & 15);
-    const int64_t a0 = ((b0 + mis + 15) & ~(int64_t)15) - mis;  // first 16-B aligned byte
-    const int64_t a1 = ((b1 + mis) & ~(int64_t)15) - mis;
-    if (a0 >= a1) {
-        for (int64_t i = m0 + tid; i < m1; i += kBlock) {
-            const T v = load_plain<T, BSWAP>(base, i);
-            acc.template add_n<1, MASKED, false>(&v, mk);
-        }
-        if (!MASKED) {} // counts of unmasked tiles are added by the caller
-        return;
-    }
-    const int64_t nhead = (a0 - b0) / ES, ntail = (b1 - a1) / ES;
-    if (tid < nhead) {
-        const T v = load_plain<T, BSWAP>(base, m0 + tid);
-        acc.template add_n<1, MASKED, false>(&v, mk);
-    }
-    if (tid < ntail) {
-        const T v = load_plain<T, BSWAP>(base, m1 - ntail + tid);
-        acc.template add_n<1, MASKED, false>(&v, mk);
-    }
-    const uint4 *v = reinterpret_cast<const uint4 *>(base + a0);  // keeps global provenance
-    const int64_t nvec = (a1 - a0) / 16;
-    constexpr int U = PYAS_UNROLL;
-    constexpr int64_t STEP = (int64_t)U * kBlock;
-    const int64_t nsteps = nvec / STEP;
-    if (nsteps > 0) {
-        uint4 cur[U], nxt[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = ldg16(v + tid + u * kBlock);
-        for (int64_t s = 0; s < nsteps; ++s) {
-            // prefetch the next step (clamped: the last step re-reads itself)
-            const int64_t ns = s + 1 < nsteps ? s + 1 : s;
-#pragma unroll
-            for (int u = 0; u < U; ++u) nxt[u] = ldg16(v + ns * STEP + tid + u * kBlock);
-#pragma unroll
-            for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED, true>(cur[u], acc, mk);
-#pragma unroll
-            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-        }
-    }
-    for (int64_t k = nsteps * STEP + tid; k < nvec; k += kBlock)
-        consume16<T, BSWAP, MASKED, false>(ldg16(v + k), acc, mk);
-}
-
-// Shuffled layout, chunk elements [i0, i1); n = elements in the chunk.
-template <typename T, bool BSWAP, bool MASKED>
-__device__ void run_shuffled(const uint8_t *base, int64_t n, int64_t i0, int64_t i1,
-                             TileAcc<T> &acc, const MaskT<T> &mk) {
-    constexpr int ES = sizeof(T);
-    const int tid = threadIdx.x;
-    const bool vec_ok = (((uintptr_t)base & 15) == 0) && ((n & 15) == 0);
-    const int64_t g0 = (i0 + 15) & ~(int64_t)15, g1 = i1 & ~(int64_t)15;
-    if (!vec_ok || g0 >= g1) {
-        for (int64_t i = i0 + tid; i < i1; i += kBlock) {
-            const T v = load_shuffled<T, BSWAP>(base, n, i);
-            acc.template add_n<1, MASKED, false>(&v, mk);
-        }
-        return;
-    }
-    if (tid < g0 - i0) {
-        const T v = load_shuffled<T, BSWAP>(base, n, i0 + tid);
-        acc.template add_n<1, MASKED, false>(&v, mk);
-    }
-    if (tid < i1 - g1) {
-        const T v = load_shuffled<T, BSWAP>(base, n, g1 + tid);
-        acc.template add_n<1, MASKED, false>(&v, mk);
-    }
-    const int64_t ng = (g1 - g0) / 16;
-    const int64_t nfull = ng / kBlock * kBlock;
-    for (int64_t g = tid; g < ng; g += kBlock) {
-        const int64_t i = g0 + g * 16;
-        uint4 pl[ES];
-#pragma unroll
-        for (int b = 0; b < ES; ++b) pl[b] = ldg16(reinterpret_cast<const uint4 *>(base + (int64_t)b * n + i));
-        T x[16];
-        unshuffle16<T, BSWAP>(pl, x);
-        if (g < nfull) acc.template add_n<16, MASKED, false>(x, mk);
-        else acc.template add_n<16, MASKED, false>(x, mk);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// generic (strided / listed / table-masked) selections
-// ---------------------------------------------------------------------------
-struct Decomp {
-    int64_t mem;
-    int64_t v[2];
-};
-
-// Decompose position e (row-major over the dims whose bit is in dmask) into
-// chunk memory index and table indices.
-__device__ __forceinline__ void decompose(const Sel &s, const int32_t *pool, const int64_t *cstride,
-                                          const MaskTab &tab, int ndim, uint32_t dmask,
-                                          int64_t e, Decomp &o) {
-#pragma unroll
-    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-        if (d < ndim && ((dmask >> d) & 1u)) {
-            const int64_t cd = s.cnt[d];
-            const int64_t q = e / cd, k = e - q * cd;
-            e = q;
-            o.mem += sel_index(s, pool, d, k) * cstride[d];
-            o.v[0] += k * tab.stride[0][d];
-            o.v[1] += k * tab.stride[1][d];
-        }
-    }
-}
-
-template <typename T>
-__device__ __forceinline__ bool all_masked(const MaskT<T> &mk, const MaskTab &tab, const Decomp &o, T x) {
-    bool m = mk.masked(x);
-    if (tab.on[0]) m |= tab_masked<T>(tab, 0, o.v[0], x);
-    if (tab.on[1]) m |= tab_masked<T>(tab, 1, o.v[1], x);
-    return m;
-}
-
-// Mixed-radix position counter over the selected box (innermost dim
-// fastest).  Divisions happen once per thread; every step of `stride`
-// elements is then a carry-propagating add per dim (no division).
-struct RadixCounter {
-    uint32_t idx[PYAS_MAX_DIMS], inc[PYAS_MAX_DIMS], cnt[PYAS_MAX_DIMS];
-    __device__ __forceinline__ void init(const Sel &s, int ndim, uint32_t dmask, uint64_t start,
-                                         uint64_t stride) {
-#pragma unroll
-        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-            const bool on = d < ndim && ((dmask >> d) & 1u);
-            const uint32_t c = on ? (uint32_t)s.cnt[d] : 1u;
-            cnt[d] = c;
-            idx[d] = (uint32_t)(start % c);
-            start /= c;
-            inc[d] = (uint32_t)(stride % c);
-            stride /= c;
-        }
-    }
-    __device__ __forceinline__ void advance() {
-        uint32_t carry = 0;
-#pragma unroll
-        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-            const uint32_t x = idx[d] + inc[d] + carry;
-            carry = x >= cnt[d] ? 1u : 0u;
-            idx[d] = carry ? x - cnt[d] : x;
-        }
-    }
-    __device__ __forceinline__ void locate(const Sel &s, const int32_t *pool, const int64_t *cstride,
-                                           const MaskTab &tab, int ndim, uint32_t dmask,
-                                           Decomp &o) const {
-#pragma unroll
-        for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
-            if (d < ndim && ((dmask >> d) & 1u)) {
-                o.mem += sel_index(s, pool, d, idx[d]) * cstride[d];
-                o.v[0] += (int64_t)idx[d] * tab.stride[0][d];
-                o.v[1] += (int64_t)idx[d] * tab.stride[1][d];
-            }
-        }
-    }
-};
-
-template <typename T, bool SHUF, bool BSWAP, bool MASKED>
-__device__ void run_generic(const ReduceArgs &a, const uint8_t *base, const Sel &s, int64_t e0,
-                            int64_t e1, TileAcc<T> &acc, const MaskT<T> &mk) {
-    const uint32_t all = (1u << a.ndim) - 1u;
-    RadixCounter rc;
-    rc.init(s, a.ndim, all, (uint64_t)(e0 + threadIdx.x), (uint64_t)kBlock);
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
-        Decomp o{0, {0, 0}};
-        rc.locate(s, a.pool, a.cstride, a.tab, a.ndim, all, o);
-        const T x = load_elem<T, SHUF, BSWAP>(base, a.chunk_elems, o.mem);
-        acc.add_one(x, MASKED ? all_masked(mk, a.tab, o, x) : false);
-        rc.advance();
-    }
-}
-
-// Box-like selections whose innermost part is a contiguous run of L
-// elements (dims > k full, dim k unit step): stream each run as 16-B vectors.
-// Work items are (outer index of dims < k, vector within the run), walked by
-// a radix counter, U independent 16-B loads in flight per lane.
-template <typename T, bool BSWAP, bool MASKED>
-__device__ void run_rows(const ReduceArgs &a, const uint8_t *base, const Sel &s, int k, int64_t L,
-                         int64_t e0, int64_t e1, TileAcc<T> &acc, const MaskT<T> &mk) {
-    constexpr int N = 16 / sizeof(T);
-    const int64_t V = L / N;                       // vectors per run
-    const int64_t q0 = e0 / N, q1 = e1 / N;        // vector range of this tile
-    // radix over (dims 0..k-1, vector) with the vector as the fastest digit
-    Sel rs = s;
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
-        if (d == k) rs.cnt[d] = (int32_t)V;
-        else if (d > k) rs.cnt[d] = 1;
-    }
-    const uint32_t dm = (2u << k) - 1u;            // dims 0..k
-    int64_t inner0 = 0;
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-        if (d == k) inner0 = (int64_t)s.start[d] * a.cstride[d];
-    RadixCounter rc;
-    rc.init(rs, a.ndim, dm, (uint64_t)(q0 + threadIdx.x), (uint64_t)kBlock);
-    auto addr = [&](const RadixCounter &r) -> const uint4 * {
-        int64_t mem = inner0;
-#pragma unroll
-        for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-            if (d < k) mem += sel_index(s, a.pool, d, r.idx[d]) * a.cstride[d];
-        uint32_t v = 0;
-#pragma unroll
-        for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-            if (d == k) v = r.idx[d];
-        return reinterpret_cast<const uint4 *>(base + (mem + (int64_t)v * N) * (int64_t)sizeof(T));
-    };
-    constexpr int U = 4;
-    int64_t q = q0 + threadIdx.x;
-    // converged part: every lane has U full items
-    const int64_t nfull = ((q1 - q0) / (U * kBlock)) * (U * kBlock);
-    for (int64_t it = 0; it < nfull; it += U * kBlock) {
-        const uint4 *p[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) { p[u] = addr(rc); rc.advance(); }
-        uint4 r[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) r[u] = ldg16(p[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED, true>(r[u], acc, mk);
-        q += U * kBlock;
-    }
-    for (; q < q1; q += kBlock) {
-        consume16<T, BSWAP, MASKED, false>(ldg16(addr(rc)), acc, mk);
-        rc.advance();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// the hot kernel
-// ---------------------------------------------------------------------------
-// SEL = false: every chunk fully selected (batch.sel == NULL) -> a lean
-// streaming-only kernel (no selection state, high occupancy).
-template <typename T, bool SHUF, bool BSWAP, bool MASKED, bool SEL>
-__global__ __launch_bounds__(kBlock) void k_reduce(ReduceArgs a) {
-    const int64_t b = blockIdx.x;
-    const int64_t c = b / a.tpc;
-    const int64_t t = b - c * a.tpc;
-    const uint8_t *base = a.data + a.offsets[c];
-    MaskT<T> mk;
-    if constexpr (MASKED) mk.init(a.mask);
-    TileAcc<T> acc;
-    acc.init();
-    if constexpr (!SEL) {
-        int64_t per = (a.chunk_elems + a.tpc - 1) / a.tpc;
-        per = (per + 63) & ~(int64_t)63;
-        const int64_t e0 = t * per, e1 = e0 + per < a.chunk_elems ? e0 + per : a.chunk_elems;
-        if (e0 < e1) {
-            if constexpr (SHUF && sizeof(T) > 1)
-                run_shuffled<T, BSWAP, MASKED>(base, a.chunk_elems, e0, e1, acc, mk);
-            else
-                run_plain<T, BSWAP, MASKED>(base, e0, e1, acc, mk);
-        }
-        tile_finish(acc, (!MASKED && e0 < e1) ? (uint64_t)(e1 - e0) : 0u, a.out + b);
-        return;
-    }
-    Sel s;
-    load_sel(s, a.sel, c, a.ndim, a.shape);
-    int64_t total = 1;
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d) total *= (int64_t)s.cnt[d];
-    int64_t per = (total + a.tpc - 1) / a.tpc;
-    per = (per + 63) & ~(int64_t)63;
-    const int64_t e0 = t * per, e1 = e0 + per < total ? e0 + per : total;
-    bool generic = false;
-    if (e0 < e1) {
-        // Is the selection one contiguous run of chunk memory?  (innermost
-        // non-full dim has unit step; every dim outside it picks one index)
-        bool contig = !(a.tab.on[0] || a.tab.on[1]);
-        bool seen_partial = false;
-        int64_t m0 = 0;
-#pragma unroll
-        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-            if (d < a.ndim) {
-                const bool full = s.step[d] == 1 && s.start[d] == 0 && (int64_t)s.cnt[d] == a.shape[d];
-                if (seen_partial) {
-                    if (s.cnt[d] > 1) contig = false;
-                } else if (!full) {
-                    seen_partial = true;
-                    if (s.cnt[d] > 1 && s.step[d] != 1) contig = false;
-                }
-                if (s.cnt[d] > 0) m0 += sel_index(s, a.pool, d, 0) * a.cstride[d];
-            }
-        }
-        if (contig) {
-            if constexpr (SHUF && sizeof(T) > 1)
-                run_shuffled<T, BSWAP, MASKED>(base, a.chunk_elems, m0 + e0, m0 + e1, acc, mk);
-            else
-                run_plain<T, BSWAP, MASKED>(base, m0 + e0, m0 + e1, acc, mk);
-        } else {
-            // rows of 16-B vectors?  (no shuffle/tables, unit-step innermost
-            // partial dim k, everything 16-B aligned)
-            constexpr int64_t ES = sizeof(T);
-            int k = -1;
-            int64_t L = 1;
-            bool rows = !SHUF && !(a.tab.on[0] || a.tab.on[1]) && ((uintptr_t)base & 15) == 0;
-#pragma unroll
-            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-                if (d < a.ndim) {
-                    if (k < 0) {
-                        const bool full = s.step[d] == 1 && s.start[d] == 0 &&
-                                          (int64_t)s.cnt[d] == a.shape[d];
-                        if (!full) {
-                            k = d;
-                            if (s.step[d] != 1) rows = false;
-                            if (((int64_t)s.start[d] * a.cstride[d] * ES) % 16 != 0) rows = false;
-                            L *= s.cnt[d];
-                        } else {
-                            L *= a.shape[d];
-                        }
-                    } else if ((a.cstride[d] * ES) % 16 != 0) {
-                        rows = false;  // an outer dim whose rows start unaligned
-                    }
-                }
-            }
-            if (k < 0 || (L * ES) % 16 != 0) rows = false;
-            if (rows) {
-                run_rows<T, BSWAP, MASKED>(a, base, s, k, L, e0, e1, acc, mk);
-            } else {
-                generic = true;
-                run_generic<T, SHUF, BSWAP, MASKED>(a, base, s, e0, e1, acc, mk);
-            }
-        }
-    }
-    // unmasked contiguous tiles count every element; the generic path counts itself
-    const uint64_t extra = (!MASKED && !generic && e0 < e1) ? (uint64_t)(e1 - e0) : 0u;
-    tile_finish(acc, extra, a.out + b);
-}
-
-// ---------------------------------------------------------------------------
-// combines (fixed order)
-// ---------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ typename TT<T>::Acc sum_of(const pyas_scalar &s, bool round) {
-    using A = typename TT<T>::Acc;
-    if constexpr (TT<T>::kind == 0) return round ? (A)(T)s.f : (A)s.f;
-    else if constexpr (TT<T>::kind == 1) return round ? (A)(T)s.i : (A)s.i;
-    else return round ? (A)(T)s.u : (A)s.u;
-}
-
-template <typename T>
-__device__ __forceinline__ void merge(WAcc<T> &acc, const pyas_partial &p, bool round) {
-    acc.sum += sum_of<T>(p.sum, round);
-    if (p.count > 0) {
-        acc.count += p.count;
-        acc.mn = pmin(acc.mn, TT<T>::from(p.min));
-        acc.mx = pmax(acc.mx, TT<T>::from(p.max));
-    }
-}
-
-// tiles -> chunks: one wave per chunk
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_tiles_to_chunks(const pyas_partial *tiles, int64_t tpc,
-                                                            int64_t n_chunks, pyas_partial *out) {
-    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-    const int lane = threadIdx.x & (kWave - 1);
-    if (c >= n_chunks) return;  // wave-uniform
-    WAcc<T> acc;
-    acc.init();
-    for (int64_t t = lane; t < tpc; t += kWave) merge(acc, tiles[c * tpc + t], false);
-    wave_reduce(acc);
-    if (lane == 0) store_wpartial(out + c, acc);
-}
-
-// n partials -> one per block (contiguous segments), fixed order
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_combine(const pyas_partial *in, int64_t n, int64_t seg,
-                                                    uint32_t flags, pyas_partial *out) {
-    const int64_t lo = (int64_t)blockIdx.x * seg;
-    const int64_t hi = lo + seg < n ? lo + seg : n;
-    const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
-    WAcc<T> acc;
-    acc.init();
-    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) merge(acc, in[i], round);
-    block_reduce_w(acc);
-    if (threadIdx.x == 0) store_wpartial(out + blockIdx.x, acc);
-}
-
-// segmented combine: one thread per output segment, sequential fixed order
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_combine_segments(const pyas_partial *in, const int64_t *index,
-                                                             const int64_t *seg, int64_t n_seg,
-                                                             uint32_t flags, pyas_partial *out) {
-    const int64_t sidx = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (sidx >= n_seg) return;
-    const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
-    WAcc<T> acc;
-    acc.init();
-    for (int64_t k = seg[sidx]; k < seg[sidx + 1]; ++k) merge(acc, in[index[k]], round);
-    store_wpartial(out + sidx, acc);
-}
-
-// ---------------------------------------------------------------------------
-// partial-axis reduction (axis ⊂ dims), one thread per output element
-// ---------------------------------------------------------------------------
-// Two layouts, chosen by the host:
-//  column (a.row == false; innermost selected dim kept): a workgroup holds
-//    OT = 256/S outputs x S splits of the reduced range; lanes with the same
-//    split hold consecutive outputs (consecutive addresses); the S partials of
-//    an output are folded through LDS in split order (deterministic);
-//  row (a.row; innermost dim reduced): G lanes per output (G a power of two,
-//    about 8 elements per lane), 64/G outputs per wave, lanes of a group read
-//    consecutive addresses, then a segmented shuffle reduce inside the group.
-// Both walk index spaces with radix counters (no per-element division) and
-// keep 4 independent loads in flight per lane.
-template <typename T, int U, bool SHUF, bool BSWAP>
-__device__ __forceinline__ void axes_walk(const ReduceArgs &r, const uint8_t *base, const Sel &s,
-                                          uint32_t red, const Decomp &base_o, RadixCounter &rc,
-                                          int64_t q0, int64_t n_red, int64_t stride, bool tabs,
-                                          const MaskT<T> &mk, TileAcc<T> &acc) {
-    int64_t q = q0;
-    const int64_t nfull = q0 + ((n_red - q0 + stride - 1) / stride) / U * U * stride;
-    for (; q < nfull; q += U * stride) {
-        Decomp od[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            od[u] = base_o;
-            rc.locate(s, r.pool, r.cstride, r.tab, r.ndim, red, od[u]);
-            rc.advance();
-        }
-        T x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = load_elem<T, SHUF, BSWAP>(base, r.chunk_elems, od[u].mem);
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc.add_one(x[u], tabs ? all_masked(mk, r.tab, od[u], x[u]) : mk.masked(x[u]));
-    }
-    for (; q < n_red; q += stride) {
-        Decomp od = base_o;
-        rc.locate(s, r.pool, r.cstride, r.tab, r.ndim, red, od);
-        const T x = load_elem<T, SHUF, BSWAP>(base, r.chunk_elems, od.mem);
-        acc.add_one(x, tabs ? all_masked(mk, r.tab, od, x) : mk.masked(x));
-        rc.advance();
-    }
-}
-
-// Same walk with the reduced-index -> element-offset map precomputed in LDS
-// (no tables): per element one LDS read, one add, one load; U in flight.
-template <typename T, int U, bool SHUF, bool BSWAP>
-__device__ __forceinline__ void axes_walk_lds(const uint8_t *base, int64_t chunk_elems,
-                                              const int32_t *roff, int64_t base_mem, int64_t q0,
-                                              int64_t n_red, int64_t stride, const MaskT<T> &mk,
-                                              TileAcc<T> &acc) {
-    int64_t q = q0;
-    const int64_t nfull = q0 + ((n_red - q0 + stride - 1) / stride) / U * U * stride;
-    for (; q < nfull; q += U * stride) {
-        T x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            x[u] = load_elem<T, SHUF, BSWAP>(base, chunk_elems, base_mem + roff[q + u * stride]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) acc.add_one(x[u], mk.masked(x[u]));
-    }
-    for (; q < n_red; q += stride) {
-        const T x = load_elem<T, SHUF, BSWAP>(base, chunk_elems, base_mem + roff[q]);
-        acc.add_one(x, mk.masked(x));
-    }
-}
-
-
-// Fold the S split partials of each of OT outputs through LDS in split order
-// (deterministic); thread (ol, sp=0) ends with the folded value.
-template <typename T>
-__device__ __forceinline__ void fold_splits(TileAcc<T> &acc, int S, int OT, int ol, int sp) {
-    __shared__ typename TT<T>::Acc l_sum[kBlock];
-    __shared__ uint32_t l_cnt[kBlock];
-    __shared__ T l_mn[kBlock], l_mx[kBlock];
-    __shared__ uint8_t l_nan[kBlock];
-    const int t = threadIdx.x;
-    l_sum[t] = acc.sum; l_cnt[t] = acc.count; l_mn[t] = acc.mn; l_mx[t] = acc.mx;
-    l_nan[t] = acc.nan ? 1 : 0;
-    __syncthreads();
-    if (sp == 0) {
-        for (int k = 1; k < S; ++k) {
-            const int u = k * OT + ol;
-            acc.sum += l_sum[u];
-            acc.count += l_cnt[u];
-            acc.mn = tmin(acc.mn, l_mn[u]);
-            acc.mx = tmax(acc.mx, l_mx[u]);
-            acc.nan = acc.nan || l_nan[u];
-        }
-    }
-    __syncthreads();
-}
-
-template <typename T, bool SHUF, bool BSWAP>
-__device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
-                           const Sel &s, uint32_t red, uint32_t keep, int64_t n_out, int64_t n_red,
-                           const MaskT<T> &mk, int32_t *roff) {
-    const ReduceArgs &r = a.r;
-    constexpr int ES = sizeof(T), N = 16 / ES;
-    const bool tabs = r.tab.on[0] || r.tab.on[1];
-    const bool use_lds = !tabs && n_red <= kAxesLds;
-    // 16-B vector modes: the last chunk dim is a unit-step, 16-B aligned run
-    const int last = r.ndim - 1;
-    int64_t cnt_last = 1, start_last = 0, step_last = 1, shape_last = 1;
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-        if (d == last) { cnt_last = s.cnt[d]; start_last = s.start[d]; step_last = s.step[d]; shape_last = r.shape[d]; }
-    const bool vec_ok = use_lds && !SHUF && ES >= 4 && step_last == 1 && ((uintptr_t)base & 15) == 0 &&
-                        (cnt_last * ES) % 16 == 0 && (start_last * ES) % 16 == 0 && (shape_last * ES) % 16 == 0;
-    const bool row_vec = a.row && a.vec && vec_ok;
-    const bool col_vec = !a.row && a.vec && vec_ok;
-    if (use_lds) {   // reduced-index -> element offset, once per workgroup
-        const int64_t nq = row_vec ? n_red / N : n_red;
-        const uint64_t m = row_vec ? N : 1;
-        RadixCounter t;   // one decomposition per thread, then digit adds
-        t.init(s, r.ndim, red, threadIdx.x * m, kBlock * m);
-        for (int64_t q = threadIdx.x; q < nq; q += kBlock) {
-            Decomp d{0, {0, 0}};
-            t.locate(s, r.pool, r.cstride, r.tab, r.ndim, red, d);
-            roff[q] = (int32_t)d.mem;
-            t.advance();
-        }
-        __syncthreads();
-    }
-    if (!a.row) {
-        const int S = a.split, OT = kBlock / S;
-        const int ol = threadIdx.x % OT, sp = threadIdx.x / OT;
-        const int64_t n_items = col_vec ? n_out / N : n_out;   // outputs or N-output vectors
-        const uint64_t m = col_vec ? N : 1;
-        RadixCounter ko;   // kept-index counter stepping with the loop
-        ko.init(s, r.ndim, keep, (uint64_t)(j * OT + ol) * m, (uint64_t)(a.bpc * OT) * m);
-        for (int64_t o0 = j * OT; o0 < n_items; o0 += a.bpc * OT) {   // block-uniform loop
-            const int64_t oi = o0 + ol;
-            Decomp base_o{0, {0, 0}};
-            if (oi < n_items) ko.locate(s, r.pool, r.cstride, r.tab, r.ndim, keep, base_o);
-            ko.advance();
-            if (col_vec) {
-                TileAcc<T> acc[N];
-#pragma unroll
-                for (int k = 0; k < N; ++k) acc[k].init();
-                if (oi < n_items) {
-                    const uint8_t *bo = base + base_o.mem * ES;
-                    constexpr int U = 4;
-                    int64_t q = sp;
-                    const int64_t nfull = sp + ((n_red - sp + S - 1) / S) / U * U * S;
-                    for (; q < nfull; q += U * S) {
-                        uint4 v[U];
-#pragma unroll
-                        for (int u = 0; u < U; ++u)
-                            v[u] = ldg16(reinterpret_cast<const uint4 *>(bo + (int64_t)roff[q + u * S] * ES));
-#pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            T x[N];
-                            unpack16<T, BSWAP>(v[u], x);
-#pragma unroll
-                            for (int k = 0; k < N; ++k) acc[k].add_one(x[k], mk.masked(x[k]));
-                        }
-                    }
-                    for (; q < n_red; q += S) {
-                        T x[N];
-                        unpack16<T, BSWAP>(ldg16(reinterpret_cast<const uint4 *>(bo + (int64_t)roff[q] * ES)), x);
-#pragma unroll
-                        for (int k = 0; k < N; ++k) acc[k].add_one(x[k], mk.masked(x[k]));
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < N; ++k) {
-                    if (S > 1) fold_splits(acc[k], S, OT, ol, sp);
-                    if (sp == 0 && oi < n_items) tile_store_lane(acc[k], a.out + a.out_offsets[c] + oi * N + k);
-                }
-                continue;
-            }
-            TileAcc<T> acc;
-            acc.init();
-            if (oi < n_items) {
-                if (use_lds) {
-                    axes_walk_lds<T, 8, SHUF, BSWAP>(base, r.chunk_elems, roff, base_o.mem, sp, n_red, S, mk, acc);
-                } else {
-                    RadixCounter rc;
-                    rc.init(s, r.ndim, red, (uint64_t)sp, (uint64_t)S);
-                    axes_walk<T, 4, SHUF, BSWAP>(r, base, s, red, base_o, rc, sp, n_red, S, tabs, mk, acc);
-                }
-            }
-            if (S > 1) fold_splits(acc, S, OT, ol, sp);
-            if (sp == 0 && oi < n_items) tile_store_lane(acc, a.out + a.out_offsets[c] + oi);
-        }
-    } else {
-        // G lanes per output (host-sized for element or 16-B vector walks)
-        const int G = a.group;
-        const int lane = threadIdx.x & (kWave - 1);
-        const int gl = lane & (G - 1);
-        const int64_t per_wave = kWave / G;
-        const int64_t wave = (int64_t)j * (kBlock / kWave) + threadIdx.x / kWave;
-        const int64_t nwaves = (int64_t)a.bpc * (kBlock / kWave);
-        RadixCounter ko;   // kept-index counter stepping with the loop
-        ko.init(s, r.ndim, keep, (uint64_t)(wave * per_wave + lane / G), (uint64_t)(nwaves * per_wave));
-        for (int64_t o0 = wave * per_wave; o0 < n_out; o0 += nwaves * per_wave) {  // wave-uniform
-            const int64_t o = o0 + lane / G;
-            TileAcc<T> acc;
-            acc.init();
-            Decomp base_o{0, {0, 0}};
-            if (o < n_out) ko.locate(s, r.pool, r.cstride, r.tab, r.ndim, keep, base_o);
-            ko.advance();
-            if (o < n_out) {
-                if (row_vec) {
-                    const uint8_t *bo = base + base_o.mem * ES;
-                    const int64_t nv = n_red / N;
-                    constexpr int U = 4;
-                    int64_t q = gl;
-                    const int64_t nfull = gl + ((nv - gl + G - 1) / G) / U * U * G;
-                    for (; q < nfull; q += U * G) {
-                        uint4 v[U];
-#pragma unroll
-                        for (int u = 0; u < U; ++u)
-                            v[u] = ldg16(reinterpret_cast<const uint4 *>(bo + (int64_t)roff[q + u * G] * ES));
-#pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            T x[N];
-                            unpack16<T, BSWAP>(v[u], x);
-                            acc.template add_n<N, true, false>(x, mk);
-                        }
-                    }
-                    for (; q < nv; q += G) {
-                        T x[N];
-                        unpack16<T, BSWAP>(ldg16(reinterpret_cast<const uint4 *>(bo + (int64_t)roff[q] * ES)), x);
-                        acc.template add_n<N, true, false>(x, mk);
-                    }
-                } else if (use_lds) {
-                    axes_walk_lds<T, 8, SHUF, BSWAP>(base, r.chunk_elems, roff, base_o.mem, gl, n_red, G, mk, acc);
-                } else {
-                    RadixCounter rc;
-                    rc.init(s, r.ndim, red, (uint64_t)gl, (uint64_t)G);
-                    axes_walk<T, 4, SHUF, BSWAP>(r, base, s, red, base_o, rc, gl, n_red, G, tabs, mk, acc);
-                }
-            }
-            group_finish(acc, G, (o < n_out && gl == 0) ? a.out + a.out_offsets[c] + o : nullptr);
-        }
-    }
-}
-
-template <typename T, bool SHUF, bool BSWAP>
-__global__ __launch_bounds__(kBlock) void k_reduce_axes(AxesArgs a) {
-    __shared__ int32_t roff[kAxesLds];
-    const int64_t c = blockIdx.x / a.bpc;
-    const int64_t j = blockIdx.x - c * a.bpc;
-    const ReduceArgs &r = a.r;
-    const uint8_t *base = r.data + r.offsets[c];
-    MaskT<T> mk;
-    mk.init(r.mask);
-    Sel s;
-    load_sel(s, r.sel, c, r.ndim, r.shape);
-    const uint32_t all = (1u << r.ndim) - 1u;
-    const uint32_t red = a.axes & all, keep = all & ~red;
-    int64_t n_out = 1, n_red = 1;
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
-        if (d < r.ndim) {
-            if ((red >> d) & 1u) n_red *= s.cnt[d];
-            else n_out *= s.cnt[d];
-        }
-    }
-    axes_block<T, SHUF, BSWAP>(a, c, j, base, s, red, keep, n_out, n_red, mk, roff);
-}
-
-// ---------------------------------------------------------------------------
-// method=None: select + mask into dense outputs
-// ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_select(SelectArgs a) {
-    const int64_t c = blockIdx.x / a.bpc;
-    const int64_t j = blockIdx.x - c * a.bpc;
-    const ReduceArgs &r = a.r;
-    const uint8_t *base = r.data + r.offsets[c];
-    MaskT<T> mk;
-    mk.init(r.mask);
-    Sel s;
-    load_sel(s, r.sel, c, r.ndim, r.shape);
-    int64_t total = 1;
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d) total *= s.cnt[d];
-    const uint32_t all = (1u << r.ndim) - 1u;
-    T *vals = reinterpret_cast<T *>(a.values) + a.out_offsets[c];
-    uint8_t *msk = a.mask_out ? a.mask_out + a.out_offsets[c] : nullptr;
-    for (int64_t e = j * kBlock + threadIdx.x; e < total; e += a.bpc * kBlock) {
-        Decomp o{0, {0, 0}};
-        decompose(s, r.pool, r.cstride, r.tab, r.ndim, all, e, o);
-        const T x = load_elem_rt<T>(base, r.chunk_elems, o.mem, a.shuf, a.bswap);
-        vals[e] = x;
-        if (msk) msk[e] = all_masked(mk, r.tab, o, x) ? 1 : 0;
-    }
-}
 
 __global__ __launch_bounds__(kBlock) void k_unshuffle(const uint8_t *src, uint8_t *dst, int64_t nbytes,
                                                       int64_t es) {
@@ -815,38 +21,6 @@ __global__ __launch_bounds__(kBlock) void k_unshuffle(const uint8_t *src, uint8_
             dst[q] = src[q];
         }
     }
-}
-
-// ---------------------------------------------------------------------------
-// launchers
-// ---------------------------------------------------------------------------
-template <typename T, bool SEL>
-static void launch_reduce_ts(const ReduceArgs &a, bool shuf, bool bsw, bool masked, dim3 g,
-                             hipStream_t st) {
-    const dim3 blk(kBlock);
-#define PYAS_L(S, B, M) hipLaunchKernelGGL((k_reduce<T, S, B, M, SEL>), g, blk, 0, st, a)
-    if constexpr (sizeof(T) == 1) {
-        if (masked) PYAS_L(false, false, true);
-        else PYAS_L(false, false, false);
-    } else {
-        if (shuf) {
-            if (bsw) { if (masked) PYAS_L(true, true, true); else PYAS_L(true, true, false); }
-            else { if (masked) PYAS_L(true, false, true); else PYAS_L(true, false, false); }
-        } else {
-            if (bsw) { if (masked) PYAS_L(false, true, true); else PYAS_L(false, true, false); }
-            else { if (masked) PYAS_L(false, false, true); else PYAS_L(false, false, false); }
-        }
-    }
-#undef PYAS_L
-}
-
-template <typename T>
-static hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool masked,
-                                  int64_t grid, hipStream_t st) {
-    const dim3 g((unsigned)grid);
-    if (a.sel) launch_reduce_ts<T, true>(a, shuf, bsw, masked, g, st);
-    else launch_reduce_ts<T, false>(a, shuf, bsw, masked, g, st);
-    return hipGetLastError();
 }
 
 #define PYAS_DISPATCH_T(DT, CALL)                                  \
@@ -866,59 +40,36 @@ static hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool
 
 hipError_t launch_reduce(int dtype, const ReduceArgs &a, bool shuf, bool bsw, bool masked,
                          int64_t grid, hipStream_t st) {
-    hipError_t e = hipSuccess;
-    PYAS_DISPATCH_T(dtype, e = launch_reduce_t<T>(a, shuf, bsw, masked, grid, st));
-    return e;
+    PYAS_DISPATCH_T(dtype, return launch_reduce_t<T>(a, shuf, bsw, masked, grid, st));
+    return hipErrorInvalidValue;
 }
 
-hipError_t launch_tiles_to_chunks(int dtype, const pyas_partial *tiles, int64_t tpc, int64_t n_chunks,
-                                  pyas_partial *out, hipStream_t st) {
-    const int per_block = kBlock / kWave;
-    const dim3 g((unsigned)((n_chunks + per_block - 1) / per_block)), blk(kBlock);
-    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_tiles_to_chunks<T>), g, blk, 0, st, tiles, tpc,
-                                              n_chunks, out));
-    return hipGetLastError();
+hipError_t launch_finish(int dtype, const FinishArgs &f, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_finish_t<T>(f, st));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_combine(int dtype, const pyas_partial *in, int64_t n, int64_t seg, int64_t nblocks,
                           uint32_t flags, pyas_partial *out, hipStream_t st) {
-    const dim3 g((unsigned)nblocks), blk(kBlock);
-    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_combine<T>), g, blk, 0, st, in, n, seg, flags, out));
-    return hipGetLastError();
+    PYAS_DISPATCH_T(dtype, return launch_combine_t<T>(in, n, seg, nblocks, flags, out, st));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int64_t *index,
                                    const int64_t *seg, int64_t n_seg, uint32_t flags,
                                    pyas_partial *out, hipStream_t st) {
-    const dim3 g((unsigned)((n_seg + kBlock - 1) / kBlock)), blk(kBlock);
-    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_combine_segments<T>), g, blk, 0, st, in, index, seg,
-                                              n_seg, flags, out));
-    return hipGetLastError();
-}
-
-template <typename T>
-static void launch_axes_t(const AxesArgs &a, dim3 g, hipStream_t st) {
-    const dim3 blk(kBlock);
-    if constexpr (sizeof(T) == 1) {
-        hipLaunchKernelGGL((k_reduce_axes<T, false, false>), g, blk, 0, st, a);
-    } else {
-        if (a.shuf && a.bswap) hipLaunchKernelGGL((k_reduce_axes<T, true, true>), g, blk, 0, st, a);
-        else if (a.shuf) hipLaunchKernelGGL((k_reduce_axes<T, true, false>), g, blk, 0, st, a);
-        else if (a.bswap) hipLaunchKernelGGL((k_reduce_axes<T, false, true>), g, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_reduce_axes<T, false, false>), g, blk, 0, st, a);
-    }
+    PYAS_DISPATCH_T(dtype, return launch_combine_segments_t<T>(in, index, seg, n_seg, flags, out, st));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st) {
-    const dim3 g((unsigned)grid);
-    PYAS_DISPATCH_T(dtype, launch_axes_t<T>(a, g, st));
-    return hipGetLastError();
+    PYAS_DISPATCH_T(dtype, return launch_axes_t<T>(a, grid, st));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st) {
-    const dim3 g((unsigned)grid), blk(kBlock);
-    PYAS_DISPATCH_T(dtype, hipLaunchKernelGGL((k_select<T>), g, blk, 0, st, a));
-    return hipGetLastError();
+    PYAS_DISPATCH_T(dtype, return launch_select_t<T>(a, grid, st));
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es, hipStream_t st) {

@@ -105,6 +105,12 @@ class Context:
     def set_tile_bytes(self, nbytes: int) -> None:
         _lib.check(self.lib.pyas_ctx_set_tile_bytes(self.handle, int(nbytes)), "set_tile_bytes")
 
+    def set_chained_combine(self, on: bool) -> None:
+        """Fold tiles -> chunks -> total in the reduce kernel's tail (default)
+        or in separate combine launches; results are bit-identical."""
+        _lib.check(self.lib.pyas_ctx_set_chained_combine(self.handle, 1 if on else 0),
+                   "set_chained_combine")
+
 
 def get_context(device: int = 0) -> Context:
     with _ctx_lock:
