@@ -20,6 +20,8 @@
  *     decode = numcodecs.Zlib (hdf2numcodec:34-35)  |   one wave per chunk)
  *   activestorage/storage.py:126-153 mask_missing   | pyas_mask (thresholds are
  *                                                   |   pre-compiled on the host)
+ *   activestorage/storage.py:51-53,156-162 open +   | pyas_read_ranges (pread
+ *     read_block, once per chunk                    |   ring -> pinned -> H2D)
  *   activestorage/active.py:557-598 thread-pool     | pyas_reduce_chunks with a
  *     fan-out + out[...] assembly + method(out)     |   `total` output, and
  *                                                   |   pyas_combine_partials
@@ -54,7 +56,8 @@ typedef enum {
     PYAS_ENOTSUP = 2,     /* unsupported dtype/filter (NotImplementedError)  */
     PYAS_EDEVICE = 3,     /* HIP runtime / launch failure                    */
     PYAS_ENOMEM = 4,      /* device allocation failed                        */
-    PYAS_EINDEX = 5       /* selection out of the chunk (IndexError)         */
+    PYAS_EINDEX = 5,      /* selection out of the chunk (IndexError)         */
+    PYAS_EIO = 6          /* file read failed or ended early (OSError)       */
 } pyas_status;
 
 /* netCDF-4 numeric types (the 10 the format defines) */
@@ -250,6 +253,24 @@ int pyas_inflate(pyas_ctx *ctx, const uint8_t *src, const int64_t *src_offsets,
                  const int64_t *src_sizes, int64_t n, uint8_t *dst,
                  const int64_t *dst_offsets, const int64_t *dst_capacity,
                  int64_t *out_sizes, int32_t *status, void *stream);
+
+/* ---- host ingest (row f2) ------------------------------------------------ */
+/* Positioned reads of n byte ranges of an open file straight into device
+ * memory.  Replaces the reference's per-chunk open + read_block
+ * (storage.py:51-53, :156-162) run on active.py:557's 30-thread pool.
+ * Range i is file[file_offsets[i] .. + sizes[i]) and lands at
+ * dst + dst_offsets[i] (dst: device).  `threads` reader threads pread(2)
+ * into a ring of pinned staging slots; each filled slot is copied H2D on
+ * `stream` while the next slots are read.  Returns once every copy is
+ * enqueued on `stream`: work queued after it on that stream sees the data.
+ * A read error or end of file before a range ends -> PYAS_EIO.  The offset
+ * and size arrays are host arrays. */
+int pyas_read_ranges(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offsets,
+                     const int64_t *sizes, void *dst, const int64_t *dst_offsets,
+                     int32_t threads, void *stream);
+/* Staging ring of pyas_read_ranges: n_slots x slot_bytes of pinned host
+ * memory (default 8 x 16 MiB), allocated on first use. */
+int pyas_ctx_set_ingest_slots(pyas_ctx *ctx, int32_t n_slots, int64_t slot_bytes);
 
 /* ---- measurement ---------------------------------------------------------- */
 /* When enabled, the main reduce kernel of each pyas_reduce_chunks call is

@@ -15,7 +15,7 @@ MAX_DIMS = 8
 ABI_VERSION = 1
 
 # pyas_status
-OK, EINVAL, ENOTSUP, EDEVICE, ENOMEM, EINDEX = range(6)
+OK, EINVAL, ENOTSUP, EDEVICE, ENOMEM, EINDEX, EIO = range(7)
 # pyas_dtype
 I8, U8, I16, U16, I32, U32, I64, U64, F32, F64 = range(10)
 # mask flags
@@ -97,6 +97,8 @@ SIGNATURES = {
     "pyas_combine_segments": [_vp, _i32, _vp, _vp, _vp, _i64, _u32, _vp, _vp],
     "pyas_unshuffle": [_vp, _vp, _vp, _i64, _i32, _vp],
     "pyas_inflate": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "pyas_read_ranges": [_vp, ctypes.c_int, _i64, _vp, _vp, _vp, _vp, _i32, _vp],
+    "pyas_ctx_set_ingest_slots": [_vp, _i32, _i64],
     "pyas_timing_enable": [_vp, _i32],
     "pyas_timing_read": [_vp, ctypes.POINTER(ctypes.c_float), _i32, ctypes.POINTER(_i32)],
 }
@@ -147,4 +149,6 @@ def check(rc: int, what: str = "") -> None:
         raise IndexError(text)
     if rc == ENOMEM:
         raise MemoryError(text)
+    if rc == EIO:
+        raise OSError(text)
     raise RuntimeError(text)

@@ -7,8 +7,10 @@ Mirrors ``activestorage/active.py``'s user API (``Active.method``,
 ``_get_selection`` + ``_from_storage`` (``active.py:439-635``):
 
 1. plan: orthogonal indexer -> touched chunks and per-chunk selections;
-2. ingest (host): positioned reads + zlib inflate on a thread pool
-   (``max_threads``, like ``active.py:557``), packed into one buffer, one H2D;
+2. ingest: for a file on disk, native pread threads (``max_threads``, like
+   ``active.py:557``) into pinned slots copied H2D as they fill
+   (``pyas_read_ranges``, row f2); zlib chunks are inflated on the device
+   (``pyas_inflate``, row f3); custom readers go through a Python pool;
 3. device: one fused reduce over every chunk (full-axis queries) or a
    partial-axis reduce plus a segmented combine (``pyas_combine_segments``),
    in both cases with per-chunk sums rounded to the variable dtype first,
@@ -26,6 +28,7 @@ from .batch import ReductionPlan
 from .device import DeviceBuffer, get_context
 from .dtypes import native, sum_dtype
 from .indexing import OrthogonalIndexer
+from .ingest import read_ranges
 from .inflate import InflateBatch, is_zlib, pack_streams
 from .masking import compile_missing
 from .storage import _decompress, _shuffle_sizes
@@ -137,42 +140,69 @@ class Active:
         nbytes = int(np.prod(ds.chunks)) * ds.dtype.itemsize
 
         device_inflate = self.device_inflate and is_zlib(compressor)
-
-        def fetch(coords):
-            off, size = ds.chunk_info(coords)
-            raw = ds.read(off, size)
-            return off, size, (raw if device_inflate else _decompress(raw, compressor))
-
-        with concurrent.futures.ThreadPoolExecutor(max_workers=self._max_threads) as ex:
-            blobs = list(ex.map(fetch, [c for c, _ in chunk_list]))
-        stride = -(-nbytes // _ALIGN) * _ALIGN
         ctx = get_context(self.device)
         st = ctx.thread_stream()
-        n = len(blobs)
-        if device_inflate:
-            # f3: one upload of the deflated bytes, one inflate launch into the
-            # chunk-major slots the reduce reads (raises like zlib.decompress)
-            host, soffs, ssizes = pack_streams([b for _, _, b in blobs])
-            self.data_read += int(ssizes.sum())
-            src = DeviceBuffer(ctx, host.nbytes)
-            ctx.h2d(src.ptr, host, st)
-            buf = DeviceBuffer(ctx, max(n, 1) * stride)
-            ib = InflateBatch(ctx, soffs, ssizes, np.arange(n, dtype=np.int64) * stride,
-                              np.full(n, nbytes, dtype=np.int64))
-            ib.launch(src.ptr, buf.ptr, st)
-            ib.check(st)
-            del src
-        else:
-            host = np.zeros(max(n, 1) * stride, dtype=np.uint8)
-            for i, (_, size, b) in enumerate(blobs):
-                a = np.frombuffer(memoryview(b), dtype=np.uint8)
-                if a.size != nbytes:
-                    raise ValueError(f"cannot reshape array of size {a.size // ds.dtype.itemsize} "
+        stride = -(-nbytes // _ALIGN) * _ALIGN
+        infos = [ds.chunk_info(c) for c, _ in chunk_list]
+        n = len(infos)
+        native_io = ds.reader is None and ds.filename is not None and (
+            device_inflate or compressor is None)
+        if native_io:
+            # f2: native pread ring -> pinned slots -> H2D, no Python per chunk
+            foff = np.array([o for o, _ in infos], dtype=np.int64)
+            fsize = np.array([z for _, z in infos], dtype=np.int64)
+            self.data_read += int(fsize.sum())
+            if device_inflate:
+                padded = -(-fsize // 16) * 16
+                soffs = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
+                src = DeviceBuffer(ctx, max(int(padded.sum()), 16))
+                read_ranges(ctx, ds.filename, foff, fsize, src.ptr, soffs, st, self._max_threads)
+                buf = DeviceBuffer(ctx, max(n, 1) * stride)
+                ib = InflateBatch(ctx, soffs, fsize, np.arange(n, dtype=np.int64) * stride,
+                                  np.full(n, nbytes, dtype=np.int64))
+                ib.launch(src.ptr, buf.ptr, st)
+                ib.check(st)
+                del src
+            else:
+                bad = np.nonzero(fsize != nbytes)[0]
+                if bad.size:   # storage.py:57-62 reshape of a wrongly sized chunk
+                    raise ValueError(f"cannot reshape array of size {int(fsize[bad[0]]) // ds.dtype.itemsize} "
                                      f"into shape {ds.chunks}")
-                host[i * stride: i * stride + nbytes] = a
-                self.data_read += size
-            buf = DeviceBuffer(ctx, host.nbytes)
-            ctx.h2d(buf.ptr, host, st)
+                buf = DeviceBuffer(ctx, max(n, 1) * stride)
+                read_ranges(ctx, ds.filename, foff, fsize, buf.ptr,
+                            np.arange(n, dtype=np.int64) * stride, st, self._max_threads)
+        else:
+            def fetch(info):
+                off, size = info
+                raw = ds.read(off, size)
+                return off, size, (raw if device_inflate else _decompress(raw, compressor))
+
+            with concurrent.futures.ThreadPoolExecutor(max_workers=self._max_threads) as ex:
+                blobs = list(ex.map(fetch, infos))
+            if device_inflate:
+                # f3: one upload of the deflated bytes, one inflate launch into the
+                # chunk-major slots the reduce reads (raises like zlib.decompress)
+                host, soffs, ssizes = pack_streams([b for _, _, b in blobs])
+                self.data_read += int(ssizes.sum())
+                src = DeviceBuffer(ctx, host.nbytes)
+                ctx.h2d(src.ptr, host, st)
+                buf = DeviceBuffer(ctx, max(n, 1) * stride)
+                ib = InflateBatch(ctx, soffs, ssizes, np.arange(n, dtype=np.int64) * stride,
+                                  np.full(n, nbytes, dtype=np.int64))
+                ib.launch(src.ptr, buf.ptr, st)
+                ib.check(st)
+                del src
+            else:
+                host = np.zeros(max(n, 1) * stride, dtype=np.uint8)
+                for i, (_, size, b) in enumerate(blobs):
+                    a = np.frombuffer(memoryview(b), dtype=np.uint8)
+                    if a.size != nbytes:
+                        raise ValueError(f"cannot reshape array of size {a.size // ds.dtype.itemsize} "
+                                         f"into shape {ds.chunks}")
+                    host[i * stride: i * stride + nbytes] = a
+                    self.data_read += size
+                buf = DeviceBuffer(ctx, host.nbytes)
+                ctx.h2d(buf.ptr, host, st)
         shuffles = _shuffle_sizes(filters)
         fused = 0
         if shuffles and shuffles[-1] == ds.dtype.itemsize:
@@ -181,10 +211,10 @@ class Active:
         for es in shuffles:   # non-itemsize shuffles: standalone device pass per chunk
             if es > 1:
                 tmp = DeviceBuffer(ctx, buf.nbytes)
-                for i in range(len(blobs)):
+                for i in range(n):
                     engine.unshuffle(ctx, buf.ptr + i * stride, tmp.ptr + i * stride, nbytes, es, st)
                 buf = tmp
-        offsets = np.arange(len(blobs), dtype=np.int64) * stride
+        offsets = np.arange(n, dtype=np.int64) * stride
         return ctx, st, buf, offsets, fused
 
     @staticmethod

@@ -69,6 +69,7 @@ struct pyas_ctx {
     int64_t tile_bytes = kDefaultTileBytes;
     int32_t inflate_wbits = 13;   // LDS history ring of pyas_inflate: 2^13 B per stream
     bool chained = true;          // k_finish folds the total itself (arrival counter)
+    pyas::Ingest *ingest = nullptr;   // pinned staging ring of pyas_read_ranges (lazy)
     std::mutex mu;
     std::unordered_map<void *, Scratch> scratch;  // keyed by stream
     // timing
@@ -247,6 +248,7 @@ int pyas_ctx_destroy(pyas_ctx *ctx) {
         if (kv.second.ptr) (void)hipFree(kv.second.ptr);
         if (kv.second.cnt) (void)hipFree(kv.second.cnt);
     }
+    if (ctx->ingest) pyas::ingest_destroy(ctx->ingest);
     for (auto e : ctx->ev0) (void)hipEventDestroy(e);
     for (auto e : ctx->ev1) (void)hipEventDestroy(e);
     delete ctx;
@@ -258,6 +260,29 @@ int pyas_ctx_set_tile_bytes(pyas_ctx *ctx, int64_t tile_bytes) {
     if (tile_bytes < 0) return fail(PYAS_EINVAL, "tile_bytes < 0");
     ctx->tile_bytes = tile_bytes == 0 ? kDefaultTileBytes : tile_bytes;
     return PYAS_OK;
+}
+
+static pyas::Ingest *ingest_of(pyas_ctx *ctx) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->ingest) ctx->ingest = pyas::ingest_create(ctx->device);
+    return ctx->ingest;
+}
+
+int pyas_ctx_set_ingest_slots(pyas_ctx *ctx, int32_t n_slots, int64_t slot_bytes) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    std::string msg;
+    const int rc = pyas::ingest_configure(ingest_of(ctx), n_slots, slot_bytes, msg);
+    return rc ? fail(rc, "%s", msg.c_str()) : PYAS_OK;
+}
+
+int pyas_read_ranges(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offsets,
+                     const int64_t *sizes, void *dst, const int64_t *dst_offsets, int32_t threads,
+                     void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    std::string msg;
+    const int rc = pyas::ingest_read(ingest_of(ctx), fd, n, file_offsets, sizes, (uint8_t *)dst,
+                                     dst_offsets, threads, (hipStream_t)stream, msg);
+    return rc ? fail(rc, "%s", msg.c_str()) : PYAS_OK;
 }
 
 int pyas_ctx_set_chained_combine(pyas_ctx *ctx, int32_t on) {

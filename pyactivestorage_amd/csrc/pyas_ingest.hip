@@ -1,0 +1,238 @@
+// pyas_ingest.hip — host ingest (row f2): positioned file reads straight into
+// device memory through a ring of pinned staging slots.
+//
+// The reference opens the file and reads each chunk on its own, once per
+// chunk, from a 30-thread pool (activestorage/storage.py:51-53 open +
+// read_block at :156-162; pool at activestorage/active.py:557-572), then
+// NumPy works on the host copy.  Here a query's chunk byte ranges are read by
+// `threads` workers with pread(2) into pinned slots; every filled slot is
+// copied H2D with hipMemcpyAsync on the caller's stream while the workers
+// fill the next slots, so disk/page-cache reads, PCIe and the device work
+// queued behind the copies overlap.  Slot reuse waits on the event recorded
+// after that slot's previous copy.
+#include <errno.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pyas_internal.hpp"
+
+namespace pyas {
+
+namespace {
+
+struct Piece {
+    int64_t file_off, size, dst_off, slot_off;
+};
+
+struct Group {   // what one staging slot carries: consecutive pieces
+    size_t first, count;
+    int64_t bytes;
+};
+
+}  // namespace
+
+struct Ingest {
+    int device = 0;
+    int32_t n_slots = 8;
+    int64_t slot_bytes = 16 << 20;
+    uint8_t *pinned = nullptr;   // n_slots * slot_bytes, hipHostMalloc
+    std::vector<hipEvent_t> done;
+    std::mutex call_mu;          // one pyas_read_ranges at a time per context
+
+    ~Ingest() { release(); }
+
+    void release() {
+        if (pinned) {
+            for (auto e : done) (void)hipEventSynchronize(e);
+            (void)hipHostFree(pinned);
+            pinned = nullptr;
+        }
+        for (auto e : done) (void)hipEventDestroy(e);
+        done.clear();
+    }
+
+    hipError_t ensure() {
+        if (pinned) return hipSuccess;
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) return e;
+        e = hipHostMalloc((void **)&pinned, (size_t)n_slots * (size_t)slot_bytes, hipHostMallocDefault);
+        if (e != hipSuccess) { pinned = nullptr; return e; }
+        done.resize(n_slots);
+        for (auto &ev : done) {
+            e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+};
+
+Ingest *ingest_create(int device) {
+    Ingest *g = new Ingest;
+    g->device = device;
+    return g;
+}
+
+void ingest_destroy(Ingest *g) { delete g; }
+
+int ingest_configure(Ingest *g, int32_t n_slots, int64_t slot_bytes, std::string &msg) {
+    std::lock_guard<std::mutex> lk(g->call_mu);
+    if (n_slots < 2 || n_slots > 256) { msg = "ingest slots must be in [2, 256]"; return PYAS_EINVAL; }
+    if (slot_bytes < (1 << 16) || slot_bytes > (int64_t(1) << 31)) {
+        msg = "ingest slot size must be in [64 KiB, 2 GiB]";
+        return PYAS_EINVAL;
+    }
+    g->release();
+    g->n_slots = n_slots;
+    g->slot_bytes = slot_bytes;
+    return PYAS_OK;
+}
+
+// pread the whole range (restarting on EINTR and short reads); returns 0 or errno,
+// ENODATA for end of file before `size` bytes.
+static int pread_full(int fd, uint8_t *dst, int64_t size, int64_t off) {
+    while (size > 0) {
+        const ssize_t r = ::pread(fd, dst, (size_t)std::min<int64_t>(size, int64_t(1) << 30), (off_t)off);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return errno;
+        }
+        if (r == 0) return ENODATA;
+        dst += r;
+        off += r;
+        size -= r;
+    }
+    return 0;
+}
+
+int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const int64_t *sizes,
+                uint8_t *dst, const int64_t *dst_offsets, int32_t threads, hipStream_t st,
+                std::string &msg) {
+    std::lock_guard<std::mutex> lk(g->call_mu);
+    if (n < 0 || (n > 0 && (!file_offsets || !sizes || !dst || !dst_offsets))) {
+        msg = "read_ranges: NULL array or negative count";
+        return PYAS_EINVAL;
+    }
+    if (fd < 0) { msg = "read_ranges: invalid file descriptor"; return PYAS_EINVAL; }
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    // ranges -> pieces of at most one slot -> groups (one slot each)
+    std::vector<Piece> pieces;
+    pieces.reserve((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        if (sizes[i] < 0 || file_offsets[i] < 0 || dst_offsets[i] < 0) {
+            msg = "read_ranges: negative offset or size at range " + std::to_string(i);
+            return PYAS_EINVAL;
+        }
+        for (int64_t p = 0; p < sizes[i]; p += g->slot_bytes)
+            pieces.push_back({file_offsets[i] + p, std::min(g->slot_bytes, sizes[i] - p), dst_offsets[i] + p, 0});
+    }
+    if (pieces.empty()) return PYAS_OK;
+    std::vector<Group> groups;
+    {
+        Group cur{0, 0, 0};
+        for (size_t k = 0; k < pieces.size(); ++k) {
+            if (cur.count && cur.bytes + pieces[k].size > g->slot_bytes) {
+                groups.push_back(cur);
+                cur = Group{k, 0, 0};
+            }
+            pieces[k].slot_off = cur.bytes;
+            cur.bytes += pieces[k].size;
+            cur.count++;
+        }
+        groups.push_back(cur);
+    }
+    hipError_t he = g->ensure();
+    if (he != hipSuccess) { msg = std::string("pinned staging: ") + hipGetErrorString(he); return PYAS_ENOMEM; }
+
+    const int K = g->n_slots;
+    const int64_t G = (int64_t)groups.size();
+    std::atomic<int64_t> next{0};
+    std::atomic<int> err_code{0};
+    std::mutex mu;
+    std::condition_variable cv;
+    // enq[s]: index of the last group whose copy from slot s is enqueued (-1 none)
+    std::vector<int64_t> enq(K, -1);
+    // a slot's first use in this call still waits for the previous call's copy
+    std::string err_msg;
+
+    auto worker = [&]() {
+        (void)hipSetDevice(g->device);
+        for (;;) {
+            const int64_t gi = next.fetch_add(1);
+            if (gi >= G || err_code.load()) break;
+            const int s = (int)(gi % K);
+            {   // the previous group of this slot must have enqueued its copy
+                std::unique_lock<std::mutex> l(mu);
+                cv.wait(l, [&] { return enq[s] == gi - K || (gi < K && enq[s] == -1) || err_code.load(); });
+                if (err_code.load()) break;
+            }
+            if (hipEventSynchronize(g->done[s]) != hipSuccess) {   // ... and that copy has landed
+                std::lock_guard<std::mutex> l(mu);
+                err_code = PYAS_EDEVICE;
+                err_msg = "staging event";
+                cv.notify_all();
+                break;
+            }
+            uint8_t *slot = g->pinned + (size_t)s * (size_t)g->slot_bytes;
+            const Group &gr = groups[(size_t)gi];
+            int rc = 0;
+            size_t bad = 0;
+            for (size_t k = gr.first; k < gr.first + gr.count && !rc; ++k) {
+                rc = pread_full(fd, slot + pieces[k].slot_off, pieces[k].size, pieces[k].file_off);
+                bad = k;
+            }
+            std::lock_guard<std::mutex> l(mu);
+            if (rc) {
+                err_code = PYAS_EIO;
+                err_msg = std::string(rc == ENODATA ? "short read (end of file)" : std::strerror(rc)) +
+                          " at file offset " + std::to_string(pieces[bad].file_off) + " (" +
+                          std::to_string(pieces[bad].size) + " bytes)";
+                cv.notify_all();
+                break;
+            }
+            // contiguous destination runs -> one copy each
+            hipError_t e = hipSuccess;
+            size_t k = gr.first;
+            while (k < gr.first + gr.count && e == hipSuccess) {
+                size_t j = k + 1;
+                int64_t len = pieces[k].size;
+                while (j < gr.first + gr.count && pieces[j].dst_off == pieces[k].dst_off + len &&
+                       pieces[j].slot_off == pieces[k].slot_off + len) {
+                    len += pieces[j].size;
+                    ++j;
+                }
+                e = hipMemcpyAsync(dst + pieces[k].dst_off, slot + pieces[k].slot_off, (size_t)len,
+                                   hipMemcpyHostToDevice, st);
+                k = j;
+            }
+            if (e == hipSuccess) e = hipEventRecord(g->done[s], st);
+            if (e != hipSuccess) {
+                err_code = PYAS_EDEVICE;
+                err_msg = std::string("H2D copy: ") + hipGetErrorString(e);
+            }
+            enq[s] = gi;
+            cv.notify_all();
+            if (e != hipSuccess) break;
+        }
+    };
+    const int nt = (int)std::min<int64_t>(threads, G);
+    std::vector<std::thread> pool;
+    pool.reserve((size_t)nt);
+    for (int t = 0; t < nt; ++t) pool.emplace_back(worker);
+    for (auto &t : pool) t.join();
+    if (err_code.load()) {
+        msg = err_msg;
+        return err_code.load();
+    }
+    return PYAS_OK;
+}
+
+}  // namespace pyas

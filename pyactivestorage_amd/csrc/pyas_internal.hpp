@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "pyas.h"
 #include "pyas_device.hpp"
 
@@ -105,6 +107,15 @@ hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int6
 hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st);
 hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
+// host ingest (pyas_ingest.hip): pread ring -> pinned slots -> H2D
+struct Ingest;
+Ingest *ingest_create(int device);
+void ingest_destroy(Ingest *g);
+int ingest_configure(Ingest *g, int32_t n_slots, int64_t slot_bytes, std::string &msg);
+int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const int64_t *sizes,
+                uint8_t *dst, const int64_t *dst_offsets, int32_t threads, hipStream_t st,
+                std::string &msg);
+
 hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es,
                             hipStream_t st);
 

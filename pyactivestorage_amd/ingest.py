@@ -1,0 +1,48 @@
+"""Host ingest (row f2): file byte ranges straight into device memory.
+
+The reference opens the file and reads every chunk separately
+(``activestorage/storage.py:51-53`` ``open`` + ``read_block`` at
+``:156-162``), once per chunk on a 30-thread pool (``active.py:557-572``).
+:func:`read_ranges` hands a whole query's ranges to ``pyas_read_ranges``
+(``include/pyas.h``): native reader threads ``pread`` into pinned staging
+slots, and each filled slot is copied H2D on the caller's stream while the
+next ones are read.  Opening the file stays in Python, so a missing file
+raises ``FileNotFoundError`` exactly where the reference's ``open`` does.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from . import _lib
+from .device import Context
+
+DEFAULT_THREADS = 16
+
+
+def read_ranges(ctx: Context, path: str, file_offsets, sizes, dst_ptr: int, dst_offsets,
+                stream=None, threads: int = DEFAULT_THREADS) -> int:
+    """Read ``file[file_offsets[i] : + sizes[i]]`` into ``dst_ptr + dst_offsets[i]``
+    (device) for every i.  Returns the bytes read.  The copies are enqueued
+    on ``stream``; work queued after them on that stream sees the data."""
+    foff = np.ascontiguousarray(file_offsets, dtype=np.int64)
+    size = np.ascontiguousarray(sizes, dtype=np.int64)
+    doff = np.ascontiguousarray(dst_offsets, dtype=np.int64)
+    if not (foff.shape == size.shape == doff.shape) or foff.ndim != 1:
+        raise ValueError("file_offsets, sizes and dst_offsets must be 1-D and of equal length")
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        _lib.check(ctx.lib.pyas_read_ranges(ctx.handle, fd, int(foff.size), foff.ctypes.data,
+                                            size.ctypes.data, dst_ptr, doff.ctypes.data,
+                                            int(threads), stream),
+                   f"pyas_read_ranges({path})")
+    finally:
+        os.close(fd)
+    return int(size.sum())
+
+
+def set_slots(ctx: Context, n_slots: int, slot_bytes: int) -> None:
+    """Resize the pinned staging ring (default 8 x 16 MiB)."""
+    _lib.check(ctx.lib.pyas_ctx_set_ingest_slots(ctx.handle, int(n_slots), int(slot_bytes)),
+               "pyas_ctx_set_ingest_slots")

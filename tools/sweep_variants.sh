@@ -10,7 +10,7 @@ for cfg in ${CONFIGS:-c3 c2 c4 c5}; do
       if [ $v = default ]; then lib=""; else lib=$PWD/pyactivestorage_amd/lib/variants/libpyas_$v.so; fi
       log=gpurun_out/sweep/${cfg}_${v}_${tile}.log
       PYAS_LIB=$lib timeout -k 10 240 python bench.py --config $cfg --steps ${STEPS:-10} --warmup 3 \
-          --cpu-chunks 0 --host-inclusive 0 --tile-bytes $tile > $log 2>&1 || exit 1
+          --cpu-chunks 0 --host-inclusive 0 --file-inclusive 0 --tile-bytes $tile > $log 2>&1 || exit 1
       python3 -c "import json;l=[x for x in open('$log') if x.startswith('{')][-1];d=json.loads(l);print('$cfg','$v','$tile',d['value'],d['ms_per_step'],d['roofline']['kernel_ms_avg'],d['roofline']['frac'])"
     done
   done
