@@ -375,7 +375,7 @@ def main():
         gbs, sec = file_inclusive(torch, ctx, data, cfg, dt, missing)
         fileinc = {"GBps": round(gbs, 2), "s_per_pass": round(sec, 4),
                    "path": "chunk-major file in page cache -> pyas_read_ranges (16 pread threads, "
-                           "8 x 16 MiB pinned slots, H2D as slots fill) -> fused reduce -> D2H 32 B"}
+                           "16 x 64 MiB pinned slots, H2D as slots fill) -> fused reduce -> D2H 32 B"}
 
     if rank == 0:
         line = {

@@ -269,7 +269,7 @@ int pyas_read_ranges(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offse
                      const int64_t *sizes, void *dst, const int64_t *dst_offsets,
                      int32_t threads, void *stream);
 /* Staging ring of pyas_read_ranges: n_slots x slot_bytes of pinned host
- * memory (default 8 x 16 MiB), allocated on first use. */
+ * memory (default 16 x 64 MiB; each slot is pinned on first use). */
 int pyas_ctx_set_ingest_slots(pyas_ctx *ctx, int32_t n_slots, int64_t slot_bytes);
 
 /* ---- measurement ---------------------------------------------------------- */

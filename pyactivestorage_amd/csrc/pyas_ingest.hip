@@ -39,36 +39,48 @@ struct Group {   // what one staging slot carries: consecutive pieces
 
 }  // namespace
 
+// Default ring: 16 x 64 MiB.  Measured on MI355X (tools/bench_ingest.py, 4 GiB
+// page-cache-hot file, 1 MiB chunks): what matters is the bytes in flight —
+// 256 MiB rings reach 25-36 GB/s, 512 MiB 48-52 GB/s, 1 GiB 51-55 GB/s (the
+// PCIe Gen5 x16 copy rate is ~56 GB/s).  Slots are pinned lazily, one at a
+// time, so a small query pins only the slots it uses.
 struct Ingest {
     int device = 0;
-    int32_t n_slots = 8;
-    int64_t slot_bytes = 16 << 20;
-    uint8_t *pinned = nullptr;   // n_slots * slot_bytes, hipHostMalloc
-    std::vector<hipEvent_t> done;
-    std::mutex call_mu;          // one pyas_read_ranges at a time per context
+    int32_t n_slots = 16;
+    int64_t slot_bytes = 64 << 20;
+    std::vector<uint8_t *> slot;     // hipHostMalloc'd on first use
+    std::vector<hipEvent_t> done;    // recorded after each slot's latest copy
+    std::mutex call_mu;              // one pyas_read_ranges at a time per context
 
     ~Ingest() { release(); }
 
     void release() {
-        if (pinned) {
-            for (auto e : done) (void)hipEventSynchronize(e);
-            (void)hipHostFree(pinned);
-            pinned = nullptr;
+        for (size_t s = 0; s < slot.size(); ++s) {
+            if (slot[s]) {
+                (void)hipEventSynchronize(done[s]);
+                (void)hipHostFree(slot[s]);
+            }
         }
         for (auto e : done) (void)hipEventDestroy(e);
+        slot.clear();
         done.clear();
     }
 
-    hipError_t ensure() {
-        if (pinned) return hipSuccess;
+    hipError_t ensure(int used) {
         hipError_t e = hipSetDevice(device);
         if (e != hipSuccess) return e;
-        e = hipHostMalloc((void **)&pinned, (size_t)n_slots * (size_t)slot_bytes, hipHostMallocDefault);
-        if (e != hipSuccess) { pinned = nullptr; return e; }
-        done.resize(n_slots);
-        for (auto &ev : done) {
-            e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-            if (e != hipSuccess) return e;
+        if (done.empty()) {
+            slot.assign((size_t)n_slots, nullptr);
+            done.resize((size_t)n_slots);
+            for (auto &ev : done) {
+                e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+                if (e != hipSuccess) return e;
+            }
+        }
+        for (int s = 0; s < used; ++s) {
+            if (slot[s]) continue;
+            e = hipHostMalloc((void **)&slot[s], (size_t)slot_bytes, hipHostMallocDefault);
+            if (e != hipSuccess) { slot[s] = nullptr; return e; }
         }
         return hipSuccess;
     }
@@ -149,11 +161,11 @@ int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const
         }
         groups.push_back(cur);
     }
-    hipError_t he = g->ensure();
-    if (he != hipSuccess) { msg = std::string("pinned staging: ") + hipGetErrorString(he); return PYAS_ENOMEM; }
-
     const int K = g->n_slots;
     const int64_t G = (int64_t)groups.size();
+    hipError_t he = g->ensure((int)std::min<int64_t>(K, G));
+    if (he != hipSuccess) { msg = std::string("pinned staging: ") + hipGetErrorString(he); return PYAS_ENOMEM; }
+
     std::atomic<int64_t> next{0};
     std::atomic<int> err_code{0};
     std::mutex mu;
@@ -181,7 +193,7 @@ int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const
                 cv.notify_all();
                 break;
             }
-            uint8_t *slot = g->pinned + (size_t)s * (size_t)g->slot_bytes;
+            uint8_t *slot = g->slot[(size_t)s];
             const Group &gr = groups[(size_t)gi];
             int rc = 0;
             size_t bad = 0;

@@ -43,6 +43,6 @@ def read_ranges(ctx: Context, path: str, file_offsets, sizes, dst_ptr: int, dst_
 
 
 def set_slots(ctx: Context, n_slots: int, slot_bytes: int) -> None:
-    """Resize the pinned staging ring (default 8 x 16 MiB)."""
+    """Resize the pinned staging ring (default 16 x 64 MiB)."""
     _lib.check(ctx.lib.pyas_ctx_set_ingest_slots(ctx.handle, int(n_slots), int(slot_bytes)),
                "pyas_ctx_set_ingest_slots")

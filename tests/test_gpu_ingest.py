@@ -54,7 +54,7 @@ def test_active_file_equals_reader(gpu, key, tmp_path):
             assert a.data_read == b.data_read
 
 
-@pytest.mark.parametrize("slots,slot_bytes", [(8, 16 << 20), (2, 1 << 16), (3, 100_000)])
+@pytest.mark.parametrize("slots,slot_bytes", [(16, 64 << 20), (2, 1 << 16), (3, 100_000)])
 def test_read_ranges_roundtrip(gpu, tmp_path, slots, slot_bytes):
     """Random ranges (some larger than a slot, some empty) land byte-exact."""
     rng = np.random.default_rng(slots)
@@ -80,7 +80,7 @@ def test_read_ranges_roundtrip(gpu, tmp_path, slots, slot_bytes):
                 np.testing.assert_array_equal(host[doff[i]: doff[i] + sizes[i]],
                                               blob[foff[i]: foff[i] + sizes[i]])
     finally:
-        ingest.set_slots(gpu, 8, 16 << 20)
+        ingest.set_slots(gpu, 16, 64 << 20)
 
 
 def test_read_ranges_errors(gpu, tmp_path):
