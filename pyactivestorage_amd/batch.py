@@ -59,8 +59,10 @@ class ReductionPlan:
                 raise ValueError("one selection per chunk is required")
             table, pool = selection.pack(selections, len(self.chunk_shape))
             _check_table(table, self.chunk_shape, pool)
-            sel_ptr = self._upload(table, st).ptr
-            pool_ptr = self._upload(pool, st).ptr
+            if not _all_full(table, self.chunk_shape):
+                # (every chunk fully selected: no table, the kernels' dense paths)
+                sel_ptr = self._upload(table, st).ptr
+                pool_ptr = self._upload(pool, st).ptr
             shapes = {s.shape for s in selections}
             if (self.cm.tables[0] is not None or self.cm.tables[1] is not None) and len(shapes) > 1:
                 raise NotImplementedError("vector fill/missing values need equal selection shapes")
@@ -122,6 +124,17 @@ class ReductionPlan:
             self.ctx.d2h(host, self.chunk_partials.ptr, stream)
         self.ctx.synchronize(stream)
         return host
+
+
+def _all_full(table, chunk_shape) -> bool:
+    """True when every chunk's selection is its whole box in C order
+    (start 0, step 1, count = extent), i.e. the table can be dropped."""
+    nd = len(chunk_shape)
+    if table.shape[0] == 0:
+        return False
+    t = table[:, :nd, :]
+    return bool((t[:, :, 0] == 0).all() and (t[:, :, 1] == 1).all()
+                and (t[:, :, 2] == np.asarray(chunk_shape, dtype=np.int32)).all())
 
 
 def _check_table(table, chunk_shape, pool):

@@ -426,6 +426,59 @@ int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *
     return PYAS_OK;
 }
 
+// Dense partial-axis geometry: merge the chunk dims into runs of reduced /
+// kept dims and fit them to (RO, KO, RI, KI); pick the column layout (a
+// kept inner run of whole 16-B vectors) or the row layout (a reduced inner
+// run of whole 16-B vectors, >= 4 lanes per output).  mode 0 = not dense.
+static void dense_geometry(pyas::AxesDense &d, const pyas_batch *b, uint32_t axes_mask, int es,
+                           bool excluded) {
+    std::memset(&d, 0, sizeof(d));
+    if (excluded || axes_mask == 0) return;
+    int64_t ext[PYAS_MAX_DIMS];
+    int kind[PYAS_MAX_DIMS], nr = 0;
+    for (int dd = 0; dd < b->ndim; ++dd) {
+        const int k = (axes_mask >> dd) & 1u;
+        if (nr && kind[nr - 1] == k) ext[nr - 1] *= b->chunk_shape[dd];
+        else { kind[nr] = k; ext[nr++] = b->chunk_shape[dd]; }
+    }
+    int64_t v[4] = {1, 1, 1, 1};   // slots RO (reduced), KO (kept), RI (reduced), KI (kept)
+    int slot = 3;
+    for (int q = nr - 1; q >= 0; --q) {
+        while (slot >= 0 && (slot % 2 == 1 ? 0 : 1) != kind[q]) --slot;
+        if (slot < 0) return;      // more than 4 alternating runs
+        v[slot--] = ext[q];
+    }
+    d.RO = v[0]; d.KO = v[1]; d.RI = v[2]; d.KI = v[3];
+    const int64_t nv = 16 / es, chunk_bytes = d.RO * d.KO * d.RI * d.KI * es;
+    auto pow2_ceil = [](int64_t x) { int64_t p = 1; while (p < x) p *= 2; return p; };
+    if (d.KI > 1) {
+        if ((d.KI * es) % 16) return;
+        const int64_t items = d.KO * (d.KI / nv), rows = d.RO * d.RI;
+        int64_t it = pow2_ceil(items < pyas::kBlock ? items : pyas::kBlock);
+        int64_t sp = pyas::kBlock / it;
+        while (sp > 1 && rows < sp * 4) sp >>= 1;   // >= 4 rows per split
+        d.mode = 1;
+        d.it = (int32_t)it;
+        d.split = (int32_t)sp;
+        d.bpc = (items + it - 1) / it;
+    } else {
+        if ((d.RI * es) % 16) return;
+        const int64_t V = d.RI / nv;
+        int64_t g = 1;
+        while (g < pyas::kWave && V % (g * 2) == 0) g *= 2;
+        if (g < 4) return;         // too few lanes per output to coalesce
+        const int64_t per_lane = d.RO * (V / g);
+        const int64_t uo = per_lane == 1 ? 4 : 1;
+        d.mode = uo == 4 ? 3 : 2;
+        d.group = (int32_t)g;
+        const int64_t per_pass = (pyas::kBlock / pyas::kWave) * (pyas::kWave / g) * uo;
+        int64_t bpc = (d.KO + per_pass - 1) / per_pass;
+        const int64_t by_bytes = chunk_bytes >> 16;   // >= ~64 KiB per workgroup
+        if (bpc > by_bytes) bpc = by_bytes;
+        d.bpc = bpc < 1 ? 1 : bpc;
+    }
+}
+
 int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
                      uint32_t axes_mask, const int64_t *out_offsets, pyas_partial *out,
                      void *stream) {
@@ -483,9 +536,19 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *ma
     x.out = out;
     x.shuf = shuf;
     x.bswap = bsw;
-    const int64_t grid = batch->n_chunks * bpc;
-    if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
-    PYAS_HIP(pyas::launch_reduce_axes(batch->dtype, x, grid, (hipStream_t)stream));
+    dense_geometry(x.d, batch, axes_mask, es, shuf || x.r.tab.on[0] || x.r.tab.on[1]);
+    // Fully selected chunks go to k_axes_dense, the rest to k_reduce_axes
+    // (each kernel skips the other's chunks); sel == NULL means all full.
+    if (x.d.mode) {
+        const int64_t g = batch->n_chunks * x.d.bpc;
+        if (g >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
+        PYAS_HIP(pyas::launch_axes_dense(batch->dtype, x, masked, g, (hipStream_t)stream));
+    }
+    if (!x.d.mode || batch->sel) {
+        const int64_t grid = batch->n_chunks * bpc;
+        if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
+        PYAS_HIP(pyas::launch_reduce_axes(batch->dtype, x, grid, (hipStream_t)stream));
+    }
     return PYAS_OK;
 }
 

@@ -45,8 +45,19 @@ struct FinishArgs {
 
 constexpr int kAxesLds = 8192;   // reduced-index offsets kept in LDS (int32, 32 KiB)
 
+// Dense partial-axis geometry (k_axes_dense): the chunk dims merged into
+// (RO, KO, RI, KI) = (reduced outer, kept outer, reduced inner, kept inner).
+struct AxesDense {
+    int32_t mode;                     // 0 off, 1 column, 2 row, 3 row with 4 outputs per lane
+    int32_t it, split;                // column: items per pass (power of 2), row splits
+    int32_t group;                    // row: lanes per output (power of 2)
+    int64_t RO, KO, RI, KI;
+    int64_t bpc;                      // workgroups per chunk of the dense launch
+};
+
 struct AxesArgs {
     ReduceArgs r;
+    AxesDense d;
     uint32_t axes;
     int64_t bpc;                      // workgroups per chunk
     const int64_t *out_offsets;
@@ -93,6 +104,8 @@ hipError_t launch_combine_segments_t(const pyas_partial *in, const int64_t *inde
 template <typename T>
 hipError_t launch_axes_t(const AxesArgs &a, int64_t grid, hipStream_t st);
 template <typename T>
+hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
+template <typename T>
 hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st);
 
 // dtype dispatch (pyas_kernels.hip)
@@ -105,6 +118,7 @@ hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int6
                                    const int64_t *seg, int64_t n_seg, uint32_t flags,
                                    pyas_partial *out, hipStream_t st);
 hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st);
+hipError_t launch_axes_dense(int dtype, const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
 hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
 // host ingest (pyas_ingest.hip): pread ring -> pinned slots -> H2D

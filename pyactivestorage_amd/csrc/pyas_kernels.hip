@@ -67,6 +67,11 @@ hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStr
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_axes_dense(int dtype, const AxesArgs &a, bool masked, int64_t grid, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_axes_dense_t<T>(a, masked, grid, st));
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st) {
     PYAS_DISPATCH_T(dtype, return launch_select_t<T>(a, grid, st));
     return hipErrorInvalidValue;

@@ -834,17 +834,281 @@ __device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_
     }
 }
 
+// ---------------------------------------------------------------------------
+// dense partial-axis reduction: a fully selected, unshuffled chunk without
+// index tables.  The host merges the chunk dims into the canonical form
+// (RO, KO, RI, KI) = (reduced outer, kept outer, reduced inner, kept inner):
+// element (ro, ko, ri, ki) at ((ro*KO + ko)*RI + ri)*KI + ki, output
+// ko*KI + ki, reduced row ro*RI + ri.  No offset maps, no radix counters:
+// addresses advance by constant strides.
+//  column (KI*ES % 16 == 0): a lane owns one 16-B vector of N outputs, the
+//    reduced rows are split over S lane sets (folded in split order);
+//    a wave reads whole 16-B runs of the same row (1 KiB when KI >= 64 N);
+//  row (KI == 1): G lanes per output read consecutive 16-B vectors of its
+//    runs (a wave reads 64/G adjacent runs = 1 KiB), DPP butterfly per group;
+//    with one vector per lane per output each lane keeps 4 outputs in flight.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool chunk_is_full(const Sel &s, const int64_t *shape, int ndim) {
+    bool full = true;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+        if (d < ndim) full = full && s.start[d] == 0 && s.step[d] == 1 && s.cnt[d] == shape[d];
+    return full;
+}
+
+// 16 bytes at any element-aligned address (AL: 16-B aligned -> one load)
+template <bool AL>
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+    if constexpr (AL) {
+        return ldg16(reinterpret_cast<const uint4 *>(p));
+    } else {
+        uint4 r;
+        __builtin_memcpy(&r, p, 16);
+        return r;
+    }
+}
+
+template <int CTRL, typename V>
+__device__ __forceinline__ V dpp_mov(V v) {
+    if constexpr (sizeof(V) <= 4) {
+        int w = 0;
+        __builtin_memcpy(&w, &v, sizeof(V));
+        w = __builtin_amdgcn_update_dpp(0, w, CTRL, 0xf, 0xf, false);
+        V r;
+        __builtin_memcpy(&r, &w, sizeof(V));
+        return r;
+    } else {
+        int w[2];
+        __builtin_memcpy(w, &v, 8);
+        w[0] = __builtin_amdgcn_update_dpp(0, w[0], CTRL, 0xf, 0xf, false);
+        w[1] = __builtin_amdgcn_update_dpp(0, w[1], CTRL, 0xf, 0xf, false);
+        V r;
+        __builtin_memcpy(&r, w, 8);
+        return r;
+    }
+}
+
+// Butterfly over aligned groups of G lanes (G power of two <= 64, wave-
+// uniform): quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror
+// (each pairs uniform halves of the group so far), then xor 16 / 32.
+// Every lane of a group ends with the group's combined partial.
+template <typename T>
+__device__ __forceinline__ void group_reduce(TileAcc<T> &a, int G, uint32_t &cnt, uint32_t &nan) {
+    cnt = a.count;
+    nan = a.nan ? 1u : 0u;
+#define PYAS_DPP_STEP(CTRL)                                   \
+    do {                                                      \
+        a.sum += dpp_mov<CTRL>(a.sum);                        \
+        cnt += dpp_mov<CTRL>(cnt);                            \
+        a.mn = tmin(a.mn, dpp_mov<CTRL>(a.mn));               \
+        a.mx = tmax(a.mx, dpp_mov<CTRL>(a.mx));               \
+        nan |= dpp_mov<CTRL>(nan);                            \
+    } while (0)
+    if (G >= 2) PYAS_DPP_STEP(0xB1);
+    if (G >= 4) PYAS_DPP_STEP(0x4E);
+    if (G >= 8) PYAS_DPP_STEP(0x141);
+    if (G >= 16) PYAS_DPP_STEP(0x140);
+#undef PYAS_DPP_STEP
+    for (int m = 16; m < G; m <<= 1) {
+        a.sum += shfl_xor(a.sum, m);
+        cnt += shfl_xor(cnt, m);
+        a.mn = tmin(a.mn, shfl_xor(a.mn, m));
+        a.mx = tmax(a.mx, shfl_xor(a.mx, m));
+        nan |= shfl_xor(nan, m);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_group(const TileAcc<T> &a, uint32_t cnt, uint32_t nan,
+                                            pyas_partial *out) {
+    pyas_partial p;
+    TT<T>::put_acc(p.sum, a.sum);
+    p.count = (int64_t)cnt;
+    T mn = a.mn, mx = a.mx;
+    if constexpr (TT<T>::kind == 0) {
+        if (nan) { mn = (T)__builtin_nan(""); mx = mn; }
+    }
+    TT<T>::put(p.min, mn);
+    TT<T>::put(p.max, mx);
+    *out = p;
+}
+
+template <typename T, bool BSWAP, bool MASKED, bool AL>
+__device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
+                          const MaskT<T> &mk) {
+    constexpr int ES = sizeof(T), N = 16 / ES;
+    const AxesDense &d = a.d;
+    const int IT = d.it, S = d.split;
+    const int il = threadIdx.x & (IT - 1), sp = threadIdx.x / IT;
+    const int64_t KIV = d.KI / N, items = d.KO * KIV, R = d.RO * d.RI;
+    const int64_t sRO = d.KO * d.RI * d.KI;                    // elements per ro step
+    const int64_t dq = S / d.RI, dr = S - dq * d.RI;            // row step S = dq*RI + dr
+    const int64_t step_off = (dq * sRO + dr * d.KI) * ES;       // bytes
+    const int64_t wrap_off = (sRO - d.RI * d.KI) * ES;          // ri wrapped past RI
+    pyas_partial *out = a.out + a.out_offsets[c];
+    for (int64_t i0 = j * IT; i0 < items; i0 += d.bpc * IT) {   // block-uniform
+        const int64_t i = i0 + il;
+        TileAcc<T> acc[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k].init();
+        if (i < items && sp < S && sp < R) {
+            const int64_t ko = i / KIV, v = i - ko * KIV;
+            int64_t ro = sp / d.RI, ri = sp - ro * d.RI;
+            const uint8_t *p = base + ((ro * d.KO + ko) * d.RI * d.KI + ri * d.KI + v * N) * ES;
+            const int64_t nt = (R - sp + S - 1) / S;
+            auto next = [&]() {
+                p += step_off;
+                ri += dr;
+                if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
+            };
+            constexpr int U = 8;
+            int64_t t = 0;
+            for (; t + U <= nt; t += U) {
+                uint4 w[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) { w[u] = ld16<AL>(p); next(); }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    T x[N];
+                    unpack16<T, BSWAP>(w[u], x);
+#pragma unroll
+                    for (int k = 0; k < N; ++k) acc[k].add_one(x[k], MASKED && mk.masked(x[k]));
+                }
+            }
+            for (; t < nt; ++t) {
+                T x[N];
+                unpack16<T, BSWAP>(ld16<AL>(p), x);
+                next();
+#pragma unroll
+                for (int k = 0; k < N; ++k) acc[k].add_one(x[k], MASKED && mk.masked(x[k]));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            if (S > 1) fold_splits(acc[k], S, IT, il, sp);
+            if (sp == 0 && i < items) tile_store_lane(acc[k], out + i * N + k);
+        }
+    }
+}
+
+template <typename T, bool BSWAP, bool MASKED, bool AL, int UO>
+__device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
+                          const MaskT<T> &mk) {
+    constexpr int ES = sizeof(T), N = 16 / ES;
+    const AxesDense &d = a.d;
+    const int G = d.group, P = kWave / G;
+    const int lane = threadIdx.x & (kWave - 1), gl = lane & (G - 1), pg = lane / G;
+    const int64_t VG = d.RI / N / G;                 // vectors per lane per run
+    const int64_t Q = d.RO * VG;                     // vectors per lane per output
+    const int64_t wave = j * (kBlock / kWave) + threadIdx.x / kWave;
+    const int64_t nwaves = d.bpc * (kBlock / kWave);
+    const int64_t vstep = (int64_t)G * N * ES;                   // bytes
+    const int64_t wrap = (d.KO - 1) * d.RI * ES;                 // next run of the output
+    pyas_partial *out = a.out + a.out_offsets[c];
+    for (int64_t o0 = wave * P * UO; o0 < d.KO; o0 += nwaves * P * UO) {   // wave-uniform
+        TileAcc<T> acc[UO];
+#pragma unroll
+        for (int u = 0; u < UO; ++u) acc[u].init();
+        if constexpr (UO > 1) {
+            // one vector per lane per output (RO == 1, RI == G*N): UO outputs in flight
+            uint4 w[UO];
+#pragma unroll
+            for (int u = 0; u < UO; ++u) {
+                const int64_t o = o0 + u * P + pg;
+                if (o < d.KO) w[u] = ld16<AL>(base + (o * d.RI + gl * N) * ES);
+            }
+#pragma unroll
+            for (int u = 0; u < UO; ++u) {
+                const int64_t o = o0 + u * P + pg;
+                if (o < d.KO) {
+                    T x[N];
+                    unpack16<T, BSWAP>(w[u], x);
+                    acc[u].template add_n<N, MASKED, false>(x, mk);
+                    if constexpr (!MASKED) acc[u].count += N;
+                }
+            }
+        } else {
+            const int64_t o = o0 + pg;
+            if (o < d.KO) {
+                const uint8_t *p = base + (o * d.RI + gl * N) * ES;
+                int64_t vc = 0;
+                auto next = [&]() {
+                    p += vstep;
+                    if (++vc == VG) { vc = 0; p += wrap; }
+                };
+                constexpr int U = 4;
+                int64_t t = 0;
+                for (; t + U <= Q; t += U) {
+                    uint4 w[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) { w[u] = ld16<AL>(p); next(); }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        T x[N];
+                        unpack16<T, BSWAP>(w[u], x);
+                        acc[0].template add_n<N, MASKED, false>(x, mk);
+                    }
+                }
+                for (; t < Q; ++t) {
+                    T x[N];
+                    unpack16<T, BSWAP>(ld16<AL>(p), x);
+                    next();
+                    acc[0].template add_n<N, MASKED, false>(x, mk);
+                }
+                if constexpr (!MASKED) acc[0].count += (uint32_t)(Q * N);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UO; ++u) {
+            uint32_t cnt, nan;
+            group_reduce(acc[u], G, cnt, nan);
+            const int64_t o = o0 + u * P + pg;
+            if (gl == 0 && o < d.KO) store_group(acc[u], cnt, nan, out + o);
+        }
+    }
+}
+
+// Which kernel owns chunk c: the dense one when the chunk is fully selected.
+__device__ __forceinline__ bool dense_owns(const AxesArgs &a, const Sel &s) {
+    return a.d.mode != 0 && chunk_is_full(s, a.r.shape, a.r.ndim);
+}
+
+template <typename T, bool BSWAP, bool MASKED, int MODE>
+__global__ __launch_bounds__(kBlock) void k_axes_dense(AxesArgs a) {
+    const int64_t c = blockIdx.x / a.d.bpc;
+    const int64_t j = blockIdx.x - c * a.d.bpc;
+    const ReduceArgs &r = a.r;
+    Sel s;
+    load_sel(s, r.sel, c, r.ndim, r.shape);
+    if (!dense_owns(a, s)) return;   // the generic kernel takes this chunk
+    const uint8_t *base = r.data + r.offsets[c];
+    MaskT<T> mk;
+    mk.init(r.mask);
+    const bool al = ((uintptr_t)base & 15) == 0;
+    if constexpr (MODE == 1) {
+        if (al) dense_col<T, BSWAP, MASKED, true>(a, c, j, base, mk);
+        else dense_col<T, BSWAP, MASKED, false>(a, c, j, base, mk);
+    } else if constexpr (MODE == 2) {
+        if (al) dense_row<T, BSWAP, MASKED, true, 1>(a, c, j, base, mk);
+        else dense_row<T, BSWAP, MASKED, false, 1>(a, c, j, base, mk);
+    } else {
+        if (al) dense_row<T, BSWAP, MASKED, true, 4>(a, c, j, base, mk);
+        else dense_row<T, BSWAP, MASKED, false, 4>(a, c, j, base, mk);
+    }
+}
+
 template <typename T, bool SHUF, bool BSWAP>
 __global__ __launch_bounds__(kBlock) void k_reduce_axes(AxesArgs a) {
     __shared__ int32_t roff[kAxesLds];
     const int64_t c = blockIdx.x / a.bpc;
     const int64_t j = blockIdx.x - c * a.bpc;
     const ReduceArgs &r = a.r;
+    Sel s;
+    load_sel(s, r.sel, c, r.ndim, r.shape);
+    if (dense_owns(a, s)) return;    // k_axes_dense took this chunk
     const uint8_t *base = r.data + r.offsets[c];
     MaskT<T> mk;
     mk.init(r.mask);
-    Sel s;
-    load_sel(s, r.sel, c, r.ndim, r.shape);
     const uint32_t all = (1u << r.ndim) - 1u;
     const uint32_t red = a.axes & all, keep = all & ~red;
     int64_t n_out = 1, n_red = 1;
@@ -947,6 +1211,27 @@ hipError_t launch_combine_segments_t(const pyas_partial *in, const int64_t *inde
     return hipGetLastError();
 }
 
+template <typename T, int MODE>
+static void launch_dense_m(const AxesArgs &a, bool masked, dim3 g, hipStream_t st) {
+    const dim3 blk(kBlock);
+    if (a.bswap && sizeof(T) > 1) {
+        if (masked) hipLaunchKernelGGL((k_axes_dense<T, true, true, MODE>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_dense<T, true, false, MODE>), g, blk, 0, st, a);
+    } else {
+        if (masked) hipLaunchKernelGGL((k_axes_dense<T, false, true, MODE>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_dense<T, false, false, MODE>), g, blk, 0, st, a);
+    }
+}
+
+template <typename T>
+hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st) {
+    const dim3 g((unsigned)grid);
+    if (a.d.mode == 1) launch_dense_m<T, 1>(a, masked, g, st);
+    else if (a.d.mode == 2) launch_dense_m<T, 2>(a, masked, g, st);
+    else launch_dense_m<T, 3>(a, masked, g, st);
+    return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_axes_t(const AxesArgs &a, int64_t grid, hipStream_t st) {
     const dim3 g((unsigned)grid), blk(kBlock);
@@ -978,6 +1263,7 @@ hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st) {
                                                      const int64_t *, int64_t, uint32_t,     \
                                                      pyas_partial *, hipStream_t);           \
     template hipError_t launch_axes_t<T>(const AxesArgs &, int64_t, hipStream_t);             \
+    template hipError_t launch_axes_dense_t<T>(const AxesArgs &, bool, int64_t, hipStream_t); \
     template hipError_t launch_select_t<T>(const SelectArgs &, int64_t, hipStream_t);
 
 }  // namespace pyas
