@@ -9,6 +9,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -464,8 +465,14 @@ static void dense_geometry(pyas::AxesDense &d, const pyas_batch *b, uint32_t axe
     } else {
         if ((d.RI * es) % 16) return;
         const int64_t V = d.RI / nv;
+        // G lanes per output: the largest power of two dividing V (<= 64)
+        // that still leaves each lane >= row_vecs vectors per run
+        static const int64_t row_vecs = [] {
+            const char *e = getenv("PYAS_ROW_VECS");
+            return e ? (int64_t)atoi(e) : (int64_t)2;   // measured: 2 beats 1 and 4 on (2,)
+        }();
         int64_t g = 1;
-        while (g < pyas::kWave && V % (g * 2) == 0) g *= 2;
+        while (g < pyas::kWave && V % (g * 2) == 0 && V / (g * 2) >= row_vecs) g *= 2;
         if (g < 4) return;         // too few lanes per output to coalesce
         const int64_t per_lane = d.RO * (V / g);
         const int64_t uo = per_lane == 1 ? 4 : 1;

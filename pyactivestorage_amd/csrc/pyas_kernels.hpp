@@ -933,9 +933,21 @@ __device__ __forceinline__ void store_group(const TileAcc<T> &a, uint32_t cnt, u
     *out = p;
 }
 
+#ifndef PYAS_COL_U
+#define PYAS_COL_U 8      // 16-B loads in flight per lane (column layout)
+#endif
+#ifndef PYAS_DENSE_WAVES
+#define PYAS_DENSE_WAVES 0
+#endif
+#if PYAS_DENSE_WAVES
+#define PYAS_DENSE_ATTR __attribute__((amdgpu_waves_per_eu(PYAS_DENSE_WAVES, 8)))
+#else
+#define PYAS_DENSE_ATTR
+#endif
+
 template <typename T, bool BSWAP, bool MASKED, bool AL>
 __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
-                          const MaskT<T> &mk) {
+                          const MaskT<T> &mk, uint4 *stage) {
     constexpr int ES = sizeof(T), N = 16 / ES;
     const AxesDense &d = a.d;
     const int IT = d.it, S = d.split;
@@ -961,7 +973,7 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
                 ri += dr;
                 if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
             };
-            constexpr int U = 8;
+            constexpr int U = PYAS_COL_U;
             int64_t t = 0;
             for (; t + U <= nt; t += U) {
                 uint4 w[U];
@@ -983,10 +995,38 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
                 for (int k = 0; k < N; ++k) acc[k].add_one(x[k], MASKED && mk.masked(x[k]));
             }
         }
+        if constexpr (N <= 4) {
+            // Stage the pass's IT*N partials (<= 32 KiB) in LDS, then write
+            // them as consecutive 16-B stores (a lane's own N partials are
+            // 32*N bytes apart from its neighbours').
 #pragma unroll
-        for (int k = 0; k < N; ++k) {
-            if (S > 1) fold_splits(acc[k], S, IT, il, sp);
-            if (sp == 0 && i < items) tile_store_lane(acc[k], out + i * N + k);
+            for (int k = 0; k < N; ++k) {
+                if (S > 1) fold_splits(acc[k], S, IT, il, sp);
+                if (sp == 0) {
+                    pyas_partial pp;
+                    tile_store_lane(acc[k], &pp);
+                    uint4 h[2];
+                    __builtin_memcpy(h, &pp, 32);
+                    stage[(il * N + k) * 2] = h[0];
+                    stage[(il * N + k) * 2 + 1] = h[1];
+                }
+            }
+            __syncthreads();
+            const int64_t n_valid = ((items - i0 < IT) ? items - i0 : IT) * N * 2;   // uint4s
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 *dst = reinterpret_cast<u32x4 *>(out + i0 * N);
+            for (int64_t q = threadIdx.x; q < n_valid; q += kBlock) {
+                const uint4 h = stage[q];
+                u32x4 v = {h.x, h.y, h.z, h.w};
+                __builtin_nontemporal_store(v, dst + q);
+            }
+            __syncthreads();
+        } else {
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                if (S > 1) fold_splits(acc[k], S, IT, il, sp);
+                if (sp == 0 && i < items) tile_store_lane(acc[k], out + i * N + k);
+            }
         }
     }
 }
@@ -1074,7 +1114,7 @@ __device__ __forceinline__ bool dense_owns(const AxesArgs &a, const Sel &s) {
 }
 
 template <typename T, bool BSWAP, bool MASKED, int MODE>
-__global__ __launch_bounds__(kBlock) void k_axes_dense(AxesArgs a) {
+__global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs a) {
     const int64_t c = blockIdx.x / a.d.bpc;
     const int64_t j = blockIdx.x - c * a.d.bpc;
     const ReduceArgs &r = a.r;
@@ -1086,8 +1126,10 @@ __global__ __launch_bounds__(kBlock) void k_axes_dense(AxesArgs a) {
     mk.init(r.mask);
     const bool al = ((uintptr_t)base & 15) == 0;
     if constexpr (MODE == 1) {
-        if (al) dense_col<T, BSWAP, MASKED, true>(a, c, j, base, mk);
-        else dense_col<T, BSWAP, MASKED, false>(a, c, j, base, mk);
+        // staging for coalesced partial stores (dense_col, N <= 4): 32 KiB
+        __shared__ uint4 stage[sizeof(T) >= 4 ? kBlock * 4 * 2 : 1];
+        if (al) dense_col<T, BSWAP, MASKED, true>(a, c, j, base, mk, stage);
+        else dense_col<T, BSWAP, MASKED, false>(a, c, j, base, mk, stage);
     } else if constexpr (MODE == 2) {
         if (al) dense_row<T, BSWAP, MASKED, true, 1>(a, c, j, base, mk);
         else dense_row<T, BSWAP, MASKED, false, 1>(a, c, j, base, mk);

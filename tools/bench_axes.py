@@ -23,6 +23,8 @@ def main():
     shape, chunks = (1024, 1024, 1024), (64, 64, 64)
     data, offsets, _ = chunk_major_device(torch, shape, chunks, np.float32, dev, fill=-999.0, fill_frac=0.01)
     missing = (np.float32(-999.0), None, np.float32(1000.0), np.float32(5e8))
+    if "--unmasked" in sys.argv:
+        missing = None
     plan = ReductionPlan(ctx, np.float32, chunks, data.data_ptr(), offsets, missing=missing, stream=st)
     nbytes = data.numel()
     res = {}
