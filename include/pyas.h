@@ -219,6 +219,31 @@ int pyas_combine_segments(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
                           int64_t n_segments, uint32_t combine_flags,
                           pyas_partial *out, void *stream);
 
+/* Box-query form of the partial-axis combine (active.py:487-516,591-598:
+ * each chunk's partial array is placed at its out_selection in `out`, then
+ * method(out, axis) folds the chunk layers).  For an orthogonal selection the
+ * chunks are the C-ordered product of per-dim chunk-coordinate lists, so the
+ * segments of pyas_combine_segments follow from small per-dim tables and no
+ * per-output index list is built on the host.  Output element f (C order
+ * over out_extent) folds, in C order over the reduced dims' coordinates,
+ * in[chunk_out_offsets[n] + j] where n is the chunk's position in the
+ * product and j the element's index in that chunk's kept-dims partial array
+ * (C order over the chunk's selected counts, reduced dims of extent 1). */
+typedef struct {
+    int32_t ndim;
+    uint32_t axes_mask;                          /* reduced dims */
+    int64_t n_coords[PYAS_MAX_DIMS];             /* chunk coordinates per dim */
+    int64_t out_extent[PYAS_MAX_DIMS];           /* kept dims: final extent; reduced: 1 */
+    const int32_t *pos_coord[PYAS_MAX_DIMS];     /* kept dims (device): position -> coordinate index */
+    const int32_t *pos_local[PYAS_MAX_DIMS];     /* kept dims (device): position -> index in that chunk's selection */
+    const int32_t *coord_count[PYAS_MAX_DIMS];   /* kept dims (device): coordinate index -> selected count */
+    const int64_t *chunk_out_offsets;            /* device [prod n_coords] (pyas_reduce_axes's out_offsets) */
+} pyas_grid;
+
+int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
+                      const pyas_grid *grid, uint32_t combine_flags, pyas_partial *out,
+                      void *stream);
+
 /* Standalone HDF5/numcodecs byte un-shuffle (storage.py:121-122), device to
  * device; n_bytes % elementsize trailing bytes are copied through. */
 int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes,

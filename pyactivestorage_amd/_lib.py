@@ -64,6 +64,20 @@ class Batch(ctypes.Structure):
     ]
 
 
+class Grid(ctypes.Structure):
+    """pyas_grid: per-dim tables of a box query for pyas_combine_grid."""
+    _fields_ = [
+        ("ndim", ctypes.c_int32),
+        ("axes_mask", ctypes.c_uint32),
+        ("n_coords", ctypes.c_int64 * MAX_DIMS),
+        ("out_extent", ctypes.c_int64 * MAX_DIMS),
+        ("pos_coord", ctypes.c_void_p * MAX_DIMS),
+        ("pos_local", ctypes.c_void_p * MAX_DIMS),
+        ("coord_count", ctypes.c_void_p * MAX_DIMS),
+        ("chunk_out_offsets", ctypes.c_void_p),
+    ]
+
+
 PARTIAL_NBYTES = ctypes.sizeof(Partial)
 assert PARTIAL_NBYTES == 32
 
@@ -95,6 +109,7 @@ SIGNATURES = {
     "pyas_select_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _vp, _vp],
     "pyas_combine_partials": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_segments": [_vp, _i32, _vp, _vp, _vp, _i64, _u32, _vp, _vp],
+    "pyas_combine_grid": [_vp, _i32, _vp, ctypes.POINTER(Grid), _u32, _vp, _vp],
     "pyas_unshuffle": [_vp, _vp, _vp, _i64, _i32, _vp],
     "pyas_inflate": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "pyas_read_ranges": [_vp, ctypes.c_int, _i64, _vp, _vp, _vp, _vp, _i32, _vp],

@@ -24,7 +24,7 @@ import concurrent.futures
 import numpy as np
 
 from . import _lib, engine, selection
-from .batch import ReductionPlan
+from .batch import ReductionPlan, _all_full
 from .device import DeviceBuffer, get_context
 from .dtypes import native, sum_dtype
 from .indexing import OrthogonalIndexer
@@ -134,7 +134,7 @@ class Active:
         return self._reduce(indexer, compressor, filters, tuple(sorted(axes)))
 
     # -- host ingest -------------------------------------------------------
-    def _ingest(self, chunk_list, compressor, filters):
+    def _ingest(self, coords, compressor, filters):
         """Read + inflate every touched chunk and upload them as one buffer."""
         ds = self.ds
         nbytes = int(np.prod(ds.chunks)) * ds.dtype.itemsize
@@ -143,7 +143,7 @@ class Active:
         ctx = get_context(self.device)
         st = ctx.thread_stream()
         stride = -(-nbytes // _ALIGN) * _ALIGN
-        infos = [ds.chunk_info(c) for c, _ in chunk_list]
+        infos = [ds.chunk_info(c) for c in coords]
         n = len(infos)
         native_io = ds.reader is None and ds.filename is not None and (
             device_inflate or compressor is None)
@@ -234,7 +234,110 @@ class Active:
         return selection.ChunkSel(dims, shape, kept)
 
     # -- reductions ---------------------------------------------------------
+    def _box_plan(self, indexer):
+        """Vectorised plan of an orthogonal selection of slices and index
+        arrays: the touched chunks are the C-ordered product of per-dim
+        projections (active.py:451-471), so the ABI selection table, index
+        pool and chunk coordinates follow from per-dim entries by
+        broadcasting, with no per-chunk Python objects.  Returns
+        ``(dims, coords, table, pool)`` or None (integer-dropped dims, or
+        vector fill/missing values whose masks need per-chunk selections)."""
+        if any(d.kind == "int" for d in indexer.dim_indexers):
+            return None
+        if any(m is not None and np.size(m) != 1 for m in self.missing):
+            return None
+        dims = [list(d) for d in indexer.dim_indexers]
+        nd = len(dims)
+        n_coords = [len(p) for p in dims]
+        ent, pool_parts, pos = [], [], 0
+        for projs in dims:
+            e = np.zeros((len(projs), 3), dtype=np.int32)
+            for a, p in enumerate(projs):
+                sl = p.chunk_sel
+                if isinstance(sl, slice):
+                    cnt = len(p.out_pos)
+                    e[a] = (sl.start if cnt else 0, sl.step, cnt)
+                else:
+                    e[a] = (pos, 0, sl.size)
+                    pool_parts.append(np.asarray(sl, dtype=np.int32))
+                    pos += sl.size
+            ent.append(e)
+        n = int(np.prod(n_coords))
+        idx = np.indices(n_coords).reshape(nd, n)
+        table = np.zeros((n, _lib.MAX_DIMS, 3), dtype=np.int32)
+        table[:, :, 1] = 1
+        table[:, :, 2] = 1
+        coords = np.zeros((n, nd), dtype=np.int64)
+        for d in range(nd):
+            table[:, d, :] = ent[d][idx[d]]
+            coords[:, d] = np.array([p.chunk_ix for p in dims[d]], dtype=np.int64)[idx[d]]
+        pool = np.concatenate(pool_parts) if pool_parts else np.zeros(1, dtype=np.int32)
+        return dims, coords, table, pool
+
     def _reduce(self, indexer, compressor, filters, axes):
+        box = self._box_plan(indexer)
+        if box is None:
+            return self._reduce_general(indexer, compressor, filters, axes)
+        ds = self.ds
+        dt = ds.dtype
+        dims, coords, table, pool = box
+        final_shape = tuple(1 if i in axes else n for i, n in enumerate(indexer.shape))
+        n_final = int(np.prod(final_shape))
+        pdt = engine.partial_dtype(dt)
+        if len(coords) == 0:
+            final = np.zeros(n_final, dtype=pdt)
+            return self._format(final.reshape(final_shape), final_shape)
+        ctx, st, buf, offsets, fused = self._ingest([tuple(c) for c in coords.tolist()],
+                                                    compressor, filters)
+        full = _all_full(table, ds.chunks)   # whole chunks: no table, dense kernels
+        plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused,
+                             sel_table=None if full else table, index_pool=None if full else pool,
+                             missing=self.missing, round_to_var=True, stream=st)
+        if len(axes) == ds.ndim:
+            plan.launch(st, chunk_partials=False)
+            final = plan.read_total(st)
+            return self._format(final.reshape(final_shape), final_shape)
+        return self._grid_combine(ctx, st, plan, self._grid_from_dims(dims, axes, final_shape),
+                                  axes, final_shape)
+
+    def _grid_combine(self, ctx, st, plan, grid, axes, final_shape):
+        """Partial axes over a box query: per-chunk partial arrays
+        (pyas_reduce_axes), then pyas_combine_grid into the final grid."""
+        ds = self.ds
+        dt = ds.dtype
+        n_final = int(np.prod(final_shape))
+        axes_mask = 0
+        for a in axes:
+            axes_mask |= 1 << a
+        out_off, tables = grid
+        obuf = DeviceBuffer(ctx, out_off.nbytes)
+        ctx.h2d(obuf.ptr, out_off, st)
+        tbuf = DeviceBuffer(ctx, max(tables["blob"].nbytes, 16))
+        ctx.h2d(tbuf.ptr, tables["blob"], st)
+        g = _lib.Grid()
+        g.ndim = ds.ndim
+        g.axes_mask = axes_mask
+        for d in range(ds.ndim):
+            g.n_coords[d] = tables["n_coords"][d]
+            g.out_extent[d] = final_shape[d] if d not in axes else 1
+            if d not in axes:
+                g.pos_coord[d] = tbuf.ptr + 4 * tables["pos_coord"][d]
+                g.pos_local[d] = tbuf.ptr + 4 * tables["pos_local"][d]
+                g.coord_count[d] = tbuf.ptr + 4 * tables["coord_count"][d]
+        g.chunk_out_offsets = obuf.ptr
+        n_parts = int(tables["n_parts"])
+        parts = DeviceBuffer(ctx, max(n_parts, 1) * _lib.PARTIAL_NBYTES)
+        fin = DeviceBuffer(ctx, max(n_final, 1) * _lib.PARTIAL_NBYTES)
+        engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st)
+        engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st)
+        final = np.zeros(n_final, dtype=engine.partial_dtype(dt))
+        ctx.d2h(final, fin.ptr, st)
+        ctx.synchronize(st)
+        return self._format(final.reshape(final_shape), final_shape)
+
+    def _reduce_general(self, indexer, compressor, filters, axes):
+        """Per-chunk selection objects and host-built segments: integer-
+        dropped dims and vector fill/missing values."""
         ds = self.ds
         dt = ds.dtype
         chunk_list = list(indexer)
@@ -244,7 +347,7 @@ class Active:
         if not chunk_list:
             final = np.zeros(n_final, dtype=pdt)
             return self._format(final.reshape(final_shape), final_shape)
-        ctx, st, buf, offsets, fused = self._ingest(chunk_list, compressor, filters)
+        ctx, st, buf, offsets, fused = self._ingest([c for c, _ in chunk_list], compressor, filters)
         sels = [self._chunk_sel(projs) for _, projs in chunk_list]
         plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused, selections=sels,
                              missing=self.missing, round_to_var=True, stream=st)
@@ -252,7 +355,13 @@ class Active:
             plan.launch(st, chunk_partials=False)
             final = plan.read_total(st)
             return self._format(final.reshape(final_shape), final_shape)
-        # partial axes: per-chunk partial arrays, then a segmented device combine
+        axes_mask = 0
+        for a in axes:
+            axes_mask |= 1 << a
+        grid = self._grid_tables(chunk_list, axes, final_shape)
+        if grid is not None:
+            return self._grid_combine(ctx, st, plan, grid, axes, final_shape)
+        # general case: per-chunk partial arrays, then a segmented device combine
         sizes, fidx = [], []
         for _, projs in chunk_list:
             pos = [p.out_pos if i not in axes else np.zeros(1, dtype=np.int64)
@@ -281,6 +390,71 @@ class Active:
         ctx.synchronize(st)
         return self._format(final.reshape(final_shape), final_shape)
 
+    def _grid_tables(self, chunk_list, axes, final_shape):
+        """``_grid_from_dims`` for a materialised chunk list, when its chunks
+        are the C-ordered product of per-dim projections; else None."""
+        nd = self.ds.ndim
+        seen = [dict() for _ in range(nd)]
+        dims = [[] for _ in range(nd)]
+        idx = np.empty((len(chunk_list), nd), dtype=np.int64)
+        for k, (cc, projs) in enumerate(chunk_list):
+            if len(projs) != nd:
+                return None
+            for d in range(nd):
+                p = projs[d]
+                if isinstance(p.chunk_sel, (int, np.integer)):
+                    return None
+                a = seen[d].get(cc[d])
+                if a is None:
+                    a = seen[d][cc[d]] = len(dims[d])
+                    dims[d].append(p)
+                idx[k, d] = a
+        n_coords = [len(o) for o in dims]
+        if int(np.prod(n_coords)) != len(chunk_list):
+            return None
+        if not (np.ravel_multi_index(idx.T, n_coords) == np.arange(len(chunk_list))).all():
+            return None
+        return self._grid_from_dims(dims, axes, final_shape)
+
+    @staticmethod
+    def _grid_from_dims(dims, axes, final_shape):
+        """Tables of ``pyas_combine_grid`` from per-dim projections (chunks =
+        their C-ordered product).  Returns ``(out_off, tables)``: ``out_off[n]``
+        is chunk n's offset in the partial array (its kept-dims selection, C
+        order); ``tables`` holds one int32 blob with, per kept dim, position
+        -> coordinate index, position -> index inside that chunk's selection
+        and coordinate -> selected count (offsets in int32 units)."""
+        nd = len(dims)
+        n_coords = [len(p) for p in dims]
+        kept = [d for d in range(nd) if d not in axes]
+        counts = {d: np.array([len(p.out_pos) for p in dims[d]], dtype=np.int64) for d in kept}
+        n = int(np.prod(n_coords))
+        idx = np.indices(n_coords).reshape(nd, n)
+        sizes = np.ones(n, dtype=np.int64)
+        for d in kept:
+            sizes *= counts[d][idx[d]]
+        out_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+        parts, off = [], 0
+        tables = {"n_coords": n_coords, "pos_coord": {}, "pos_local": {}, "coord_count": {},
+                  "n_parts": int(sizes.sum())}
+        for d in kept:
+            F = final_shape[d]
+            pc = np.full(F, -1, dtype=np.int32)
+            pl = np.zeros(F, dtype=np.int32)
+            for a, p in enumerate(dims[d]):
+                o = np.asarray(p.out_pos, dtype=np.int64)
+                pc[o] = a
+                pl[o] = np.arange(o.size, dtype=np.int32)
+            if (pc < 0).any():
+                raise AssertionError("output positions not covered by the chunk projections")
+            for name, arr in (("pos_coord", pc), ("pos_local", pl),
+                              ("coord_count", counts[d].astype(np.int32))):
+                tables[name][d] = off
+                parts.append(arr)
+                off += arr.size
+        tables["blob"] = np.concatenate(parts) if parts else np.zeros(1, dtype=np.int32)
+        return out_off, tables
+
     def _format(self, final, shape):
         """active.py:591-630 on combined partials."""
         dt = self.ds.dtype
@@ -305,7 +479,7 @@ class Active:
         out_vals = np.zeros(indexer.shape, dtype=dt)
         out_mask = np.zeros(indexer.shape, dtype=bool)
         if chunk_list:
-            ctx, st, buf, offsets, fused = self._ingest(chunk_list, compressor, filters)
+            ctx, st, buf, offsets, fused = self._ingest([c for c, _ in chunk_list], compressor, filters)
             sels = [self._chunk_sel(projs) for _, projs in chunk_list]
             plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused,
                                  selections=sels, missing=self.missing, stream=st)

@@ -616,6 +616,35 @@ int pyas_combine_segments(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
     return PYAS_OK;
 }
 
+int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, const pyas_grid *g,
+                      uint32_t combine_flags, pyas_partial *out, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (elem_size(dtype) == 0) return fail(PYAS_ENOTSUP, "unsupported dtype code %d", dtype);
+    if (!g) return fail(PYAS_EINVAL, "grid is NULL");
+    if (g->ndim < 1 || g->ndim > PYAS_MAX_DIMS)
+        return fail(PYAS_EINVAL, "grid rank %d outside 1..%d", g->ndim, PYAS_MAX_DIMS);
+    if (g->axes_mask >> g->ndim) return fail(PYAS_EINVAL, "axes mask 0x%x beyond rank %d", g->axes_mask, g->ndim);
+    if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
+        return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
+    int64_t n_out = 1, n_layers = 1;
+    for (int d = 0; d < g->ndim; ++d) {
+        if (g->n_coords[d] < 1) return fail(PYAS_EINVAL, "n_coords[%d] = %lld", d, (long long)g->n_coords[d]);
+        if ((g->axes_mask >> d) & 1u) {
+            n_layers *= g->n_coords[d];
+        } else {
+            if (g->out_extent[d] < 1) return fail(PYAS_EINVAL, "out_extent[%d] = %lld", d, (long long)g->out_extent[d]);
+            if (!g->pos_coord[d] || !g->pos_local[d] || !g->coord_count[d])
+                return fail(PYAS_EINVAL, "kept dim %d has a NULL table", d);
+            n_out *= g->out_extent[d];
+        }
+    }
+    if (!in || !out || !g->chunk_out_offsets) return fail(PYAS_EINVAL, "NULL argument");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(pyas::launch_combine_grid(dtype, in, *g, n_out, n_layers, combine_flags, out,
+                                       (hipStream_t)stream));
+    return PYAS_OK;
+}
+
 int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes, int32_t elementsize,
                    void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");

@@ -104,6 +104,10 @@ hipError_t launch_combine_segments_t(const pyas_partial *in, const int64_t *inde
 template <typename T>
 hipError_t launch_axes_t(const AxesArgs &a, int64_t grid, hipStream_t st);
 template <typename T>
+hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int64_t n_out,
+                                 int64_t n_layers, uint32_t flags, pyas_partial *out,
+                                 hipStream_t st);
+template <typename T>
 hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
 template <typename T>
 hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st);
@@ -118,6 +122,9 @@ hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int6
                                    const int64_t *seg, int64_t n_seg, uint32_t flags,
                                    pyas_partial *out, hipStream_t st);
 hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st);
+hipError_t launch_combine_grid(int dtype, const pyas_partial *in, const pyas_grid &g,
+                               int64_t n_out, int64_t n_layers, uint32_t flags,
+                               pyas_partial *out, hipStream_t st);
 hipError_t launch_axes_dense(int dtype, const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
 hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);

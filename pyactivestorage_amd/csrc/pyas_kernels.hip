@@ -67,6 +67,13 @@ hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStr
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_combine_grid(int dtype, const pyas_partial *in, const pyas_grid &g,
+                               int64_t n_out, int64_t n_layers, uint32_t flags,
+                               pyas_partial *out, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_combine_grid_t<T>(in, g, n_out, n_layers, flags, out, st));
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_axes_dense(int dtype, const AxesArgs &a, bool masked, int64_t grid, hipStream_t st) {
     PYAS_DISPATCH_T(dtype, return launch_axes_dense_t<T>(a, masked, grid, st));
     return hipErrorInvalidValue;

@@ -595,6 +595,55 @@ __global__ __launch_bounds__(kBlock) void k_combine_segments(const pyas_partial 
     store_wpartial(out + sidx, acc);
 }
 
+// box-query combine (pyas_combine_grid): one thread per final output element,
+// chunk layers folded in C order of the reduced dims' coordinates
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in, pyas_grid g,
+                                                         int64_t n_out, int64_t n_layers,
+                                                         uint32_t flags, pyas_partial *out) {
+    const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (f >= n_out) return;
+    const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
+    int64_t a[PYAS_MAX_DIMS], gstride[PYAS_MAX_DIMS];
+    int64_t j = 0, jstride = 1, rest = f, st = 1;
+#pragma unroll
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+        a[d] = 0;
+        gstride[d] = st;
+        if (d < g.ndim) {
+            st *= g.n_coords[d];
+            if (!((g.axes_mask >> d) & 1u)) {
+                const int64_t e = g.out_extent[d];
+                const int64_t p = rest % e;
+                rest /= e;
+                a[d] = g.pos_coord[d][p];
+                j += (int64_t)g.pos_local[d][p] * jstride;
+                jstride *= g.coord_count[d][a[d]];
+            }
+        }
+    }
+    int64_t nk = 0;   // chunk position from the kept coordinates
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+        if (d < g.ndim && !((g.axes_mask >> d) & 1u)) nk += a[d] * gstride[d];
+    WAcc<T> acc;
+    acc.init();
+    for (int64_t l = 0; l < n_layers; ++l) {
+        int64_t n = nk, r = l;
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            if (d < g.ndim && ((g.axes_mask >> d) & 1u)) {
+                const int64_t c = g.n_coords[d];
+                const int64_t q = r / c;
+                n += (r - q * c) * gstride[d];
+                r = q;
+            }
+        }
+        merge(acc, in[g.chunk_out_offsets[n] + j], round);
+    }
+    store_wpartial(out + f, acc);
+}
+
 // ---------------------------------------------------------------------------
 // partial-axis reduction (axis ⊂ dims), one thread per output element
 // ---------------------------------------------------------------------------
@@ -1253,6 +1302,15 @@ hipError_t launch_combine_segments_t(const pyas_partial *in, const int64_t *inde
     return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int64_t n_out,
+                                 int64_t n_layers, uint32_t flags, pyas_partial *out,
+                                 hipStream_t st) {
+    const dim3 grid((unsigned)((n_out + kBlock - 1) / kBlock)), blk(kBlock);
+    hipLaunchKernelGGL((k_combine_grid<T>), grid, blk, 0, st, in, g, n_out, n_layers, flags, out);
+    return hipGetLastError();
+}
+
 template <typename T, int MODE>
 static void launch_dense_m(const AxesArgs &a, bool masked, dim3 g, hipStream_t st) {
     const dim3 blk(kBlock);
@@ -1305,6 +1363,9 @@ hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st) {
                                                      const int64_t *, int64_t, uint32_t,     \
                                                      pyas_partial *, hipStream_t);           \
     template hipError_t launch_axes_t<T>(const AxesArgs &, int64_t, hipStream_t);             \
+    template hipError_t launch_combine_grid_t<T>(const pyas_partial *, const pyas_grid &,     \
+                                                 int64_t, int64_t, uint32_t, pyas_partial *,  \
+                                                 hipStream_t);                               \
     template hipError_t launch_axes_dense_t<T>(const AxesArgs &, bool, int64_t, hipStream_t); \
     template hipError_t launch_select_t<T>(const SelectArgs &, int64_t, hipStream_t);
 

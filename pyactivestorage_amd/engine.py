@@ -114,6 +114,12 @@ def combine_segments(ctx: Context, dt, in_ptr, index_ptr, seg_ptr, n_seg, out_pt
                "pyas_combine_segments")
 
 
+def combine_grid(ctx: Context, dt, in_ptr, grid: _lib.Grid, out_ptr, round_to_var: bool, stream) -> None:
+    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
+    _lib.check(ctx.lib.pyas_combine_grid(ctx.handle, dtype_code(dt), in_ptr, ctypes.byref(grid), flags,
+                                         out_ptr, stream), "pyas_combine_grid")
+
+
 def unshuffle(ctx: Context, src_ptr, dst_ptr, nbytes, elementsize, stream) -> None:
     _lib.check(ctx.lib.pyas_unshuffle(ctx.handle, src_ptr, dst_ptr, int(nbytes), int(elementsize),
                                       stream), "pyas_unshuffle")

@@ -93,3 +93,76 @@ def test_decode_filters_mapping():
         decode_filters([{"filter_id": 32001, "client_data": []}], 4, "x")
     with pytest.raises(ValueError):
         decode_filters([{"filter_id": 1, "client_data": [1]}, {"filter_id": 1, "client_data": [1]}], 4, "x")
+
+
+# ---------------------------------------------------------------------------
+# pyas_combine_grid tables (Active._grid_tables) vs the general segment plan
+# ---------------------------------------------------------------------------
+def _segments_argsort(chunk_list, axes, final_shape):
+    """The general path of Active._reduce: per output, the partial indices in
+    chunk order (what pyas_combine_segments folds)."""
+    sizes, fidx = [], []
+    for _, projs in chunk_list:
+        pos = [p.out_pos if i not in axes else np.zeros(1, dtype=np.int64) for i, p in enumerate(projs)]
+        grids = np.meshgrid(*pos, indexing="ij")
+        fidx.append(np.ravel_multi_index([g.reshape(-1) for g in grids], final_shape))
+        sizes.append(grids[0].size)
+    out_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    f_all = np.concatenate(fidx)
+    order = np.argsort(f_all, kind="stable")
+    seg = np.searchsorted(f_all[order], np.arange(int(np.prod(final_shape)) + 1))
+    return [list(order[seg[f]:seg[f + 1]]) for f in range(len(seg) - 1)]
+
+
+def _segments_grid(out_off, t, axes, final_shape, nd):
+    """k_combine_grid's index arithmetic restated on the host."""
+    blob = t["blob"]
+    n_coords = t["n_coords"]
+    gstride = [int(np.prod(n_coords[d + 1:])) for d in range(nd)]
+    red = [d for d in range(nd) if d in axes]
+    out = []
+    for f in range(int(np.prod(final_shape))):
+        p = np.unravel_index(f, final_shape)
+        a = [0] * nd
+        j, jstride = 0, 1
+        for d in reversed(range(nd)):
+            if d in axes:
+                continue
+            a[d] = int(blob[t["pos_coord"][d] + p[d]])
+            j += int(blob[t["pos_local"][d] + p[d]]) * jstride
+            jstride *= int(blob[t["coord_count"][d] + a[d]])
+        nk = sum(a[d] * gstride[d] for d in range(nd) if d not in axes)
+        seg = []
+        for layer in np.ndindex(*[n_coords[d] for d in red]):
+            n = nk + sum(c * gstride[d] for c, d in zip(layer, red))
+            seg.append(int(out_off[n]) + j)
+        out.append(seg)
+    return out
+
+
+@pytest.mark.parametrize("index", [
+    (slice(None), slice(None), slice(None)),
+    (slice(1, 9), slice(2, 11, 2), slice(None)),
+    (slice(1, 10, 3), slice(None), slice(3, 7)),
+    (slice(None), [0, 5, 6, 11], slice(1, 8)),
+    ([7, 1, 3], slice(None), slice(None, None, 3)),
+])
+@pytest.mark.parametrize("axes", [(0,), (1,), (2,), (0, 1), (0, 2), (1, 2)])
+def test_grid_tables_match_segments(index, axes):
+    from pyactivestorage_amd.active import Active
+    from pyactivestorage_amd.indexing import OrthogonalIndexer
+    shape, chunks = (10, 12, 9), (4, 5, 3)
+    ix = OrthogonalIndexer(index, shape, chunks)
+    chunk_list = list(ix)
+    final_shape = tuple(1 if i in axes else n for i, n in enumerate(ix.shape))
+
+    class _DS:
+        ndim = 3
+    act = Active.__new__(Active)
+    act.ds = _DS()
+    res = Active._grid_tables(act, chunk_list, axes, final_shape)
+    assert res is not None
+    out_off, t = res
+    want = _segments_argsort(chunk_list, axes, final_shape)
+    got = _segments_grid(out_off, t, axes, final_shape, 3)
+    assert got == want

@@ -1,0 +1,73 @@
+"""End-to-end Active queries on the C3 workload (1024^3 f32 in 64^3 chunks,
+_FillValue + valid_min/valid_max): a chunk-major file in the page cache ->
+Active.__getitem__ (plan, native pread ring -> H2D, fused reduce, combine)
+-> masked result.  Times whole queries for the full reduction and for
+partial-axis reductions (row f1 end to end, active.py:487-516,591-630).
+
+    python tools/bench_active.py [--reps 3] [--shape 1024]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--shape", type=int, default=1024)
+    a = ap.parse_args()
+    import torch
+    from pyactivestorage_amd.active import Active
+    from pyactivestorage_amd.synthetic import chunk_major_device
+    from pyactivestorage_amd.variable import ChunkedVariable
+    n, c = a.shape, 64
+    shape, chunks = (n, n, n), (c, c, c)
+    dev = torch.device("cuda", 0)
+    data, offsets, _ = chunk_major_device(torch, shape, chunks, np.float32, dev, fill=-999.0, fill_frac=0.01)
+    path = os.path.join(tempfile.gettempdir(), f"pyas_active_{os.getpid()}.chunks")
+    res = {}
+    try:
+        with open(path, "wb") as f:
+            step = 256 << 20
+            for o in range(0, data.numel(), step):
+                f.write(data[o:o + step].cpu().numpy().tobytes())
+        del data
+        torch.cuda.empty_cache()
+        grid = [s // k for s, k in zip(shape, chunks)]
+        cb = c * c * c * 4
+        index = {cc: (int(offsets[i]), cb) for i, cc in enumerate(np.ndindex(*grid))}
+        attrs = {"_FillValue": np.array([-999.0], dtype=np.float32),
+                 "valid_min": np.array([1000.0], dtype=np.float32),
+                 "valid_max": np.array([5e8], dtype=np.float32)}
+        var = ChunkedVariable(name="c3", shape=shape, chunks=chunks, dtype=np.float32,
+                              chunk_index=index, attrs=attrs, filename=path)
+        nbytes = n ** 3 * 4
+        for axis in (None, (0,), (1,), (2,), (0, 1), (1, 2), (0, 2)):
+            act = Active(var)
+            act.mean(axis=axis)
+            act[...]                       # warm-up (pinned ring, kernels)
+            times = []
+            for _ in range(a.reps):
+                act.mean(axis=axis)
+                t0 = time.perf_counter()
+                r = act[...]
+                times.append(time.perf_counter() - t0)
+            t = float(np.median(times))
+            res[str(axis)] = {"s": round(t, 4), "GBps_file_to_result": round(nbytes / t / 1e9, 2),
+                              "result_shape": list(np.shape(r))}
+            print(json.dumps({str(axis): res[str(axis)]}), flush=True)
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+    print(json.dumps({"workload": f"Active.mean over c3 {shape} file (page cache) -> result", "results": res}))
+
+
+if __name__ == "__main__":
+    main()
