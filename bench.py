@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--cpu-chunks", type=int, default=4096,
                    help="chunks in the CPU-baseline sample (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=30)
+    p.add_argument("--force-dist", action="store_true",
+                   help="rehearsal: run the RCCL branch (init, all-gather, device combine) "
+                        "even at world size 1 (launch under torch.distributed.run)")
     p.add_argument("--host-inclusive", type=int, default=1,
                    help="also time pinned host -> H2D -> reduce -> D2H (rank 0, N=1)")
     p.add_argument("--file-inclusive", type=int, default=1,
@@ -228,7 +231,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -285,7 +289,7 @@ def main():
     final = torch.zeros(_lib.PARTIAL_NBYTES, dtype=torch.uint8, device=dev)
 
     def step():
-        if world > 1:
+        if use_dist:
             reduce_sharded(torch, plan, ctx, stream, final)
         else:
             plan.launch(stream, chunk_partials=False)
@@ -294,14 +298,14 @@ def main():
         step()
     torch.cuda.synchronize()
     _lib.check(ctx.lib.pyas_timing_enable(ctx.handle, args.steps), "timing_enable")
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     import ctypes
@@ -309,7 +313,7 @@ def main():
     nrec = ctypes.c_int32(0)
     _lib.check(ctx.lib.pyas_timing_read(ctx.handle, ms, args.steps, ctypes.byref(nrec)), "timing_read")
     kern_ms = float(np.mean(np.array(ms[: nrec.value]))) if nrec.value else float("nan")
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms_max = float(t[0]), float(t[1])
@@ -323,13 +327,13 @@ def main():
         check["kernel_count"] = local["count"]
         check["ok"] = check["torch_count"] == local["count"]
     result = local
-    if world > 1:
+    if use_dist:
         fin = np.frombuffer(final.cpu().numpy().tobytes(), dtype=engine.partial_dtype(dt))[0]
         result = {"sum": float(fin["sum"]), "count": int(fin["count"]), "min": float(fin["min"]),
                   "max": float(fin["max"])}
 
     ms_per_step = elapsed / args.steps * 1e3
-    if world > 1:
+    if use_dist:
         agg = torch.tensor([bytes_per_launch, n_chunks], dtype=torch.float64, device=dev)
         dist.all_reduce(agg)
         total_bytes, total_chunks = float(agg[0]), float(agg[1])
@@ -398,7 +402,7 @@ def main():
             "file_inclusive": fileinc,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 
