@@ -359,54 +359,133 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
             status = PYAS_INFLATE_BAD_BLOCK;
             break;
         }
-        // symbol loop
-        for (;;) {
-            if (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
-            if (in.pos > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
-            uint32_t bits = in.peek();
-            uint32_t l;
-            uint32_t sym = decode(bits, lit, kLitBits, L.lit_cnt, L.lit_sym, l);
-            if (!l) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
-            if (sym < 256) {
-                if (o.pos >= o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
-                if (lane == 0) win[o.pos & kWinMask] = (uint8_t)sym;
-                o.pos++;
-                in.pos += l;
-                continue;
-            }
-            if (sym == 256) { in.pos += l; break; }
-            sym -= 257;
-            if (sym >= 29) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
-            const uint32_t le = c_len_extra[sym];
-            const uint32_t len = c_len_base[sym] + ((bits >> l) & ((1u << le) - 1u));
-            in.pos += l + le;
-            bits = in.peek();
-            const uint32_t ds = decode(bits, dist, kDistBits, L.dist_cnt, L.dist_sym, l);
-            if (!l || ds >= 30) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
-            const uint32_t de = c_dist_extra[ds];
-            const uint32_t d = c_dist_base[ds] + ((bits >> l) & ((1u << de) - 1u));
-            in.pos += l + de;
-            if (d > o.pos) { status = PYAS_INFLATE_BAD_DISTANCE; break; }
-            if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
+        // Match copy out[p+i] = out[p-d+(i mod d)], lane-parallel (all
+        // sources precede p); beyond the ring every source byte is in dst.
+        auto copy_match = [&](uint32_t d, uint32_t len) {
             const uint32_t from = o.pos - d;
-            if (d > kWin) {   // beyond the ring: every source byte is already in dst
+            if (d > kWin) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 for (uint32_t r = 0; r < len; r += 64) {
                     const uint32_t i = r + lane;
                     if (i < len) win[(o.pos + i) & kWinMask] = (uint8_t)far_byte(o.dst + from + i);
                 }
-                o.pos += len;
-                continue;
-            }
-            for (uint32_t r = 0; r < len; r += 64) {
-                const uint32_t i = r + lane;
-                if (i < len) {
-                    const uint32_t srcp = from + (d >= len ? i : i % d);
-                    win[(o.pos + i) & kWinMask] = win[srcp & kWinMask];
+            } else {
+                for (uint32_t r = 0; r < len; r += 64) {
+                    const uint32_t i = r + lane;
+                    if (i < len) {
+                        const uint32_t srcp = from + (d >= len ? i : i % d);
+                        win[(o.pos + i) & kWinMask] = win[srcp & kWinMask];
+                    }
                 }
             }
             o.pos += len;
+        };
+        // One symbol, any code length (canonical walk past the root tables).
+        // Returns 0 = continue, 1 = end of block, 2 = error (status set).
+        auto one_symbol = [&]() -> int {
+            if (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
+            if (in.pos > in.nbits) { status = PYAS_INFLATE_TRUNCATED; return 2; }
+            uint32_t bits = in.peek();
+            uint32_t l;
+            uint32_t sym = decode(bits, lit, kLitBits, L.lit_cnt, L.lit_sym, l);
+            if (!l) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
+            if (sym < 256) {
+                if (o.pos >= o.cap) { status = PYAS_INFLATE_OVERFLOW; return 2; }
+                if (lane == 0) win[o.pos & kWinMask] = (uint8_t)sym;
+                o.pos++;
+                in.pos += l;
+                return 0;
+            }
+            if (sym == 256) { in.pos += l; return 1; }
+            sym -= 257;
+            if (sym >= 29) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
+            const uint32_t le = c_len_extra[sym];
+            const uint32_t len = c_len_base[sym] + ((bits >> l) & ((1u << le) - 1u));
+            in.pos += l + le;
+            bits = in.peek();
+            const uint32_t ds = decode(bits, dist, kDistBits, L.dist_cnt, L.dist_sym, l);
+            if (!l || ds >= 30) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
+            const uint32_t de = c_dist_extra[ds];
+            const uint32_t d = c_dist_base[ds] + ((bits >> l) & ((1u << de) - 1u));
+            in.pos += l + de;
+            if (d > o.pos) { status = PYAS_INFLATE_BAD_DISTANCE; return 2; }
+            if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; return 2; }
+            copy_match(d, len);
+            return 0;
+        };
+        // Symbol loop.  Fast path: a speculative window.  Lane k holds the 32
+        // bits at pos + k and looks up both root tables there, in one LDS
+        // round trip for the whole wave; the symbol chain is then walked on
+        // the scalar unit with v_readlane (a symbol at window offset `off`
+        // is lane off's entry; its length extra bits come from lane off's
+        // bits, the distance code from lane off + l + le).  A code longer
+        // than its root table, or a length/distance pair that would start
+        // its distance past the window, drops to one_symbol / a new window.
+        bool eob = false;
+        while (!eob) {
+            in.peek();                                   // cur/nxt hold the window
+            const uint32_t k0 = in.pos >> 5, sh = in.pos & 31;
+            const uint32_t w0 = in.word(k0), w1 = in.word(k0 + 1), w2 = in.word(k0 + 2),
+                           w3 = in.word(k0 + 3);
+            const uint32_t t = sh + (uint32_t)lane;       // 0..94
+            const uint32_t wb = t >> 5;
+            const uint32_t lo = wb == 0 ? w0 : wb == 1 ? w1 : w2;
+            const uint32_t hi = wb == 0 ? w1 : wb == 1 ? w2 : w3;
+            const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (t & 31));
+            const uint32_t E = lit[v & ((1u << kLitBits) - 1u)];
+            const uint32_t D = dist[v & ((1u << kDistBits) - 1u)];
+            auto rl = [](uint32_t x, uint32_t k) {
+                return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)k);
+            };
+            uint32_t off = 0;
+            bool slow = false;
+            for (;;) {
+                if (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
+                if (off > 63) break;
+                if (in.pos + off > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
+                const uint32_t e = rl(E, off);
+                const uint32_t l = e >> 9;
+                if (!l) { slow = true; break; }
+                uint32_t sym = e & 511u;
+                if (sym < 256) {
+                    if (o.pos >= o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
+                    if (lane == 0) win[o.pos & kWinMask] = (uint8_t)sym;
+                    o.pos++;
+                    off += l;
+                    continue;
+                }
+                if (sym == 256) { off += l; eob = true; break; }
+                sym -= 257;
+                if (sym >= 29) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
+                // RFC 1951 3.2.5 length/distance bases, arithmetic form
+                const uint32_t le = (sym < 8 || sym == 28) ? 0u : (sym - 4u) >> 2;
+                const uint32_t lbase = sym < 8 ? sym + 3u : sym == 28 ? 258u : ((4u + (sym & 3u)) << le) + 3u;
+                const uint32_t doff = off + l + le;
+                if (doff > 63) break;                    // next window starts at this symbol
+                const uint32_t len = lbase + ((rl(v, off) >> l) & ((1u << le) - 1u));
+                const uint32_t f = rl(D, doff);
+                const uint32_t dl = f >> 9;
+                if (!dl) { slow = true; break; }         // long distance code
+                const uint32_t ds = f & 511u;
+                if (ds >= 30) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
+                const uint32_t de = ds < 4 ? 0u : (ds - 2u) >> 1;
+                const uint32_t dbase = ds < 4 ? ds + 1u : ((2u + (ds & 1u)) << de) + 1u;
+                const uint32_t d = dbase + ((rl(v, doff) >> dl) & ((1u << de) - 1u));
+                if (d > o.pos) { status = PYAS_INFLATE_BAD_DISTANCE; break; }
+                if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
+                off = doff + dl + de;
+                copy_match(d, len);
+            }
+            if (status) break;
+            in.pos += off;
+            if (eob) break;
+            if (slow) {
+                const int r = one_symbol();
+                if (r == 2) break;
+                if (r == 1) eob = true;
+            }
         }
+        if (status) break;
     }
     if (status == 0) {
         __syncthreads();
