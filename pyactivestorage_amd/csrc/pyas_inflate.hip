@@ -380,9 +380,34 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
             }
             o.pos += len;
         };
+        // A short match (len <= 64, source in the ring) is split: its ring
+        // read is issued at once, its write is deferred until the next ring
+        // read or flush, so the LDS round trip overlaps the decode of the
+        // symbols that follow (they only write later positions).
+        uint32_t pend_v = 0, pend_p = 0, pend_n = 0;
+        auto issue_pending = [&]() {
+            if (pend_n) {
+                if ((uint32_t)lane < pend_n) win[(pend_p + lane) & kWinMask] = (uint8_t)pend_v;
+                pend_n = 0;
+            }
+        };
+        auto start_match = [&](uint32_t d, uint32_t len) {
+            issue_pending();
+            if (len <= 64 && d <= kWin) {
+                const uint32_t from = o.pos - d;
+                const uint32_t i = (uint32_t)lane < len ? (uint32_t)lane : 0u;
+                pend_v = win[(from + (d >= len ? i : i % d)) & kWinMask];
+                pend_p = o.pos;
+                pend_n = len;
+                o.pos += len;
+            } else {
+                copy_match(d, len);
+            }
+        };
         // One symbol, any code length (canonical walk past the root tables).
         // Returns 0 = continue, 1 = end of block, 2 = error (status set).
         auto one_symbol = [&]() -> int {
+            issue_pending();
             if (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
             if (in.pos > in.nbits) { status = PYAS_INFLATE_TRUNCATED; return 2; }
             uint32_t bits = in.peek();
@@ -440,7 +465,10 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
             uint32_t off = 0;
             bool slow = false;
             for (;;) {
-                if (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
+                if (o.pos - o.fpos >= kFlush) {
+                    issue_pending();
+                    flush<kWinMask>(win, o, kFlush);
+                }
                 if (off > 63) break;
                 if (in.pos + off > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
                 const uint32_t e = rl(E, off);
@@ -474,7 +502,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
                 if (d > o.pos) { status = PYAS_INFLATE_BAD_DISTANCE; break; }
                 if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
                 off = doff + dl + de;
-                copy_match(d, len);
+                start_match(d, len);
             }
             if (status) break;
             in.pos += off;
@@ -485,6 +513,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
                 if (r == 1) eob = true;
             }
         }
+        issue_pending();
         if (status) break;
     }
     if (status == 0) {
