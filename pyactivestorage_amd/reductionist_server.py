@@ -264,6 +264,9 @@ def _err(msg):
 
 class _Handler(http.server.BaseHTTPRequestHandler):
     protocol_version = "HTTP/1.1"
+    # headers and body go out as two writes on a keep-alive connection:
+    # without TCP_NODELAY, Nagle + the client's delayed ACK add ~40 ms each
+    disable_nagle_algorithm = True
 
     def do_POST(self):  # noqa: N802 (http.server API)
         parts = [p for p in urllib.parse.urlparse(self.path).path.split("/") if p]
@@ -288,11 +291,22 @@ class ReductionistServer(http.server.ThreadingHTTPServer):
     """``ReductionistServer(root, ("127.0.0.1", 0))``; ``.url`` is its base URL."""
 
     daemon_threads = True
+    # the reference client opens one connection per pool thread at once
+    # (active.py:557, up to max_threads): socketserver's default listen
+    # backlog of 5 resets the rest
+    request_queue_size = 256
 
-    def __init__(self, root, address=("127.0.0.1", 8080), verbose=False):
+    def __init__(self, root, address=("127.0.0.1", 8080), verbose=False, reuse_port=False):
         self.root = root
         self.verbose = verbose
+        self.reuse_port = reuse_port
         super().__init__(address, _Handler)
+
+    def server_bind(self):
+        if self.reuse_port:   # worker processes share one port (the kernel balances)
+            import socket
+            self.socket.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+        super().server_bind()
 
     @property
     def url(self):
@@ -313,10 +327,33 @@ def main(argv=None):
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8080)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--workers", type=int, default=1,
+                    help="server processes sharing the port (SO_REUSEPORT); each has its own "
+                         "GPU context, so request handling scales past one Python interpreter")
+    ap.add_argument("--reuse-port", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
-    srv = ReductionistServer(a.root, (a.host, a.port), a.verbose)
-    print(f"serving {a.root} at {srv.url}/v2/<operation>/", flush=True)
-    srv.serve_forever()
+    if a.workers > 1 and a.port == 0:
+        ap.error("--workers needs a fixed --port")
+    children = []
+    if a.workers > 1:
+        import signal
+        import subprocess
+        # SIGTERM ends serve_forever through the finally below, which stops the workers
+        signal.signal(signal.SIGTERM, lambda *_: sys.exit(0))
+        cmd = [sys.executable, "-m", "pyactivestorage_amd.reductionist_server", a.root,
+               "--host", a.host, "--port", str(a.port), "--reuse-port"] + (["-v"] if a.verbose else [])
+        # started before this process touches the GPU; children, not forks
+        children = [subprocess.Popen(cmd) for _ in range(a.workers - 1)]
+    srv = ReductionistServer(a.root, (a.host, a.port), a.verbose, reuse_port=a.reuse_port or a.workers > 1)
+    if not a.reuse_port:
+        print(f"serving {a.root} at {srv.url}/v2/<operation>/ ({a.workers} process(es))", flush=True)
+    try:
+        srv.serve_forever()
+    finally:
+        for ch in children:
+            ch.terminate()
+        for ch in children:
+            ch.wait()
 
 
 if __name__ == "__main__":
