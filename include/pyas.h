@@ -174,6 +174,11 @@ int pyas_memcpy_d2h(pyas_ctx *ctx, void *dst, const void *src, size_t n, void *s
 int pyas_stream_create(pyas_ctx *ctx, void **stream);
 int pyas_stream_destroy(pyas_ctx *ctx, void *stream);
 int pyas_stream_synchronize(pyas_ctx *ctx, void *stream);
+/* Work queued on `waiter` after this call starts only once everything queued
+ * on `waitee` so far has finished (an event recorded on waitee, waited on by
+ * waiter; no host synchronisation).  Lets ingest copies on one stream
+ * overlap device inflate on another (Active's compressed-chunk pipeline). */
+int pyas_stream_wait(pyas_ctx *ctx, void *waiter, void *waitee);
 
 /* ---- hot path ------------------------------------------------------------ */
 /* Fused un-shuffle -> byte-swap -> select -> mask -> sum/count/min/max for

@@ -104,6 +104,7 @@ SIGNATURES = {
     "pyas_stream_create": [_vp, ctypes.POINTER(_vp)],
     "pyas_stream_destroy": [_vp, _vp],
     "pyas_stream_synchronize": [_vp, _vp],
+    "pyas_stream_wait": [_vp, _vp, _vp],
     "pyas_reduce_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _u32, _vp],
     "pyas_reduce_axes": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _u32, _vp, _vp, _vp],
     "pyas_select_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _vp, _vp],

@@ -20,6 +20,7 @@ Mirrors ``activestorage/active.py``'s user API (``Active.method``,
 from __future__ import annotations
 
 import concurrent.futures
+import os
 
 import numpy as np
 
@@ -35,6 +36,19 @@ from .storage import _decompress, _shuffle_sizes
 from .variable import decode_filters, get_missing_attributes
 
 _ALIGN = 256
+# read -> inflate pipeline stages of a compressed query (PYAS_INFLATE_GROUPS)
+_INFLATE_GROUPS = int(os.environ.get("PYAS_INFLATE_GROUPS", "4"))
+
+
+def _pipeline_groups(sizes, n_groups):
+    """Up to ``n_groups`` contiguous index ranges of about equal total size."""
+    z = np.asarray(sizes, dtype=np.int64)
+    if z.size == 0:
+        return []
+    cum = np.cumsum(z)
+    cuts = np.searchsorted(cum, cum[-1] * np.arange(1, max(1, n_groups)) / max(1, n_groups), side="left") + 1
+    edges = np.unique(np.concatenate([[0], np.minimum(cuts, z.size), [z.size]]))
+    return [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:]) if b > a]
 
 
 class Active:
@@ -153,15 +167,32 @@ class Active:
             fsize = np.array([z for _, z in infos], dtype=np.int64)
             self.data_read += int(fsize.sum())
             if device_inflate:
+                # f2+f3 pipeline: the compressed bytes arrive in groups on a
+                # copy stream; each group is inflated on its own stream as soon
+                # as its copies land (inflate waves of every group can be
+                # resident together: one stream per wave, so concurrency is
+                # what buys inflate throughput), while the host reads on
                 padded = -(-fsize // 16) * 16
                 soffs = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
                 src = DeviceBuffer(ctx, max(int(padded.sum()), 16))
-                read_ranges(ctx, ds.filename, foff, fsize, src.ptr, soffs, st, self._max_threads)
                 buf = DeviceBuffer(ctx, max(n, 1) * stride)
-                ib = InflateBatch(ctx, soffs, fsize, np.arange(n, dtype=np.int64) * stride,
-                                  np.full(n, nbytes, dtype=np.int64))
-                ib.launch(src.ptr, buf.ptr, st)
-                ib.check(st)
+                copy_st = ctx.thread_aux_stream(0)
+                doffs = np.arange(n, dtype=np.int64) * stride
+                ctx.stream_wait(copy_st, st)      # order after prior work on st
+                batches = []
+                groups = _pipeline_groups(padded, _INFLATE_GROUPS)
+                for g, (lo, hi) in enumerate(groups):
+                    read_ranges(ctx, ds.filename, foff[lo:hi], fsize[lo:hi], src.ptr, soffs[lo:hi],
+                                copy_st, self._max_threads)
+                    inf_st = ctx.thread_aux_stream(1 + g)
+                    ctx.stream_wait(inf_st, copy_st)
+                    ib = InflateBatch(ctx, soffs[lo:hi], fsize[lo:hi], doffs[lo:hi],
+                                      np.full(hi - lo, nbytes, dtype=np.int64))
+                    ib.launch(src.ptr, buf.ptr, inf_st)
+                    batches.append((lo, ib, inf_st))
+                for lo, ib, inf_st in batches:
+                    ib.check(inf_st, base=lo)
+                    ctx.stream_wait(st, inf_st)
                 del src
             else:
                 bad = np.nonzero(fsize != nbytes)[0]

@@ -364,6 +364,19 @@ int pyas_stream_synchronize(pyas_ctx *ctx, void *stream) {
     return PYAS_OK;
 }
 
+int pyas_stream_wait(pyas_ctx *ctx, void *waiter, void *waitee) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (waiter == waitee) return PYAS_OK;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    hipEvent_t ev;
+    PYAS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, (hipStream_t)waitee);
+    if (e == hipSuccess) e = hipStreamWaitEvent((hipStream_t)waiter, ev, 0);
+    (void)hipEventDestroy(ev);   // released once the wait is satisfied
+    if (e != hipSuccess) return hip_fail(e, "pyas_stream_wait");
+    return PYAS_OK;
+}
+
 int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
                        pyas_partial *chunk_out, pyas_partial *total, uint32_t combine_flags,
                        void *stream) {

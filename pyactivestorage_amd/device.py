@@ -68,6 +68,24 @@ class Context:
             s = self._tls.stream = p.value
         return s
 
+    def thread_aux_stream(self, k: int = 0) -> int:
+        """Extra stream ``k`` of the calling thread (ingest copies and inflate
+        groups that overlap device work queued on :meth:`thread_stream`)."""
+        aux = getattr(self._tls, "aux_streams", None)
+        if aux is None:
+            aux = self._tls.aux_streams = {}
+        s = aux.get(k)
+        if s is None:
+            p = ctypes.c_void_p()
+            _lib.check(self.lib.pyas_stream_create(self.handle, ctypes.byref(p)),
+                       "pyas_stream_create")
+            s = aux[k] = p.value
+        return s
+
+    def stream_wait(self, waiter: int, waitee: int) -> None:
+        """Later work on ``waiter`` waits for everything queued on ``waitee``."""
+        _lib.check(self.lib.pyas_stream_wait(self.handle, waiter, waitee), "pyas_stream_wait")
+
     def synchronize(self, stream: int | None) -> None:
         _lib.check(self.lib.pyas_stream_synchronize(self.handle, stream), "pyas_stream_synchronize")
         self._tls.pending = []

@@ -33,7 +33,8 @@ _MESSAGES = {
 }
 
 
-def raise_for_status(status: np.ndarray, out_sizes: np.ndarray, capacity: np.ndarray) -> None:
+def raise_for_status(status: np.ndarray, out_sizes: np.ndarray, capacity: np.ndarray,
+                     base: int = 0) -> None:
     """Raise the ``zlib.error`` zlib.decompress would give for the first failed
     stream; an output larger than the caller's capacity is a ValueError (the
     reference fails reshaping the oversized chunk, storage.py:57-62)."""
@@ -43,7 +44,7 @@ def raise_for_status(status: np.ndarray, out_sizes: np.ndarray, capacity: np.nda
     c = int(bad[0])
     code = int(status[c])
     if code == 10:
-        raise ValueError(f"chunk {c} inflates to more than its {int(capacity[c])} bytes")
+        raise ValueError(f"chunk {base + c} inflates to more than its {int(capacity[c])} bytes")
     rc, msg = _MESSAGES.get(code, (-3, f"inflate status {code}"))
     if rc == 2:
         raise zlib.error(f"Error {rc} while decompressing data")
@@ -89,14 +90,15 @@ class InflateBatch:
         self.ctx.synchronize(stream)
         return self.out_sizes, self.status
 
-    def check(self, stream, exact: bool = True) -> np.ndarray:
+    def check(self, stream, exact: bool = True, base: int = 0) -> np.ndarray:
         """Synchronise, raise like zlib on failure, and (``exact``) require every
         stream to fill its slot exactly (a chunk's decoded size is fixed)."""
         sizes, status = self.results(stream)
-        raise_for_status(status, sizes, self.capacity)
+        raise_for_status(status, sizes, self.capacity, base)
         if exact and self.n and (sizes != self.capacity).any():
             c = int(np.nonzero(sizes != self.capacity)[0][0])
-            raise ValueError(f"chunk {c} inflated to {int(sizes[c])} bytes, expected {int(self.capacity[c])}")
+            raise ValueError(f"chunk {base + c} inflated to {int(sizes[c])} bytes, "
+                             f"expected {int(self.capacity[c])}")
         return sizes
 
 

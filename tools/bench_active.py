@@ -22,6 +22,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--shape", type=int, default=1024)
+    ap.add_argument("--zlib", action="store_true",
+                    help="chunks HDF5-shuffled + deflated (level 4, as test1.nc): 32 distinct "
+                         "compressed chunks repeated over the variable (rows f2+f3 end to end)")
+    ap.add_argument("--axes", default="all", help="'all' or 'none' (full reduction only)")
     a = ap.parse_args()
     import torch
     from pyactivestorage_amd.active import Active
@@ -30,26 +34,41 @@ def main():
     n, c = a.shape, 64
     shape, chunks = (n, n, n), (c, c, c)
     dev = torch.device("cuda", 0)
-    data, offsets, _ = chunk_major_device(torch, shape, chunks, np.float32, dev, fill=-999.0, fill_frac=0.01)
     path = os.path.join(tempfile.gettempdir(), f"pyas_active_{os.getpid()}.chunks")
+    grid = [s // k for s, k in zip(shape, chunks)]
+    cb = c * c * c * 4
     res = {}
+    filters = None
     try:
-        with open(path, "wb") as f:
-            step = 256 << 20
-            for o in range(0, data.numel(), step):
-                f.write(data[o:o + step].cpu().numpy().tobytes())
-        del data
-        torch.cuda.empty_cache()
-        grid = [s // k for s, k in zip(shape, chunks)]
-        cb = c * c * c * 4
-        index = {cc: (int(offsets[i]), cb) for i, cc in enumerate(np.ndindex(*grid))}
+        if a.zlib:
+            from tools.bench_inflate import make_streams
+            streams = [z for _, z in make_streams(32, 4)]
+            index, pos = {}, 0
+            with open(path, "wb") as f:
+                for i, cc in enumerate(np.ndindex(*grid)):
+                    z = streams[i % len(streams)]
+                    f.write(z)
+                    index[cc] = (pos, len(z))
+                    pos += len(z)
+            filters = [{"filter_id": 2, "client_data": [4]}, {"filter_id": 1, "client_data": [4]}]
+        else:
+            data, offsets, _ = chunk_major_device(torch, shape, chunks, np.float32, dev, fill=-999.0,
+                                                  fill_frac=0.01)
+            with open(path, "wb") as f:
+                step = 256 << 20
+                for o in range(0, data.numel(), step):
+                    f.write(data[o:o + step].cpu().numpy().tobytes())
+            del data
+            torch.cuda.empty_cache()
+            index = {cc: (int(offsets[i]), cb) for i, cc in enumerate(np.ndindex(*grid))}
         attrs = {"_FillValue": np.array([-999.0], dtype=np.float32),
                  "valid_min": np.array([1000.0], dtype=np.float32),
                  "valid_max": np.array([5e8], dtype=np.float32)}
         var = ChunkedVariable(name="c3", shape=shape, chunks=chunks, dtype=np.float32,
-                              chunk_index=index, attrs=attrs, filename=path)
+                              chunk_index=index, attrs=attrs, filename=path, filter_pipeline=filters)
         nbytes = n ** 3 * 4
-        for axis in (None, (0,), (1,), (2,), (0, 1), (1, 2), (0, 2)):
+        axes_list = (None,) if a.axes == "none" else (None, (0,), (1,), (2,), (0, 1), (1, 2), (0, 2))
+        for axis in axes_list:
             act = Active(var)
             act.mean(axis=axis)
             act[...]                       # warm-up (pinned ring, kernels)
@@ -66,7 +85,9 @@ def main():
     finally:
         if os.path.exists(path):
             os.unlink(path)
-    print(json.dumps({"workload": f"Active.mean over c3 {shape} file (page cache) -> result", "results": res}))
+    kind = "shuffle+zlib level-4 chunks" if a.zlib else "uncompressed chunks"
+    print(json.dumps({"workload": f"Active.mean over c3 {shape} file of {kind} (page cache) -> result",
+                      "results": res}))
 
 
 if __name__ == "__main__":
