@@ -59,8 +59,10 @@ class ReductionPlan:
                 raise ValueError("one selection per chunk is required")
             table, pool = selection.pack(selections, len(self.chunk_shape))
             _check_table(table, self.chunk_shape, pool)
-            if not _all_full(table, self.chunk_shape):
-                # (every chunk fully selected: no table, the kernels' dense paths)
+            vector_mask = self.cm.tables[0] is not None or self.cm.tables[1] is not None
+            if vector_mask or not _all_full(table, self.chunk_shape):
+                # (every chunk fully selected and scalar masks: no table, the
+                # kernels' lean/dense paths)
                 sel_ptr = self._upload(table, st).ptr
                 pool_ptr = self._upload(pool, st).ptr
             shapes = {s.shape for s in selections}

@@ -150,6 +150,8 @@ __device__ __forceinline__ T load_elem_rt(const uint8_t *base, int64_t n, int64_
 // ---------------------------------------------------------------------------
 // mask (compiled mask_missing, storage.py:126-153)
 // ---------------------------------------------------------------------------
+constexpr int kMaskAll = 1, kMaskNoEq1 = 2;
+
 template <typename T> struct MaskT {
     T lo0, hi0, lo1, hi1, gt, lt;
     __device__ void init(const pyas_mask &m) {
@@ -167,6 +169,14 @@ template <typename T> struct MaskT {
         const bool e0 = (x >= lo0) & (x <= hi0);
         const bool e1 = (x >= lo1) & (x <= hi1);
         return e0 | e1 | (x > gt) | (x < lt);
+    }
+    // Kernel-level mask mode M (the MASKED template argument): 0 none,
+    // kMaskAll every rule, kMaskNoEq1 without the second equality rule
+    // (the common _FillValue + valid_min/valid_max case: 4 fewer ops).
+    template <int M>
+    __device__ __forceinline__ bool masked_m(T x) const {
+        if constexpr (M == kMaskNoEq1) return ((x >= lo0) & (x <= hi0)) | (x > gt) | (x < lt);
+        else return masked(x);
     }
 };
 
@@ -223,10 +233,10 @@ template <typename T, typename C> struct AccT {
         mn = v ? pmin(mn, x) : mn;
         mx = v ? pmax(mx, x) : mx;
     }
-    template <bool MASKED>
+    template <int MASKED>
     __device__ __forceinline__ void add(T x, const MaskT<T> &mk) {
         if constexpr (!MASKED) add_valid(x);
-        else add_flag(x, mk.masked(x));
+        else add_flag(x, mk.template masked_m<MASKED>(x));
     }
 };
 template <typename T> using Acc = AccT<T, uint32_t>;
@@ -275,7 +285,7 @@ template <typename T> struct TileAcc {
         nan = false;
     }
     // N values; CONV: all 64 lanes execute this call (uniform trip count).
-    template <int N, bool MASKED, bool CONV>
+    template <int N, int MASKED, bool CONV>
     __device__ __forceinline__ void add_n(const T *x, const MaskT<T> &mk) {
         using G = typename GroupSum<T>::type;
         G g = 0;
@@ -284,7 +294,7 @@ template <typename T> struct TileAcc {
             const T v = x[k];
             if constexpr (TT<T>::kind == 0) nan |= (v != v);
             if constexpr (MASKED) {
-                const bool ok = !mk.masked(v);
+                const bool ok = !mk.template masked_m<MASKED>(v);
                 if constexpr (TT<T>::kind == 0) {
                     const T y = ok ? v : (T)__builtin_nan("");  // v_min/v_max skip NaN
                     mn = tmin(mn, y);

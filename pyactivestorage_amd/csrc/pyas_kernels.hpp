@@ -103,7 +103,7 @@ __device__ __forceinline__ void unpack16(const uint4 &r, T *x) {
     for (int k = 0; k < N; ++k) x[k] = bits_to<T>(BSWAP ? bswap(w[k]) : w[k]);
 }
 
-template <typename T, bool BSWAP, bool MASKED, bool CONV>
+template <typename T, bool BSWAP, int MASKED, bool CONV>
 __device__ __forceinline__ void consume16(const uint4 &r, TileAcc<T> &acc, const MaskT<T> &mk) {
     constexpr int N = 16 / sizeof(T);
     T x[N];
@@ -117,7 +117,7 @@ __device__ __forceinline__ void consume16(const uint4 &r, TileAcc<T> &acc, const
 // Plain layout, memory elements [m0, m1) of the chunk at `base`.  The body is
 // 16-B global loads, U per lane per step, register double-buffered so the
 // next step's loads are in flight while the current step is reduced.
-template <typename T, bool BSWAP, bool MASKED>
+template <typename T, bool BSWAP, int MASKED>
 __device__ void run_plain(const uint8_t *base, int64_t m0, int64_t m1, TileAcc<T> &acc,
                           const MaskT<T> &mk) {
     constexpr int ES = sizeof(T);
@@ -169,7 +169,7 @@ __device__ void run_plain(const uint8_t *base, int64_t m0, int64_t m1, TileAcc<T
 }
 
 // Shuffled layout, chunk elements [i0, i1); n = elements in the chunk.
-template <typename T, bool BSWAP, bool MASKED>
+template <typename T, bool BSWAP, int MASKED>
 __device__ void run_shuffled(const uint8_t *base, int64_t n, int64_t i0, int64_t i1,
                              TileAcc<T> &acc, const MaskT<T> &mk) {
     constexpr int ES = sizeof(T);
@@ -280,7 +280,7 @@ struct RadixCounter {
     }
 };
 
-template <typename T, bool SHUF, bool BSWAP, bool MASKED>
+template <typename T, bool SHUF, bool BSWAP, int MASKED>
 __device__ void run_generic(const ReduceArgs &a, const uint8_t *base, const Sel &s, int64_t e0,
                             int64_t e1, TileAcc<T> &acc, const MaskT<T> &mk) {
     const uint32_t all = (1u << a.ndim) - 1u;
@@ -299,7 +299,7 @@ __device__ void run_generic(const ReduceArgs &a, const uint8_t *base, const Sel 
 // elements (dims > k full, dim k unit step): stream each run as 16-B vectors.
 // Work items are (outer index of dims < k, vector within the run), walked by
 // a radix counter, U independent 16-B loads in flight per lane.
-template <typename T, bool BSWAP, bool MASKED>
+template <typename T, bool BSWAP, int MASKED>
 __device__ void run_rows(const ReduceArgs &a, const uint8_t *base, const Sel &s, int k, int64_t L,
                          int64_t e0, int64_t e1, TileAcc<T> &acc, const MaskT<T> &mk) {
     constexpr int N = 16 / sizeof(T);
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinishArgs f) {
 // ---------------------------------------------------------------------------
 // SEL = false: every chunk fully selected (batch.sel == NULL) -> a lean
 // streaming-only kernel (no selection state, high occupancy).
-template <typename T, bool SHUF, bool BSWAP, bool MASKED, bool SEL>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL>
 __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
     const int64_t b = blockIdx.x;
     const int64_t c = b / a.tpc;
@@ -568,7 +568,7 @@ __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
 #else
 #define PYAS_WAVES_ATTR
 #endif
-template <typename T, bool SHUF, bool BSWAP, bool MASKED>
+template <typename T, bool SHUF, bool BSWAP, int MASKED>
 __global__ __launch_bounds__(kBlock) PYAS_WAVES_ATTR void k_reduce(ReduceArgs a) {
     reduce_body<T, SHUF, BSWAP, MASKED, false>(a);
 }
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(kBlock) PYAS_WAVES_ATTR void k_reduce(ReduceArgs a)
 // Uncapped: per-chunk selections (hyperslabs, strides, lists), where the cap
 // spills (C5 measured 46 % slower), and 1-/2-byte dtypes (16 or 8 values per
 // 16-B load also spill under the cap).  Keeps the compiler's allocation.
-template <typename T, bool SHUF, bool BSWAP, bool MASKED, bool SEL>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL>
 __global__ __launch_bounds__(kBlock) void k_reduce_u(ReduceArgs a) {
     reduce_body<T, SHUF, BSWAP, MASKED, SEL>(a);
 }
@@ -994,7 +994,7 @@ __device__ __forceinline__ void store_group(const TileAcc<T> &a, uint32_t cnt, u
 #define PYAS_DENSE_ATTR
 #endif
 
-template <typename T, bool BSWAP, bool MASKED, bool AL>
+template <typename T, bool BSWAP, int MASKED, bool AL>
 __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                           const MaskT<T> &mk, uint4 *stage) {
     constexpr int ES = sizeof(T), N = 16 / ES;
@@ -1080,7 +1080,7 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     }
 }
 
-template <typename T, bool BSWAP, bool MASKED, bool AL, int UO>
+template <typename T, bool BSWAP, int MASKED, bool AL, int UO>
 __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                           const MaskT<T> &mk) {
     constexpr int ES = sizeof(T), N = 16 / ES;
@@ -1162,7 +1162,7 @@ __device__ __forceinline__ bool dense_owns(const AxesArgs &a, const Sel &s) {
     return a.d.mode != 0 && chunk_is_full(s, a.r.shape, a.r.ndim);
 }
 
-template <typename T, bool BSWAP, bool MASKED, int MODE>
+template <typename T, bool BSWAP, int MASKED, int MODE>
 __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs a) {
     const int64_t c = blockIdx.x / a.d.bpc;
     const int64_t j = blockIdx.x - c * a.d.bpc;
@@ -1254,16 +1254,29 @@ static void launch_reduce_ts(const ReduceArgs &a, bool shuf, bool bsw, bool mask
             hipLaunchKernelGGL((k_reduce_u<T, S, B, M, SEL>), g, blk, 0, st, a);       \
         else hipLaunchKernelGGL((k_reduce<T, S, B, M>), g, blk, 0, st, a);             \
     } while (0)
+    // the lean kernel also has a variant without the second equality rule
+    const bool no_eq1 = !SEL && sizeof(T) >= 4 && !(a.mask.flags & PYAS_MASK_EQ1);
     if constexpr (sizeof(T) == 1) {
-        if (masked) PYAS_L(false, false, true);
-        else PYAS_L(false, false, false);
+        if (masked) PYAS_L(false, false, kMaskAll);
+        else PYAS_L(false, false, 0);
+    } else if constexpr (!SEL && sizeof(T) >= 4) {
+#define PYAS_LM(S, B)                                                 \
+        do {                                                          \
+            if (!masked) PYAS_L(S, B, 0);                             \
+            else if (no_eq1) PYAS_L(S, B, kMaskNoEq1);                \
+            else PYAS_L(S, B, kMaskAll);                              \
+        } while (0)
+        if (shuf) { if (bsw) PYAS_LM(true, true); else PYAS_LM(true, false); }
+        else { if (bsw) PYAS_LM(false, true); else PYAS_LM(false, false); }
+#undef PYAS_LM
     } else {
+        (void)no_eq1;
         if (shuf) {
-            if (bsw) { if (masked) PYAS_L(true, true, true); else PYAS_L(true, true, false); }
-            else { if (masked) PYAS_L(true, false, true); else PYAS_L(true, false, false); }
+            if (bsw) { if (masked) PYAS_L(true, true, kMaskAll); else PYAS_L(true, true, 0); }
+            else { if (masked) PYAS_L(true, false, kMaskAll); else PYAS_L(true, false, 0); }
         } else {
-            if (bsw) { if (masked) PYAS_L(false, true, true); else PYAS_L(false, true, false); }
-            else { if (masked) PYAS_L(false, false, true); else PYAS_L(false, false, false); }
+            if (bsw) { if (masked) PYAS_L(false, true, kMaskAll); else PYAS_L(false, true, 0); }
+            else { if (masked) PYAS_L(false, false, kMaskAll); else PYAS_L(false, false, 0); }
         }
     }
 #undef PYAS_L
@@ -1273,7 +1286,9 @@ template <typename T>
 hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool masked, int64_t grid,
                            hipStream_t st) {
     const dim3 g((unsigned)grid);
-    if (a.sel) launch_reduce_ts<T, true>(a, shuf, bsw, masked, g, st);
+    // vector fill/missing tables are applied by the selection-aware path only
+    // (a NULL table there means every chunk whole)
+    if (a.sel || a.tab.on[0] || a.tab.on[1]) launch_reduce_ts<T, true>(a, shuf, bsw, masked, g, st);
     else launch_reduce_ts<T, false>(a, shuf, bsw, masked, g, st);
     return hipGetLastError();
 }

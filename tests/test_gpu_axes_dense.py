@@ -158,3 +158,47 @@ def test_dense_batch_mixed_and_misaligned(gpu, dt, axes):
             np.testing.assert_allclose(part_k["sum"][ok], wsum[ok], rtol=1e-6, atol=1e-3, err_msg=what)
         else:
             np.testing.assert_array_equal(part_k["sum"][ok], wsum[ok], err_msg=what)
+
+
+@pytest.mark.parametrize("with_sels", [True, False])
+def test_vector_fill_on_whole_chunks(gpu, with_sels):
+    """Broadcast (vector) missing values on fully selected chunks: the
+    selection table may not be dropped (the lean kernel applies scalar rules
+    only) and a NULL table must still route to the table-aware kernel.
+    Reference: storage.py:133-143 (broadcast ==)."""
+    from pyactivestorage_amd.batch import ReductionPlan
+    from pyactivestorage_amd.device import DeviceBuffer, get_context
+    from pyactivestorage_amd import selection
+    dt = np.dtype("<f4")
+    shape = (4, 6, 8)
+    ctx = get_context(0)
+    st = ctx.thread_stream()
+    rng = np.random.default_rng(5)
+    chunks = [_data(dt, shape, rng) for _ in range(5)]
+    vec = np.arange(8, dtype=np.float32) + 40.0           # broadcast along the last dim
+    for a in chunks:
+        a[..., 2] = 42.0                                  # matches vec[2]
+    miss = (None, vec, None, None)
+    blob = np.concatenate([np.frombuffer(a.tobytes(), np.uint8) for a in chunks])
+    dbuf = DeviceBuffer(ctx, blob.nbytes)
+    ctx.h2d(dbuf.ptr, blob, st)
+    offsets = np.arange(5, dtype=np.int64) * chunks[0].nbytes
+    full = tuple(slice(0, n, 1) for n in shape)
+    sels = [selection.normalize(full, shape) for _ in chunks] if with_sels else None
+    plan = ReductionPlan(ctx, dt, shape, dbuf.ptr, offsets, selections=sels, missing=miss,
+                         round_to_var=False, stream=st)
+    plan.launch(st)
+    tot = plan.read_total(st)[0]
+    want_n, want_sum, mins, maxs = 0, 0.0, [], []
+    for a in chunks:
+        m, n = ref.reduce_chunk_bytes(a.tobytes(), None, None, miss, dt, shape, "C", full,
+                                      (0, 1, 2), np.ma.sum)
+        want_n += int(np.asarray(n).reshape(-1)[0])
+        want_sum += float(np.ma.filled(m, 0).reshape(-1)[0])
+        mins.append(float(np.ma.min(ref.reduce_chunk_bytes(a.tobytes(), None, None, miss, dt, shape, "C",
+                                                            full, (0, 1, 2), None)[0])))
+        maxs.append(float(np.ma.max(ref.reduce_chunk_bytes(a.tobytes(), None, None, miss, dt, shape, "C",
+                                                            full, (0, 1, 2), None)[0])))
+    assert int(tot["count"]) == want_n and want_n < 5 * chunks[0].size
+    assert float(tot["min"]) == min(mins) and float(tot["max"]) == max(maxs)
+    np.testing.assert_allclose(float(tot["sum"]), want_sum, rtol=1e-6)
