@@ -60,7 +60,7 @@ class Active:
         return inst
 
     def __init__(self, variable, axis=None, max_threads: int = 30, device: int = 0,
-                 device_inflate: bool = True):
+                 device_inflate: bool = True, group=None):
         if variable is None:
             raise ValueError("Must use a valid variable object. Got None")
         self.ds = variable
@@ -72,6 +72,11 @@ class Active:
         self._max_threads = int(max_threads)
         self.device = device
         self.device_inflate = bool(device_inflate)   # f3: zlib chunks inflate on the GPU
+        # row (e): a torch.distributed process group (one process per GPU).
+        # Each rank reads and reduces a contiguous range of the query's chunks
+        # from its own GPU; one all-gather of the per-rank partial grids and a
+        # fixed rank-order device combine give every rank the same result.
+        self.group = group
         self.missing = None
         self.data_read = 0
 
@@ -308,6 +313,9 @@ class Active:
     def _reduce(self, indexer, compressor, filters, axes):
         box = self._box_plan(indexer)
         if box is None:
+            if self.group is not None:
+                raise NotImplementedError("a distributed Active query needs slices/index lists on every "
+                                          "dimension and scalar missing-data attributes")
             return self._reduce_general(indexer, compressor, filters, axes)
         ds = self.ds
         dt = ds.dtype
@@ -315,25 +323,77 @@ class Active:
         final_shape = tuple(1 if i in axes else n for i, n in enumerate(indexer.shape))
         n_final = int(np.prod(final_shape))
         pdt = engine.partial_dtype(dt)
-        if len(coords) == 0:
-            final = np.zeros(n_final, dtype=pdt)
-            return self._format(final.reshape(final_shape), final_shape)
-        ctx, st, buf, offsets, fused = self._ingest([tuple(c) for c in coords.tolist()],
-                                                    compressor, filters)
-        full = _all_full(table, ds.chunks)   # whole chunks: no table, dense kernels
-        plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused,
-                             sel_table=None if full else table, index_pool=None if full else pool,
-                             missing=self.missing, round_to_var=True, stream=st)
-        if len(axes) == ds.ndim:
-            plan.launch(st, chunk_partials=False)
-            final = plan.read_total(st)
-            return self._format(final.reshape(final_shape), final_shape)
-        return self._grid_combine(ctx, st, plan, self._grid_from_dims(dims, axes, final_shape),
-                                  axes, final_shape)
+        n = len(coords)
+        lo, hi = 0, n
+        if self.group is not None:   # this rank's contiguous chunk range
+            import torch.distributed as dist
+            from .distributed import shard_ranges
+            weights = np.prod(table[:, :ds.ndim, 2].astype(np.int64), axis=1)
+            lo, hi = shard_ranges(weights, dist.get_world_size(self.group))[dist.get_rank(self.group)]
+        if hi > lo:
+            ctx, st, buf, offsets, fused = self._ingest([tuple(c) for c in coords[lo:hi].tolist()],
+                                                        compressor, filters)
+            sub = table[lo:hi]
+            full = _all_full(sub, ds.chunks)   # whole chunks: no table, lean/dense kernels
+            plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused,
+                                 sel_table=None if full else sub, index_pool=None if full else pool,
+                                 missing=self.missing, round_to_var=True, stream=st)
+            if len(axes) == ds.ndim:
+                plan.launch(st, chunk_partials=False)
+                final = plan.read_total(st)
+            else:
+                final = self._grid_partials(ctx, st, plan, self._grid_from_dims(dims, axes, final_shape),
+                                            axes, final_shape, lo, hi)
+        else:
+            final = np.zeros(n_final, dtype=pdt)   # count 0: neutral in every combine
+        if self.group is not None:
+            final = self._exchange(final)
+        return self._format(final.reshape(final_shape), final_shape)
+
+    def _exchange(self, final):
+        """All-gather the per-rank partial grids (RCCL for an nccl group,
+        else over the group's CPU backend) and fold them in rank order on
+        the device (pyas_combine_segments).  Every rank gets the result."""
+        import torch
+        import torch.distributed as dist
+        world = dist.get_world_size(self.group)
+        if world == 1:
+            return final
+        dev = torch.device("cuda", torch.cuda.current_device()) \
+            if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        t = torch.from_numpy(np.ascontiguousarray(final).view(np.uint8).copy()).to(dev)
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=self.group)
+        gathered = np.concatenate([p.cpu().numpy() for p in parts])
+        n = final.size
+        ctx = get_context(self.device)
+        st = ctx.thread_stream()
+        index = (np.arange(world, dtype=np.int64)[None, :] * n
+                 + np.arange(n, dtype=np.int64)[:, None]).reshape(-1)
+        seg = np.arange(n + 1, dtype=np.int64) * world
+        gbuf = DeviceBuffer(ctx, gathered.nbytes)
+        ctx.h2d(gbuf.ptr, gathered, st)
+        meta = np.concatenate([index, seg])
+        mbuf = DeviceBuffer(ctx, meta.nbytes)
+        ctx.h2d(mbuf.ptr, meta, st)
+        fin = DeviceBuffer(ctx, max(n, 1) * _lib.PARTIAL_NBYTES)
+        engine.combine_segments(ctx, self.ds.dtype, gbuf.ptr, mbuf.ptr, mbuf.ptr + 8 * index.size, n,
+                                fin.ptr, False, st)
+        out = np.zeros(n, dtype=final.dtype)
+        ctx.d2h(out, fin.ptr, st)
+        ctx.synchronize(st)
+        return out
 
     def _grid_combine(self, ctx, st, plan, grid, axes, final_shape):
-        """Partial axes over a box query: per-chunk partial arrays
-        (pyas_reduce_axes), then pyas_combine_grid into the final grid."""
+        """Partial axes over a box query, every chunk local."""
+        final = self._grid_partials(ctx, st, plan, grid, axes, final_shape, 0, plan.n_chunks)
+        return self._format(final.reshape(final_shape), final_shape)
+
+    def _grid_partials(self, ctx, st, plan, grid, axes, final_shape, lo, hi):
+        """Per-chunk partial arrays of chunks [lo, hi) of the box query
+        (pyas_reduce_axes over ``plan``), then pyas_combine_grid into the
+        final grid; chunks outside [lo, hi) read a zeroed (count 0, neutral)
+        partial region."""
         ds = self.ds
         dt = ds.dtype
         n_final = int(np.prod(final_shape))
@@ -341,8 +401,20 @@ class Active:
         for a in axes:
             axes_mask |= 1 << a
         out_off, tables = grid
-        obuf = DeviceBuffer(ctx, out_off.nbytes)
-        ctx.h2d(obuf.ptr, out_off, st)
+        n_all = out_off.size
+        n_parts_all = int(tables["n_parts"])
+        end = np.append(out_off, n_parts_all)
+        base, top = int(end[lo]), int(end[hi])
+        neutral = 0
+        if lo > 0 or hi < n_all:
+            neutral = int(np.diff(end).max())
+        mine = out_off[lo:hi] - base
+        all_off = np.full(n_all, top - base, dtype=np.int64)   # the neutral region
+        all_off[lo:hi] = mine
+        obuf = DeviceBuffer(ctx, mine.nbytes)
+        ctx.h2d(obuf.ptr, mine, st)
+        abuf = DeviceBuffer(ctx, all_off.nbytes)
+        ctx.h2d(abuf.ptr, all_off, st)
         tbuf = DeviceBuffer(ctx, max(tables["blob"].nbytes, 16))
         ctx.h2d(tbuf.ptr, tables["blob"], st)
         g = _lib.Grid()
@@ -355,16 +427,19 @@ class Active:
                 g.pos_coord[d] = tbuf.ptr + 4 * tables["pos_coord"][d]
                 g.pos_local[d] = tbuf.ptr + 4 * tables["pos_local"][d]
                 g.coord_count[d] = tbuf.ptr + 4 * tables["coord_count"][d]
-        g.chunk_out_offsets = obuf.ptr
-        n_parts = int(tables["n_parts"])
-        parts = DeviceBuffer(ctx, max(n_parts, 1) * _lib.PARTIAL_NBYTES)
+        g.chunk_out_offsets = abuf.ptr
+        n_parts = top - base
+        parts = DeviceBuffer(ctx, max(n_parts + neutral, 1) * _lib.PARTIAL_NBYTES)
+        if neutral:
+            zeros = np.zeros(neutral * _lib.PARTIAL_NBYTES, dtype=np.uint8)
+            ctx.h2d(parts.ptr + n_parts * _lib.PARTIAL_NBYTES, zeros, st)
         fin = DeviceBuffer(ctx, max(n_final, 1) * _lib.PARTIAL_NBYTES)
         engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st)
         engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st)
         final = np.zeros(n_final, dtype=engine.partial_dtype(dt))
         ctx.d2h(final, fin.ptr, st)
         ctx.synchronize(st)
-        return self._format(final.reshape(final_shape), final_shape)
+        return final
 
     def _reduce_general(self, indexer, compressor, filters, axes):
         """Per-chunk selection objects and host-built segments: integer-
