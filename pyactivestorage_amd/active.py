@@ -36,6 +36,16 @@ from .storage import _decompress, _shuffle_sizes
 from .variable import decode_filters, get_missing_attributes
 
 _ALIGN = 256
+def release_resident(variable) -> None:
+    """Free the HBM copy that resident-mode ``Active`` queries keep for
+    ``variable`` (e.g. after the file changed)."""
+    store = getattr(variable, "_pyas_resident", None)
+    if store is not None:
+        get_context(store["device"]).synchronize(get_context(store["device"]).thread_stream())
+        store["buf"].free()
+        variable._pyas_resident = None
+
+
 # read -> inflate pipeline stages of a compressed query (PYAS_INFLATE_GROUPS)
 _INFLATE_GROUPS = int(os.environ.get("PYAS_INFLATE_GROUPS", "4"))
 
@@ -60,7 +70,7 @@ class Active:
         return inst
 
     def __init__(self, variable, axis=None, max_threads: int = 30, device: int = 0,
-                 device_inflate: bool = True, group=None):
+                 device_inflate: bool = True, group=None, resident: bool = False):
         if variable is None:
             raise ValueError("Must use a valid variable object. Got None")
         self.ds = variable
@@ -77,6 +87,9 @@ class Active:
         # from its own GPU; one all-gather of the per-rank partial grids and a
         # fixed rank-order device combine give every rank the same result.
         self.group = group
+        # keep the variable's decoded chunks in HBM across queries (288 GB per
+        # MI355X): later queries read only chunks not loaded yet
+        self.resident = bool(resident)
         self.missing = None
         self.data_read = 0
 
@@ -154,7 +167,46 @@ class Active:
 
     # -- host ingest -------------------------------------------------------
     def _ingest(self, coords, compressor, filters):
-        """Read + inflate every touched chunk and upload them as one buffer."""
+        """Device buffer + per-chunk offsets of every touched chunk (decoded,
+        still byte-shuffled when the shuffle is fused into the kernels)."""
+        if self.resident:
+            got = self._ingest_resident(coords, compressor, filters)
+            if got is not None:
+                return got
+        return self._ingest_fresh(coords, compressor, filters)
+
+    def _ingest_resident(self, coords, compressor, filters):
+        """Resident mode: the variable's decoded chunks stay in HBM (one slot
+        per chunk of the variable's grid, allocated on first use), so a query
+        reads from the file only the chunks no earlier query loaded.  None
+        when the filter pipeline needs a standalone device pass."""
+        ds = self.ds
+        shuffles = _shuffle_sizes(filters)
+        if shuffles and shuffles[-1] == ds.dtype.itemsize:
+            shuffles.pop()
+        if any(es > 1 for es in shuffles):
+            return None
+        nbytes = int(np.prod(ds.chunks)) * ds.dtype.itemsize
+        stride = -(-nbytes // _ALIGN) * _ALIGN
+        grid = tuple(-(-s // c) for s, c in zip(ds.shape, ds.chunks))
+        ctx = get_context(self.device)
+        store = getattr(ds, "_pyas_resident", None)
+        if store is None or store["device"] != self.device:
+            n_all = int(np.prod(grid))
+            store = {"device": self.device, "buf": DeviceBuffer(ctx, max(n_all, 1) * stride),
+                     "loaded": np.zeros(n_all, dtype=bool)}
+            ds._pyas_resident = store
+        c = np.asarray(coords, dtype=np.int64).reshape(len(coords), len(grid))
+        slots = np.ravel_multi_index(c.T, grid) if len(coords) else np.zeros(0, dtype=np.int64)
+        todo = np.nonzero(~store["loaded"][slots])[0]
+        _, st, _, _, fused = self._ingest_fresh([coords[i] for i in todo.tolist()], compressor, filters,
+                                                dst=store["buf"], dst_offsets=slots[todo] * stride)
+        store["loaded"][slots[todo]] = True
+        return ctx, st, store["buf"], slots.astype(np.int64) * stride, fused
+
+    def _ingest_fresh(self, coords, compressor, filters, dst=None, dst_offsets=None):
+        """Read + inflate every touched chunk into one device buffer (``dst``
+        at ``dst_offsets`` when given)."""
         ds = self.ds
         nbytes = int(np.prod(ds.chunks)) * ds.dtype.itemsize
 
@@ -164,6 +216,11 @@ class Active:
         stride = -(-nbytes // _ALIGN) * _ALIGN
         infos = [ds.chunk_info(c) for c in coords]
         n = len(infos)
+        doffs = (np.arange(n, dtype=np.int64) * stride if dst_offsets is None
+                 else np.ascontiguousarray(dst_offsets, dtype=np.int64))
+        if n == 0:
+            buf = dst if dst is not None else DeviceBuffer(ctx, stride)
+            return ctx, st, buf, doffs, self._fused_shuffle(filters)
         native_io = ds.reader is None and ds.filename is not None and (
             device_inflate or compressor is None)
         if native_io:
@@ -180,9 +237,8 @@ class Active:
                 padded = -(-fsize // 16) * 16
                 soffs = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
                 src = DeviceBuffer(ctx, max(int(padded.sum()), 16))
-                buf = DeviceBuffer(ctx, max(n, 1) * stride)
+                buf = dst if dst is not None else DeviceBuffer(ctx, max(n, 1) * stride)
                 copy_st = ctx.thread_aux_stream(0)
-                doffs = np.arange(n, dtype=np.int64) * stride
                 ctx.stream_wait(copy_st, st)      # order after prior work on st
                 batches = []
                 groups = _pipeline_groups(padded, _INFLATE_GROUPS)
@@ -204,9 +260,8 @@ class Active:
                 if bad.size:   # storage.py:57-62 reshape of a wrongly sized chunk
                     raise ValueError(f"cannot reshape array of size {int(fsize[bad[0]]) // ds.dtype.itemsize} "
                                      f"into shape {ds.chunks}")
-                buf = DeviceBuffer(ctx, max(n, 1) * stride)
-                read_ranges(ctx, ds.filename, foff, fsize, buf.ptr,
-                            np.arange(n, dtype=np.int64) * stride, st, self._max_threads)
+                buf = dst if dst is not None else DeviceBuffer(ctx, max(n, 1) * stride)
+                read_ranges(ctx, ds.filename, foff, fsize, buf.ptr, doffs, st, self._max_threads)
         else:
             def fetch(info):
                 off, size = info
@@ -222,9 +277,8 @@ class Active:
                 self.data_read += int(ssizes.sum())
                 src = DeviceBuffer(ctx, host.nbytes)
                 ctx.h2d(src.ptr, host, st)
-                buf = DeviceBuffer(ctx, max(n, 1) * stride)
-                ib = InflateBatch(ctx, soffs, ssizes, np.arange(n, dtype=np.int64) * stride,
-                                  np.full(n, nbytes, dtype=np.int64))
+                buf = dst if dst is not None else DeviceBuffer(ctx, max(n, 1) * stride)
+                ib = InflateBatch(ctx, soffs, ssizes, doffs, np.full(n, nbytes, dtype=np.int64))
                 ib.launch(src.ptr, buf.ptr, st)
                 ib.check(st)
                 del src
@@ -237,21 +291,31 @@ class Active:
                                          f"into shape {ds.chunks}")
                     host[i * stride: i * stride + nbytes] = a
                     self.data_read += size
-                buf = DeviceBuffer(ctx, host.nbytes)
-                ctx.h2d(buf.ptr, host, st)
+                if dst is None:
+                    buf = DeviceBuffer(ctx, host.nbytes)
+                    ctx.h2d(buf.ptr, host, st)
+                else:
+                    buf = dst
+                    for i in range(n):
+                        ctx.h2d(buf.ptr + int(doffs[i]), host[i * stride: (i + 1) * stride], st)
         shuffles = _shuffle_sizes(filters)
-        fused = 0
+        fused = self._fused_shuffle(filters)
         if shuffles and shuffles[-1] == ds.dtype.itemsize:
             shuffles.pop()
-            fused = ds.dtype.itemsize if ds.dtype.itemsize > 1 else 0
         for es in shuffles:   # non-itemsize shuffles: standalone device pass per chunk
             if es > 1:
+                assert dst is None   # resident mode keeps such pipelines out
                 tmp = DeviceBuffer(ctx, buf.nbytes)
                 for i in range(n):
                     engine.unshuffle(ctx, buf.ptr + i * stride, tmp.ptr + i * stride, nbytes, es, st)
                 buf = tmp
-        offsets = np.arange(n, dtype=np.int64) * stride
-        return ctx, st, buf, offsets, fused
+        return ctx, st, buf, doffs, fused
+
+    def _fused_shuffle(self, filters):
+        """Element size of the shuffle the kernels undo on load (0: none)."""
+        shuffles = _shuffle_sizes(filters)
+        es = self.ds.dtype.itemsize
+        return es if shuffles and shuffles[-1] == es and es > 1 else 0
 
     @staticmethod
     def _chunk_sel(projs):

@@ -1,0 +1,53 @@
+"""Resident mode: ``Active(..., resident=True)`` keeps a variable's decoded
+chunks in HBM across queries.  Every query must return exactly what the
+non-resident path returns (which the other GPU tests pin to the reference),
+while reading from the file only chunks no earlier query loaded.  Covers an
+uncompressed variable and the reference's test1.nc (shuffle + zlib, f8).
+"""
+import numpy as np
+import pytest
+
+from pyactivestorage_amd.active import Active, release_resident
+from tests import _dist_active as D
+from tests.test_gpu_active import variable
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b, what):
+    assert type(a) is type(b) and np.shape(a) == np.shape(b), what
+    np.testing.assert_array_equal(np.ma.getmaskarray(a), np.ma.getmaskarray(b), err_msg=what)
+    np.testing.assert_array_equal(np.ma.getdata(a), np.ma.getdata(b), err_msg=what)
+
+
+def _query(var, method, axis, index, resident):
+    act = Active(var, resident=resident)
+    getattr(act, method)(axis=axis)
+    r = act[index]
+    return r, act.data_read
+
+
+@pytest.mark.parametrize("make", ["synthetic", "test1.nc:tas"])
+def test_resident_matches_fresh(gpu, make):
+    var = D.make_variable() if make == "synthetic" else variable(make)
+    nd = len(var.shape)
+    half = tuple(slice(0, max(1, n // 2)) for n in var.shape)
+    other = tuple(slice(n // 3, n) for n in var.shape)
+    queries = [("mean", None, half), ("max", (0,), other), ("min", (nd - 1,), (slice(None),) * nd),
+               ("mean", (0, nd - 1), half)]
+    try:
+        seen = 0
+        for k, (method, axis, index) in enumerate(queries):
+            want, _ = _query(var, method, axis, index, False)
+            got, read = _query(var, method, axis, index, True)
+            _same(got, want, f"{make} query {k}")
+            seen += read
+        # every chunk is now resident: a repeat reads nothing
+        got, read = _query(var, "mean", None, (slice(None),) * nd, True)
+        assert read == 0
+        want, full_read = _query(var, "mean", None, (slice(None),) * nd, False)
+        _same(got, want, f"{make} repeat")
+        assert 0 < seen <= full_read
+    finally:
+        release_resident(var)
+    assert getattr(var, "_pyas_resident", None) is None
