@@ -33,7 +33,7 @@ from .ingest import read_ranges
 from .inflate import InflateBatch, is_zlib, pack_streams
 from .masking import compile_missing
 from .storage import _decompress, _shuffle_sizes
-from .variable import decode_filters, get_missing_attributes
+from .variable import ChunkedVariable, decode_filters, get_missing_attributes
 
 _ALIGN = 256
 def release_resident(variable) -> None:
@@ -69,10 +69,27 @@ class Active:
         inst._methods = {"min": np.ma.min, "max": np.ma.max, "sum": np.ma.sum, "mean": np.ma.sum}
         return inst
 
-    def __init__(self, variable, axis=None, max_threads: int = 30, device: int = 0,
+    def __init__(self, dataset, ncvar=None, axis=None, max_threads: int = 30, device: int = 0,
                  device_inflate: bool = True, group=None, resident: bool = False):
-        if variable is None:
-            raise ValueError("Must use a valid variable object. Got None")
+        """``dataset``: a netCDF4/HDF5 file path with ``ncvar`` naming the
+        variable (``active.py:185-280``: same checks, same errors), or a
+        :class:`ChunkedVariable` (the reference accepts a pyfive Dataset)."""
+        if dataset is None:
+            raise ValueError(f"Must use a valid file name or variable object for dataset. Got {dataset!r}")
+        if isinstance(dataset, (str, os.PathLike)):
+            path = os.fspath(dataset)
+            if not os.path.isfile(path):
+                raise ValueError(f"Must use existing file for uri. {path} not found")
+            if ncvar is None:
+                raise ValueError("Must set a netCDF variable name to slice")
+            from .hdf5 import open_variable
+            variable = open_variable(path, ncvar)
+        elif isinstance(dataset, ChunkedVariable):
+            variable = dataset
+        else:
+            raise TypeError(f"Variable object dataset can only be a ChunkedVariable. Got {dataset!r}")
+        self.uri = dataset
+        self.ncvar = ncvar
         self.ds = variable
         if axis is not None:
             axis = (axis,) if isinstance(axis, int) else tuple(axis)
