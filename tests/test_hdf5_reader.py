@@ -69,3 +69,44 @@ def test_active_constructor_like_reference(tmp_path):
         Active(123)
     a = Active(os.path.join(NC, "test1.nc"), "tas", axis=1)
     assert a.ds.shape == (12, 64, 128) and a._axis == (1,)
+
+
+# ---------------------------------------------------------------------------
+# synthetic files written by libhdf5 (tests/golden/make_h5_synthetic.py)
+# ---------------------------------------------------------------------------
+SYN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "h5synth")
+
+
+def _synth():
+    import json
+    with open(os.path.join(os.path.dirname(SYN), "h5synth.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("key", sorted(_synth()))
+def test_reader_matches_libhdf5_synthetic(key):
+    m = _synth()[key]
+    path = os.path.join(SYN, m["file"])
+    v = open_variable(path, m["var"])
+    assert list(v.shape) == m["shape"] and list(v.chunks) == m["chunks"]
+    assert v.dtype.str == m["dtype"]
+    got_f = [{"id": x["filter_id"], "client_data": x["client_data"]} for x in (v.filter_pipeline or [])]
+    assert got_f == m["filters"]
+    for k, a in m["attrs"].items():
+        np.testing.assert_array_equal(np.asarray(v.attrs[k]).reshape(-1),
+                                      np.array(a["values"], dtype=a["dtype"]))
+    if m["layout"] == 0:   # compact: the data sit inside the object header
+        (off, size), = v.chunk_index.values()
+        assert size == m["chunk_table"][0]["size"]
+        with open(path, "rb") as fh:
+            fh.seek(off)
+            np.testing.assert_array_equal(np.frombuffer(fh.read(size), dtype=v.dtype),
+                                          np.arange(24, dtype="<i4"))
+    else:
+        want = {tuple(c["coords"]): (c["offset"], c["size"]) for c in m["chunk_table"]}
+        assert v.chunk_index == want
+
+
+def test_reader_refuses_layout_v4_by_name():
+    with pytest.raises(NotImplementedError, match="layout message v4"):
+        open_variable(os.path.join(SYN, "latest.h5"), "v")
