@@ -1,21 +1,29 @@
 """Batched ``Active`` front end: one device launch chain per query.
 
-Mirrors ``activestorage/active.py``'s user API (``Active.method``,
-``.mean()/.min()/.max(axis)``, ``.components``, ``active[index]``,
-``active.py:162-427``) over a :class:`~pyactivestorage_amd.variable.ChunkedVariable`
-(the metadata pyfive supplies to the reference).  ``__getitem__`` replaces
-``_get_selection`` + ``_from_storage`` (``active.py:439-635``):
+Mirrors ``activestorage/active.py``'s user API (``Active(path, ncvar)``,
+``Active.method``, ``.mean()/.min()/.max(axis)``, ``.components``,
+``active[index]``, ``active.py:162-427``).  The dataset is a netCDF4/HDF5
+path, whose metadata and chunk index :mod:`.hdf5` reads (pyfive's part in
+the reference), or a :class:`~pyactivestorage_amd.variable.ChunkedVariable`.
+``__getitem__`` replaces ``_get_selection`` + ``_from_storage``
+(``active.py:439-635``):
 
-1. plan: orthogonal indexer -> touched chunks and per-chunk selections;
+1. plan: orthogonal indexer -> per-dim projections; for box queries the
+   selection table, index pool and chunk list follow by broadcasting;
 2. ingest: for a file on disk, native pread threads (``max_threads``, like
    ``active.py:557``) into pinned slots copied H2D as they fill
    (``pyas_read_ranges``, row f2); zlib chunks are inflated on the device
-   (``pyas_inflate``, row f3); custom readers go through a Python pool;
+   (``pyas_inflate``, row f3) in stream groups that overlap the reads;
+   ``resident=True`` keeps decoded chunks in HBM across queries;
 3. device: one fused reduce over every chunk (full-axis queries) or a
-   partial-axis reduce plus a segmented combine (``pyas_combine_segments``),
-   in both cases with per-chunk sums rounded to the variable dtype first,
-   like the reference's ``out`` array (``active.py:512,585``);
-4. host: format the combined partials exactly like ``active.py:591-630``.
+   partial-axis reduce plus the grid combine (``pyas_combine_grid``; host
+   segments via ``pyas_combine_segments`` otherwise), with per-chunk sums
+   rounded to the variable dtype first, like the reference's ``out`` array
+   (``active.py:512,585``);
+4. ``group=``: each rank of a torch.distributed group does 2-3 for its
+   contiguous share of the chunks, then one all-gather and a rank-order
+   device combine (row e);
+5. host: format the combined partials exactly like ``active.py:591-630``.
 """
 from __future__ import annotations
 

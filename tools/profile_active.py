@@ -10,7 +10,8 @@ import tools.bench_active as B  # noqa: E402
 
 
 def main():
-    axis = tuple(int(x) for x in sys.argv[1:]) or None
+    resident = "--resident" in sys.argv
+    axis = tuple(int(x) for x in sys.argv[1:] if x != "--resident") or None
     import numpy as np
     import torch
     from pyactivestorage_amd.active import Active
@@ -31,7 +32,7 @@ def main():
     attrs = {"_FillValue": np.array([-999.0], dtype=np.float32)}
     var = ChunkedVariable(name="c3", shape=shape, chunks=chunks, dtype=np.float32, chunk_index=index,
                           attrs=attrs, filename=path)
-    act = Active(var)
+    act = Active(var, resident=resident)
     act.mean(axis=axis)
     act[...]
     act.mean(axis=axis)
