@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import concurrent.futures
 import os
+import threading
 
 import numpy as np
 
@@ -44,6 +45,9 @@ from .storage import _decompress, _shuffle_sizes
 from .variable import ChunkedVariable, decode_filters, get_missing_attributes
 
 _ALIGN = 256
+_RESIDENT_LOCK = threading.Lock()
+
+
 def release_resident(variable) -> None:
     """Free the HBM copy that resident-mode ``Active`` queries keep for
     ``variable`` (e.g. after the file changed)."""
@@ -215,18 +219,24 @@ class Active:
         stride = -(-nbytes // _ALIGN) * _ALIGN
         grid = tuple(-(-s // c) for s, c in zip(ds.shape, ds.chunks))
         ctx = get_context(self.device)
-        store = getattr(ds, "_pyas_resident", None)
-        if store is None or store["device"] != self.device:
-            n_all = int(np.prod(grid))
-            store = {"device": self.device, "buf": DeviceBuffer(ctx, max(n_all, 1) * stride),
-                     "loaded": np.zeros(n_all, dtype=bool)}
-            ds._pyas_resident = store
-        c = np.asarray(coords, dtype=np.int64).reshape(len(coords), len(grid))
-        slots = np.ravel_multi_index(c.T, grid) if len(coords) else np.zeros(0, dtype=np.int64)
-        todo = np.nonzero(~store["loaded"][slots])[0]
+        with _RESIDENT_LOCK:
+            store = getattr(ds, "_pyas_resident", None)
+            if store is None or store["device"] != self.device:
+                n_all = int(np.prod(grid))
+                store = {"device": self.device, "buf": DeviceBuffer(ctx, max(n_all, 1) * stride),
+                         "loaded": np.zeros(n_all, dtype=bool)}
+                ds._pyas_resident = store
+            c = np.asarray(coords, dtype=np.int64).reshape(len(coords), len(grid))
+            slots = np.ravel_multi_index(c.T, grid) if len(coords) else np.zeros(0, dtype=np.int64)
+            todo = np.nonzero(~store["loaded"][slots])[0]
         _, st, _, _, fused = self._ingest_fresh([coords[i] for i in todo.tolist()], compressor, filters,
                                                 dst=store["buf"], dst_offsets=slots[todo] * stride)
-        store["loaded"][slots[todo]] = True
+        if todo.size:
+            # another thread's kernels (on its own stream) may read these slots
+            # as soon as they are marked: mark them once the copies have landed
+            ctx.synchronize(st)
+            with _RESIDENT_LOCK:
+                store["loaded"][slots[todo]] = True
         return ctx, st, store["buf"], slots.astype(np.int64) * stride, fused
 
     def _ingest_fresh(self, coords, compressor, filters, dst=None, dst_offsets=None):
