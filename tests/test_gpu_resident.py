@@ -51,3 +51,23 @@ def test_resident_matches_fresh(gpu, make):
     finally:
         release_resident(var)
     assert getattr(var, "_pyas_resident", None) is None
+
+
+def test_resident_concurrent_threads(gpu):
+    """Threads share one resident store (the reference drives Active from
+    dask worker threads, dask-demo/demo.py:107-168): each thread's queries,
+    on its own stream, must see complete chunks."""
+    import concurrent.futures
+    var = D.make_variable()
+    nd = len(var.shape)
+    index_list = [tuple(slice(k, n) for n in var.shape) for k in range(8)]
+    want = [_query(var, "mean", (0,), ix, False)[0] for ix in index_list]
+    try:
+        with concurrent.futures.ThreadPoolExecutor(max_workers=8) as ex:
+            for rep in range(3):
+                got = list(ex.map(lambda ix: _query(var, "mean", (0,), ix, True)[0], index_list))
+                for k, (g, w) in enumerate(zip(got, want)):
+                    _same(g, w, f"rep {rep} thread query {k}")
+    finally:
+        release_resident(var)
+    assert nd == 3
