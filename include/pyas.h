@@ -207,6 +207,24 @@ int pyas_select_chunks(pyas_ctx *ctx, const pyas_batch *batch,
                        const pyas_mask *mask, const int64_t *out_offsets,
                        void *values, uint8_t *mask_out, void *stream);
 
+/* method=None for a whole orthogonal query (Active._select, active.py:
+ * 483-485 -> storage.py:95-103 per chunk, then the reference places each
+ * chunk's selection at its out_selection): element k = (k_0..k_{n-1}) of
+ * chunk c's selection (C order over the selection counts) is written to
+ * values/mask_out at  sum_d pos[chunk_base[c*ndim + d] + k_d] * out_stride[d]
+ * (an element index of the caller's output array).  pos (int64) and
+ * chunk_base (int32) are device arrays; dims dropped by an integer index use
+ * out_stride 0. */
+typedef struct {
+    const int64_t *pos;
+    const int32_t *chunk_base;
+    int64_t out_stride[PYAS_MAX_DIMS];
+} pyas_scatter;
+
+int pyas_select_scatter(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                        const pyas_scatter *scatter, void *values, uint8_t *mask_out,
+                        void *stream);
+
 /* Fixed-order combine of n partials (device) into *out (device).  Used for
  * the per-chunk -> total step and for the cross-GPU combine of per-rank
  * partials after an RCCL all-gather. */

@@ -78,6 +78,15 @@ class Grid(ctypes.Structure):
     ]
 
 
+class Scatter(ctypes.Structure):
+    """pyas_scatter: output placement tables of pyas_select_scatter."""
+    _fields_ = [
+        ("pos", ctypes.c_void_p),
+        ("chunk_base", ctypes.c_void_p),
+        ("out_stride", ctypes.c_int64 * MAX_DIMS),
+    ]
+
+
 PARTIAL_NBYTES = ctypes.sizeof(Partial)
 assert PARTIAL_NBYTES == 32
 
@@ -108,6 +117,8 @@ SIGNATURES = {
     "pyas_reduce_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _u32, _vp],
     "pyas_reduce_axes": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _u32, _vp, _vp, _vp],
     "pyas_select_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _vp, _vp],
+    "pyas_select_scatter": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(Scatter),
+                            _vp, _vp, _vp],
     "pyas_combine_partials": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_segments": [_vp, _i32, _vp, _vp, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_grid": [_vp, _i32, _vp, ctypes.POINTER(Grid), _u32, _vp, _vp],

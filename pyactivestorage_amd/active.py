@@ -678,6 +678,98 @@ class Active:
 
     # -- method=None --------------------------------------------------------
     def _select(self, indexer, compressor, filters):
+        if not any(m is not None and np.size(m) != 1 for m in self.missing):
+            return self._select_scatter(indexer, compressor, filters)
+        return self._select_general(indexer, compressor, filters)
+
+    def _select_scatter(self, indexer, compressor, filters):
+        """method=None over the whole query in one launch: every selected
+        element is written by the device straight to its place in the
+        C-ordered result (pyas_select_scatter), instead of per-chunk host
+        placement at each chunk's out_selection."""
+        ds = self.ds
+        dt = ds.dtype
+        dims = [list(d) for d in indexer.dim_indexers]
+        nd = len(dims)
+        n_coords = [len(p) for p in dims]
+        n = int(np.prod(n_coords))
+        out_shape = indexer.shape
+        # output strides: C order over the kept dims, 0 for integer-dropped ones
+        ostride = np.zeros(nd, dtype=np.int64)
+        kept = [d for d in range(nd) if indexer.dim_indexers[d].kind != "int"]
+        acc = 1
+        for d in reversed(kept):
+            ostride[d] = acc
+            acc *= out_shape[kept.index(d)]
+        ent, pos_parts, bases, pool_parts = [], [], [], []
+        ppos = poolpos = 0
+        for projs in dims:
+            e = np.zeros((len(projs), 3), dtype=np.int32)
+            b = np.zeros(len(projs), dtype=np.int32)
+            for a, p in enumerate(projs):
+                sl = p.chunk_sel
+                if isinstance(sl, slice):
+                    cnt = len(p.out_pos)
+                    e[a] = (sl.start if cnt else 0, sl.step, cnt)
+                    op = np.asarray(p.out_pos, dtype=np.int64)
+                elif isinstance(sl, np.ndarray):
+                    e[a] = (poolpos, 0, sl.size)
+                    pool_parts.append(sl.astype(np.int32))
+                    poolpos += sl.size
+                    op = np.asarray(p.out_pos, dtype=np.int64)
+                else:                                        # integer index: dropped dim
+                    e[a] = (int(sl), 1, 1)
+                    op = np.zeros(1, dtype=np.int64)
+                b[a] = ppos
+                pos_parts.append(op)
+                ppos += op.size
+            ent.append(e)
+            bases.append(b)
+        nd_native = native(dt)
+        if n == 0 or int(np.prod(out_shape)) == 0:
+            return np.ma.MaskedArray(np.zeros(out_shape, dtype=dt))
+        idx = np.indices(n_coords).reshape(nd, n)
+        table = np.zeros((n, _lib.MAX_DIMS, 3), dtype=np.int32)
+        table[:, :, 1] = 1
+        table[:, :, 2] = 1
+        cbase = np.zeros((n, nd), dtype=np.int32)
+        coords = np.zeros((n, nd), dtype=np.int64)
+        for d in range(nd):
+            table[:, d, :] = ent[d][idx[d]]
+            cbase[:, d] = bases[d][idx[d]]
+            coords[:, d] = np.array([p.chunk_ix for p in dims[d]], dtype=np.int64)[idx[d]]
+        pool = np.concatenate(pool_parts) if pool_parts else np.zeros(1, dtype=np.int32)
+        pos = np.concatenate(pos_parts)
+        ctx, st, buf, offsets, fused = self._ingest([tuple(c) for c in coords.tolist()], compressor, filters)
+        full = _all_full(table, ds.chunks)
+        plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused,
+                             sel_table=None if full else table, index_pool=None if full else pool,
+                             missing=self.missing, stream=st)
+        total = int(np.prod(out_shape))
+        pb = DeviceBuffer(ctx, pos.nbytes)
+        ctx.h2d(pb.ptr, pos, st)
+        cb = DeviceBuffer(ctx, cbase.nbytes)
+        ctx.h2d(cb.ptr, np.ascontiguousarray(cbase), st)
+        sc = _lib.Scatter()
+        sc.pos, sc.chunk_base = pb.ptr, cb.ptr
+        for d in range(nd):
+            sc.out_stride[d] = int(ostride[d])
+        vals = np.empty(total, dtype=nd_native)
+        msk = np.empty(total, dtype=np.uint8)
+        vb = DeviceBuffer(ctx, vals.nbytes)
+        mb = DeviceBuffer(ctx, msk.nbytes)
+        engine.select_scatter(ctx, plan.batch, plan.mask_up.struct, sc, vb.ptr, mb.ptr, st)
+        ctx.d2h(vals, vb.ptr, st)
+        ctx.d2h(msk, mb.ptr, st)
+        ctx.synchronize(st)
+        out_vals = vals.reshape(out_shape).astype(dt, copy=False)
+        out_mask = msk.reshape(out_shape).view(bool)
+        if out_mask.any():
+            return np.ma.MaskedArray(out_vals, mask=out_mask)
+        return np.ma.MaskedArray(out_vals)
+
+    def _select_general(self, indexer, compressor, filters):
+        """method=None with vector fill/missing values (per-chunk selections)."""
         ds = self.ds
         dt = ds.dtype
         chunk_list = list(indexer)

@@ -599,6 +599,37 @@ int pyas_select_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *
     return PYAS_OK;
 }
 
+int pyas_select_scatter(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                        const pyas_scatter *scatter, void *values, uint8_t *mask_out,
+                        void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!scatter || !scatter->pos || !scatter->chunk_base)
+        return fail(PYAS_EINVAL, "scatter tables are NULL");
+    pyas::SelectArgs x;
+    std::memset(&x, 0, sizeof(x));
+    int es;
+    bool shuf, bsw, masked;
+    int rc = prepare(ctx, batch, mask, x.r, es, shuf, bsw, masked);
+    if (rc) return rc;
+    if (batch->n_chunks == 0) return PYAS_OK;
+    if (!values) return fail(PYAS_EINVAL, "values is NULL");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    int64_t bpc = (x.r.chunk_elems + pyas::kBlock - 1) / pyas::kBlock;
+    if (bpc > 64) bpc = 64;
+    x.bpc = bpc;
+    x.values = values;
+    x.mask_out = mask_out;
+    x.shuf = shuf;
+    x.bswap = bsw;
+    x.scatter_pos = scatter->pos;
+    x.scatter_base = scatter->chunk_base;
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) x.ostride[d] = scatter->out_stride[d];
+    const int64_t grid = batch->n_chunks * bpc;
+    if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
+    PYAS_HIP(pyas::launch_select(batch->dtype, x, grid, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
 int pyas_combine_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, int64_t n,
                           uint32_t combine_flags, pyas_partial *out, void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");

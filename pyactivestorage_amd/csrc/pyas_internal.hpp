@@ -85,6 +85,11 @@ struct SelectArgs {
     void *values;
     uint8_t *mask_out;
     bool shuf, bswap;
+    // scatter mode (pyas_select_scatter): element k of chunk c's selection
+    // lands at sum_d pos[base[c][d] + k_d] * ostride[d] of the output array
+    const int64_t *scatter_pos;
+    const int32_t *scatter_base;
+    int64_t ostride[PYAS_MAX_DIMS];
 };
 
 // Per-dtype launchers: defined in pyas_kernels.hpp, instantiated per dtype by

@@ -1230,14 +1230,30 @@ __global__ __launch_bounds__(kBlock) void k_select(SelectArgs a) {
 #pragma unroll
     for (int d = 0; d < PYAS_MAX_DIMS; ++d) total *= s.cnt[d];
     const uint32_t all = (1u << r.ndim) - 1u;
-    T *vals = reinterpret_cast<T *>(a.values) + a.out_offsets[c];
-    uint8_t *msk = a.mask_out ? a.mask_out + a.out_offsets[c] : nullptr;
+    const bool scatter = a.scatter_pos != nullptr;
+    T *vals = reinterpret_cast<T *>(a.values) + (scatter ? 0 : a.out_offsets[c]);
+    uint8_t *msk = a.mask_out ? a.mask_out + (scatter ? 0 : a.out_offsets[c]) : nullptr;
+    const int32_t *cb = scatter ? a.scatter_base + c * r.ndim : nullptr;
     for (int64_t e = j * kBlock + threadIdx.x; e < total; e += a.bpc * kBlock) {
         Decomp o{0, {0, 0}};
         decompose(s, r.pool, r.cstride, r.tab, r.ndim, all, e, o);
         const T x = load_elem_rt<T>(base, r.chunk_elems, o.mem, a.shuf, a.bswap);
-        vals[e] = x;
-        if (msk) msk[e] = all_masked(mk, r.tab, o, x) ? 1 : 0;
+        int64_t out = e;
+        if (scatter) {   // block-uniform
+            out = 0;
+            int64_t rem = e;
+#pragma unroll
+            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+                if (d < r.ndim) {
+                    const int64_t cd = s.cnt[d];
+                    const int64_t q = rem / cd, k = rem - q * cd;
+                    rem = q;
+                    out += a.scatter_pos[cb[d] + k] * a.ostride[d];
+                }
+            }
+        }
+        vals[out] = x;
+        if (msk) msk[out] = all_masked(mk, r.tab, o, x) ? 1 : 0;
     }
 }
 

@@ -100,6 +100,13 @@ def select_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, out_offsets_
                "pyas_select_chunks")
 
 
+def select_scatter(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, scatter: _lib.Scatter,
+                   values_ptr, mask_ptr, stream) -> None:
+    _lib.check(ctx.lib.pyas_select_scatter(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
+                                           ctypes.byref(scatter), values_ptr, mask_ptr, stream),
+               "pyas_select_scatter")
+
+
 def combine_partials(ctx: Context, dt, in_ptr, n, out_ptr, round_to_var: bool, stream) -> None:
     flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
     _lib.check(ctx.lib.pyas_combine_partials(ctx.handle, dtype_code(dt), in_ptr, int(n), flags,
