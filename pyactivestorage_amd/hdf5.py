@@ -25,6 +25,7 @@ Anything else raises ``NotImplementedError`` naming the structure.
 """
 from __future__ import annotations
 
+import mmap
 import os
 
 import numpy as np
@@ -42,12 +43,25 @@ class HDF5Error(ValueError):
 class _File:
     def __init__(self, path):
         self.path = path
+        # memory-mapped: only the metadata pages are touched (a variable's
+        # file can be far larger than host memory)
         with open(path, "rb") as f:
-            self.buf = f.read()
-        self.base = self.buf.find(_SIG)
-        if self.base < 0 or self.base % 512:
+            if os.fstat(f.fileno()).st_size == 0:
+                raise HDF5Error(f"{path}: empty file")
+            self.buf = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+        self.base = self._find_superblock()
+        if self.base < 0:
             raise HDF5Error(f"{path}: not an HDF5 file")
         self._superblock()
+
+    def _find_superblock(self):
+        """The signature sits at byte 0, 512, 1024, 2048, ... (user block)."""
+        pos = 0
+        while pos + 8 <= len(self.buf):
+            if self.buf[pos:pos + 8] == _SIG:
+                return pos
+            pos = 512 if pos == 0 else pos * 2
+        return -1
 
     # -- primitives --------------------------------------------------------
     def u(self, pos, n):
@@ -187,7 +201,7 @@ class _File:
         for _ in range(n):
             name_off, oh = self.addr(q), self.addr(q + self.so)
             e = heap_data + name_off
-            name = self.buf[e:self.buf.index(b"\0", e)].decode()
+            name = self.buf[e:self.buf.find(b"\0", e)].decode()
             out[name] = oh
             q += 2 * self.so + 24
 
