@@ -14,7 +14,7 @@ Supported, per the HDF5 File Format Specification (v3.0):
 * object headers v1 and v2 (``OHDR``/``OCHK``, continuation messages);
 * groups stored as symbol tables (v1 B-tree ``TREE`` type 0 + ``SNOD``
   nodes + local ``HEAP``), compact link messages, or dense links
-  (fractal heap ``FRHP`` + v2 B-tree ``BTHD`` name index, leaf roots);
+  (fractal heap ``FRHP`` + v2 B-tree ``BTHD`` name index);
 * dataspace, datatype (fixed-point and IEEE float, either byte order),
   data layout v3 (compact, contiguous, chunked with a v1 chunk B-tree),
   filter pipeline v1/v2, and attributes v1-v3, compact or dense;
@@ -224,20 +224,54 @@ class _File:
         return name, (self.addr(q) if ltype == 0 else None)
 
     def _btree2_records(self, bt):
+        """Every record of a v2 B-tree (``BTHD``), internal nodes included.
+        Field widths follow libhdf5's H5B2__hdr_init: a child pointer is the
+        child's address, its record count (width of the leaf maximum) and,
+        below depth 1, the child subtree's total count."""
         p = self.at(bt)
         if self.buf[p:p + 4] != b"BTHD":
             raise HDF5Error("bad v2 B-tree header")
+        node_size = self.u(p + 6, 4)
         rec_size = self.u(p + 10, 2)
         depth = self.u(p + 12, 2)
         root = self.addr(p + 16)
         nroot = self.u(p + 16 + self.so, 2)
-        if depth != 0:
-            raise NotImplementedError("v2 B-tree deeper than one leaf")
-        r = self.at(root)
-        if self.buf[r:r + 4] != b"BTLF":
-            raise HDF5Error("bad v2 B-tree leaf")
-        q = r + 6
-        return [self.buf[q + i * rec_size: q + (i + 1) * rec_size] for i in range(nroot)]
+        if root == _UNDEF or nroot == 0:
+            return []
+
+        def enc(v):          # H5VM_limit_enc_size: bytes to encode v
+            return (max(v, 1).bit_length() - 1) // 8 + 1
+
+        prefix = 10          # signature, version, type, checksum
+        cum = [(node_size - prefix) // rec_size]
+        max_nrec_size = enc(cum[0])
+        cum_size = [0]
+        for u in range(1, depth + 1):
+            ptr = self.so + max_nrec_size + (cum_size[u - 1] if u > 1 else 0)
+            mx = (node_size - (prefix + ptr)) // (rec_size + ptr)
+            cum.append((mx + 1) * cum[u - 1] + mx)
+            cum_size.append(enc(cum[u]))
+        out = []
+
+        def node(addr, nrec, d):
+            q = self.at(addr)
+            sig = b"BTLF" if d == 0 else b"BTIN"
+            if self.buf[q:q + 4] != sig:
+                raise HDF5Error("bad v2 B-tree node")
+            q += 6
+            out.extend(self.buf[q + i * rec_size: q + (i + 1) * rec_size] for i in range(nrec))
+            if d == 0:
+                return
+            q += nrec * rec_size
+            for _ in range(nrec + 1):
+                child = self.addr(q)
+                q += self.so
+                cn = self.u(q, max_nrec_size)
+                q += max_nrec_size + (cum_size[d - 1] if d > 1 else 0)
+                node(child, cn, d - 1)
+
+        node(root, nroot, depth)
+        return out
 
     # -- attributes --------------------------------------------------------------
     def attributes(self, msgs):

@@ -92,6 +92,16 @@ def main():
         dsid.write(h5py.h5s.ALL, h5py.h5s.ALL, np.arange(24, dtype="<i4").reshape(6, 4))
     cases += [(p, "small")]
 
+    p = os.path.join(OUT, "v108_big_btrees.h5")               # v2 B-trees with internal nodes
+    with h5py.File(p, "w", libver=("v108", "v110")) as f:
+        for i in range(400):                                    # dense links, depth >= 1 name index
+            f.create_dataset(f"var{i:03d}", data=np.full((3,), i, dtype="<i4"), chunks=(3,))
+        d = f.create_dataset("many_attrs", data=np.arange(12, dtype="<f4").reshape(3, 4), chunks=(3, 2))
+        for i in range(3000):                                   # dense attributes, depth 2 name index
+            d.attrs[f"attr{i:04d}"] = np.float64(i) / 7
+        d.attrs["_FillValue"] = np.float32(-1.0)
+    cases += [(p, "var000"), (p, "var257"), (p, "var399"), (p, "many_attrs")]
+
     p = os.path.join(OUT, "latest.h5")                        # layout v4: refused by name
     with h5py.File(p, "w", libver="latest") as f:
         f.create_dataset("v", data=np.zeros((8, 8), "<f4"), chunks=(4, 4), maxshape=(None, 8))
