@@ -16,7 +16,8 @@ Supported, per the HDF5 File Format Specification (v3.0):
   nodes + local ``HEAP``), compact link messages, or dense links
   (fractal heap ``FRHP`` + v2 B-tree ``BTHD`` name index);
 * dataspace, datatype (fixed-point and IEEE float, either byte order),
-  data layout v3 (compact, contiguous, chunked with a v1 chunk B-tree),
+  data layout v3 (compact, contiguous, chunked with a v1 chunk B-tree) and
+  v4 (single-chunk, implicit and fixed-array chunk indexes),
   filter pipeline v1/v2, and attributes v1-v3, compact or dense;
 * attribute values of numeric type (what ``get_missing_attributes`` needs,
   ``active.py:126-159``) and fixed-length strings.
@@ -479,6 +480,80 @@ class _FractalHeap:
         raise HDF5Error(f"heap offset {off} not in any direct block")
 
 
+_INDEX_NAMES = {1: "single chunk", 2: "implicit", 3: "fixed array", 4: "extensible array",
+                5: "v2 B-tree"}
+
+
+def _layout4_chunks(f: _File, d: int, shape, dtype):
+    """Data layout message v4, chunked class: {chunk coords: (offset, size)}
+    for the single-chunk, implicit and fixed-array chunk indexes."""
+    flags, dimensionality, enc = f.buf[d + 2], f.buf[d + 3], f.buf[d + 4]
+    q = d + 5
+    dims = [f.u(q + enc * i, enc) for i in range(dimensionality)]
+    q += enc * dimensionality
+    chunks, esize = tuple(dims[:-1]), dims[-1]
+    itype = f.buf[q]
+    q += 1
+    grid = [-(-s // c) for s, c in zip(shape, chunks)]
+    nbytes = int(np.prod(chunks)) * esize
+    coords = list(np.ndindex(*grid))
+    if itype == 1:                                  # single chunk
+        size = nbytes
+        if flags & 0x02:                            # filtered: size + filter mask
+            size = f.length(q)
+            q += f.sl + 4
+        a = f.addr(q)
+        return chunks, ({} if a == _UNDEF else {coords[0]: (f.at(a), size)})
+    if itype == 2:                                  # implicit: chunks back to back
+        a = f.addr(q)
+        return chunks, ({} if a == _UNDEF else
+                        {c: (f.at(a) + i * nbytes, nbytes) for i, c in enumerate(coords)})
+    if itype == 3:                                  # fixed array (FAHD / FADB)
+        a = f.addr(q + 1)
+        return chunks, ({} if a == _UNDEF else _fixed_array(f, a, coords, nbytes))
+    raise NotImplementedError(f"chunk index type {itype} "
+                              f"({_INDEX_NAMES.get(itype, 'unknown')})")
+
+
+def _fixed_array(f: _File, hdr, coords, nbytes):
+    p = f.at(hdr)
+    if f.buf[p:p + 4] != b"FAHD":
+        raise HDF5Error("bad fixed array header")
+    client, esz, page_bits = f.buf[p + 5], f.buf[p + 6], f.buf[p + 7]
+    nent = f.length(p + 8)
+    db = f.at(f.addr(p + 8 + f.sl))
+    if f.buf[db:db + 4] != b"FADB":
+        raise HDF5Error("bad fixed array data block")
+    q = db + 6 + f.so
+    page = 1 << page_bits
+    paged = nent > page
+    if paged:
+        npages = -(-nent // page)
+        q += (npages + 7) // 8 + 4                  # page init bitmap + prefix checksum
+
+    def entry(i):
+        if paged:                                   # pages of `page` entries + checksum
+            pg, k = divmod(i, page)
+            pos = q + pg * (page * esz + 4) + k * esz
+        else:
+            pos = q + i * esz
+        a = f.addr(pos)
+        if client == 1:                             # filtered: address, size, filter mask
+            size = f.u(pos + f.so, esz - f.so - 4)
+            if f.u(pos + esz - 4, 4):
+                raise NotImplementedError("chunk with skipped filters (filter mask)")
+        else:
+            size = nbytes
+        return a, size
+
+    out = {}
+    for i, c in enumerate(coords[:nent]):
+        a, size = entry(i)
+        if a != _UNDEF:
+            out[c] = (f.at(a), size)
+    return out
+
+
 def _variable_messages(f: _File, name: str):
     node = f.root
     for part in [p for p in name.split("/") if p]:
@@ -511,9 +586,11 @@ def open_variable(path: str, name: str) -> ChunkedVariable:
         raise HDF5Error(f"{name!r} in {path} is not a dataset")
     d, _ = layout
     ver, cls = f.buf[d], f.buf[d + 1]
-    if ver != 3:
+    if ver not in (3, 4):
         raise NotImplementedError(f"data layout message v{ver}")
-    if cls == 2:                                   # chunked
+    if cls == 2 and ver == 4:                      # chunked, v4 chunk indexes
+        chunks, index = _layout4_chunks(f, d, shape, dtype)
+    elif cls == 2:                                 # chunked, v1 B-tree
         rank = f.buf[d + 2] - 1
         bt = f.addr(d + 3)
         q = d + 3 + f.so

@@ -102,9 +102,24 @@ def main():
         d.attrs["_FillValue"] = np.float32(-1.0)
     cases += [(p, "var000"), (p, "var257"), (p, "var399"), (p, "many_attrs")]
 
-    p = os.path.join(OUT, "latest.h5")                        # layout v4: refused by name
+    p = os.path.join(OUT, "latest.h5")                        # layout v4 chunk indexes
     with h5py.File(p, "w", libver="latest") as f:
-        f.create_dataset("v", data=np.zeros((8, 8), "<f4"), chunks=(4, 4), maxshape=(None, 8))
+        f.create_dataset("v", data=np.zeros((8, 8), "<f4"), chunks=(4, 4), maxshape=(None, 8))  # extensible array
+        f.create_dataset("fa", data=rng.normal(size=(20, 30)).astype("<f4"), chunks=(8, 8))       # fixed array
+        f.create_dataset("fa_z", data=rng.normal(size=(20, 30)).astype(">f8"), chunks=(8, 8),
+                         compression="gzip", shuffle=True)                                         # filtered
+        f.create_dataset("fa_paged", data=np.arange(2500 * 4, dtype="<i2").reshape(2500, 4),
+                         chunks=(1, 4))                                                            # > 1024 entries
+        f.create_dataset("single", data=rng.normal(size=(6, 7)).astype("<f4"), chunks=(6, 7))
+        f.create_dataset("single_z", data=rng.normal(size=(6, 7)).astype("<f4"), chunks=(6, 7),
+                         compression="gzip")
+        dcpl = h5py.h5p.create(h5py.h5p.DATASET_CREATE)
+        dcpl.set_chunk((4, 5))
+        dcpl.set_alloc_time(h5py.h5d.ALLOC_TIME_EARLY)
+        sid = h5py.h5s.create_simple((12, 10))
+        dsid = h5py.h5d.create(f.id, b"implicit", h5py.h5t.IEEE_F32LE, sid, dcpl=dcpl)
+        dsid.write(h5py.h5s.ALL, h5py.h5s.ALL, rng.normal(size=(12, 10)).astype("<f4"))
+    cases += [(p, n) for n in ("fa", "fa_z", "fa_paged", "single", "single_z", "implicit")]
     out = {f"{os.path.basename(a)}:{b}": describe(a, b) for a, b in cases}
     with open(os.path.join(HERE, "h5synth.json"), "w") as fh:
         json.dump(out, fh, indent=1)

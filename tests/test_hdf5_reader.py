@@ -107,6 +107,6 @@ def test_reader_matches_libhdf5_synthetic(key):
         assert v.chunk_index == want
 
 
-def test_reader_refuses_layout_v4_by_name():
-    with pytest.raises(NotImplementedError, match="layout message v4"):
+def test_reader_refuses_extensible_array_by_name():
+    with pytest.raises(NotImplementedError, match="extensible array"):
         open_variable(os.path.join(SYN, "latest.h5"), "v")
