@@ -81,11 +81,20 @@ class Active:
         inst._methods = {"min": np.ma.min, "max": np.ma.max, "sum": np.ma.sum, "mean": np.ma.sum}
         return inst
 
-    def __init__(self, dataset, ncvar=None, axis=None, max_threads: int = 30, device: int = 0,
-                 device_inflate: bool = True, group=None, resident: bool = False):
+    def __init__(self, dataset, ncvar=None, axis=None, interface_type=None, max_threads: int = 30,
+                 storage_options=None, active_storage_url=None, option_disable_chunk_cache=False,
+                 *, device: int = 0, device_inflate: bool = True, group=None, resident: bool = False):
         """``dataset``: a netCDF4/HDF5 file path with ``ncvar`` naming the
-        variable (``active.py:185-280``: same checks, same errors), or a
-        :class:`ChunkedVariable` (the reference accepts a pyfive Dataset)."""
+        variable (``active.py:185-280``: same signature, checks and errors),
+        or a :class:`ChunkedVariable` (the reference accepts a pyfive
+        Dataset).  Local files only: ``interface_type`` "s3"/"https" and
+        ``storage_options`` (remote object stores) are not served here."""
+        if interface_type not in (None, "", "posix", "ActivePosix") or storage_options is not None:
+            raise NotImplementedError(
+                f"interface_type={interface_type!r}: remote object stores are outside this backend; "
+                "point Reductionist clients at pyactivestorage_amd.reductionist_server instead")
+        self.active_storage_url = active_storage_url
+        self.option_disable_chunk_cache = bool(option_disable_chunk_cache)
         if dataset is None:
             raise ValueError(f"Must use a valid file name or variable object for dataset. Got {dataset!r}")
         if isinstance(dataset, (str, os.PathLike)):

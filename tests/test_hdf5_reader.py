@@ -110,3 +110,14 @@ def test_reader_matches_libhdf5_synthetic(key):
 def test_reader_refuses_extensible_array_by_name():
     with pytest.raises(NotImplementedError, match="extensible array"):
         open_variable(os.path.join(SYN, "latest.h5"), "v")
+
+
+def test_active_remote_interfaces_refused():
+    """The reference's remote modes (interface_type s3/https, storage_options,
+    active.py:185-260) are not served by this backend: refused by name."""
+    with pytest.raises(NotImplementedError, match="remote object stores"):
+        Active("s3://bucket/file.nc", "tas", interface_type="s3")
+    with pytest.raises(NotImplementedError):
+        Active(os.path.join(NC, "test1.nc"), "tas", storage_options={"anon": True})
+    a = Active(os.path.join(NC, "test1.nc"), "tas", None, None, 30, None, None, True)
+    assert a.option_disable_chunk_cache and a._max_threads == 30
