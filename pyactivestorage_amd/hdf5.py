@@ -17,7 +17,8 @@ Supported, per the HDF5 File Format Specification (v3.0):
   (fractal heap ``FRHP`` + v2 B-tree ``BTHD`` name index);
 * dataspace, datatype (fixed-point and IEEE float, either byte order),
   data layout v3 (compact, contiguous, chunked with a v1 chunk B-tree) and
-  v4 (single-chunk, implicit and fixed-array chunk indexes),
+  v4 (single-chunk, implicit, fixed-array and extensible-array chunk
+  indexes; the v2-B-tree index for several unlimited dims is refused),
   filter pipeline v1/v2, and attributes v1-v3, compact or dense;
 * attribute values of numeric type (what ``get_missing_attributes`` needs,
   ``active.py:126-159``) and fixed-length strings.
@@ -338,6 +339,18 @@ class _File:
             raise NotImplementedError(f"dataspace v{ver}")
         return tuple(self.length(q + i * self.sl) for i in range(rank))
 
+    def max_dims(self, d):
+        """Maximum dimension sizes of a dataspace message (None: unlimited);
+        the current sizes when the message holds none."""
+        ver, rank, flags = self.buf[d], self.buf[d + 1], self.buf[d + 2]
+        q = d + (8 if ver == 1 else 4)
+        cur = tuple(self.length(q + i * self.sl) for i in range(rank))
+        if not flags & 1:
+            return cur
+        q += rank * self.sl
+        mx = [self.length(q + i * self.sl) for i in range(rank)]
+        return tuple(None if m == _UNDEF else m for m in mx)
+
     def datatype(self, d, strict=True):
         cls = self.buf[d] & 0x0F
         bits = self.buf[d + 1]
@@ -484,7 +497,7 @@ _INDEX_NAMES = {1: "single chunk", 2: "implicit", 3: "fixed array", 4: "extensib
                 5: "v2 B-tree"}
 
 
-def _layout4_chunks(f: _File, d: int, shape, dtype):
+def _layout4_chunks(f: _File, d: int, shape, dtype, maxdims=None):
     """Data layout message v4, chunked class: {chunk coords: (offset, size)}
     for the single-chunk, implicit and fixed-array chunk indexes."""
     flags, dimensionality, enc = f.buf[d + 2], f.buf[d + 3], f.buf[d + 4]
@@ -511,8 +524,114 @@ def _layout4_chunks(f: _File, d: int, shape, dtype):
     if itype == 3:                                  # fixed array (FAHD / FADB)
         a = f.addr(q + 1)
         return chunks, ({} if a == _UNDEF else _fixed_array(f, a, coords, nbytes))
+    if itype == 4 and maxdims is not None:          # extensible array (EAHD ...)
+        a = f.addr(q + 5)
+        unlim = [i for i, m in enumerate(maxdims) if m is None]
+        if len(unlim) != 1:
+            raise NotImplementedError("extensible array index without exactly one unlimited dim")
+        u = unlim[0]
+        # linear chunk index: the unlimited dim slowest, the others row-major
+        # over their (fixed) chunk counts (libhdf5's swizzled down-chunks)
+        order = [u] + [i for i in range(len(grid)) if i != u]
+        sub = [grid[i] for i in order[1:]]
+        lin = {}
+        for c in coords:
+            k = c[u]
+            for i in order[1:]:
+                k = k * grid[i] + c[i]
+            lin[c] = k
+        return chunks, ({} if a == _UNDEF else _extensible_array(f, a, lin, nbytes))
     raise NotImplementedError(f"chunk index type {itype} "
                               f"({_INDEX_NAMES.get(itype, 'unknown')})")
+
+
+def _chunk_entry(f: _File, pos, client, esz, nbytes):
+    """(address, size) of one chunk-index array element (client 1: filtered)."""
+    a = f.addr(pos)
+    if client == 1:
+        size = f.u(pos + f.so, esz - f.so - 4)
+        if f.u(pos + esz - 4, 4):
+            raise NotImplementedError("chunk with skipped filters (filter mask)")
+        return a, size
+    return a, nbytes
+
+
+def _extensible_array(f: _File, hdr, lin, nbytes):
+    """Chunk addresses from an extensible array (libhdf5 H5EA: index block
+    elements, then super blocks of doubling data blocks, as H5EA__hdr_init
+    and H5EA__lookup_elmt lay them out)."""
+    p = f.at(hdr)
+    if f.buf[p:p + 4] != b"EAHD":
+        raise HDF5Error("bad extensible array header")
+    client, esz = f.buf[p + 5], f.buf[p + 6]
+    max_bits, idx_elmts, dblk_min, sblk_min_ptrs, page_bits = (f.buf[p + 7], f.buf[p + 8], f.buf[p + 9],
+                                                               f.buf[p + 10], f.buf[p + 11])
+    ib = f.addr(p + 12 + 6 * f.sl)
+    arr_off = (max_bits + 7) // 8
+    page_n = 1 << page_bits
+    nsblks = 1 + (max_bits - (dblk_min.bit_length() - 1))
+    info, start_idx, start_dblk = [], 0, 0
+    for u in range(nsblks):
+        nd, ne = 1 << (u // 2), (1 << ((u + 1) // 2)) * dblk_min
+        info.append((nd, ne, start_idx, start_dblk))
+        start_idx += nd * ne
+        start_dblk += nd
+    ib_nsblks = 2 * (sblk_min_ptrs.bit_length() - 1)
+    ndblk_addrs = 2 * (sblk_min_ptrs - 1)
+    nsblk_addrs = nsblks - ib_nsblks
+    q = f.at(ib)
+    if f.buf[q:q + 4] != b"EAIB":
+        raise HDF5Error("bad extensible array index block")
+    q += 6 + f.so
+    elmts = q
+    dblk_addrs = [f.addr(q + idx_elmts * esz + i * f.so) for i in range(ndblk_addrs)]
+    sq = q + idx_elmts * esz + ndblk_addrs * f.so
+    sblk_addrs = [f.addr(sq + i * f.so) for i in range(nsblk_addrs)]
+
+    def in_dblock(daddr, ne, k):
+        d = f.at(daddr)
+        if f.buf[d:d + 4] != b"EADB":
+            raise HDF5Error("bad extensible array data block")
+        d += 6 + f.so + arr_off
+        if ne > page_n:                              # paged: prefix checksum, pages + checksums
+            d += 4
+            pg, k = divmod(k, page_n)
+            return d + pg * (page_n * esz + 4) + k * esz
+        return d + k * esz
+
+    def lookup(i):
+        if i < idx_elmts:
+            return elmts + i * esz
+        j = i - idx_elmts
+        s = ((j // dblk_min) + 1).bit_length() - 1
+        nd, ne, s_start, s_dblk = info[s]
+        e = j - s_start
+        if s < ib_nsblks:
+            daddr = dblk_addrs[s_dblk + e // ne]
+        else:
+            sb = sblk_addrs[s - ib_nsblks]
+            if sb == _UNDEF:
+                return None
+            b = f.at(sb)
+            if f.buf[b:b + 4] != b"EASB":
+                raise HDF5Error("bad extensible array super block")
+            b += 6 + f.so + arr_off
+            if ne > page_n:                          # page-init bitmap per data block
+                b += nd * (((ne // page_n) + 7) // 8)
+            daddr = f.addr(b + (e // ne) * f.so)
+        if daddr == _UNDEF:
+            return None
+        return in_dblock(daddr, ne, e % ne)
+
+    out = {}
+    for c, i in lin.items():
+        pos = lookup(i)
+        if pos is None:
+            continue
+        a, size = _chunk_entry(f, pos, client, esz, nbytes)
+        if a != _UNDEF:
+            out[c] = (f.at(a), size)
+    return out
 
 
 def _fixed_array(f: _File, hdr, coords, nbytes):
@@ -571,11 +690,12 @@ def open_variable(path: str, name: str) -> ChunkedVariable:
     ``pyfive.File(path)[name]``, ``active.py:439-471``)."""
     f = _File(os.fspath(path))
     msgs = _variable_messages(f, name)
-    shape = dtype = layout = None
+    shape = dtype = layout = maxdims = None
     filters = None
     for mtype, d, size in msgs:
         if mtype == 0x01:
             shape = f.dataspace(d)
+            maxdims = f.max_dims(d)
         elif mtype == 0x03:
             dtype = f.datatype(d)
         elif mtype == 0x08:
@@ -589,7 +709,7 @@ def open_variable(path: str, name: str) -> ChunkedVariable:
     if ver not in (3, 4):
         raise NotImplementedError(f"data layout message v{ver}")
     if cls == 2 and ver == 4:                      # chunked, v4 chunk indexes
-        chunks, index = _layout4_chunks(f, d, shape, dtype)
+        chunks, index = _layout4_chunks(f, d, shape, dtype, maxdims)
     elif cls == 2:                                 # chunked, v1 B-tree
         rank = f.buf[d + 2] - 1
         bt = f.addr(d + 3)

@@ -119,7 +119,24 @@ def main():
         sid = h5py.h5s.create_simple((12, 10))
         dsid = h5py.h5d.create(f.id, b"implicit", h5py.h5t.IEEE_F32LE, sid, dcpl=dcpl)
         dsid.write(h5py.h5s.ALL, h5py.h5s.ALL, rng.normal(size=(12, 10)).astype("<f4"))
-    cases += [(p, n) for n in ("fa", "fa_z", "fa_paged", "single", "single_z", "implicit")]
+        # extensible arrays: one unlimited dim, first or not; enough chunks to
+        # fill the index block, index-block data blocks, super blocks, pages
+        f.create_dataset("ea", data=rng.normal(size=(10, 8)).astype("<f4"), chunks=(3, 4),
+                         maxshape=(None, 8))
+        f.create_dataset("ea_big", data=np.arange(6000 * 3, dtype="<i4").reshape(6000, 3), chunks=(1, 3),
+                         maxshape=(None, 3))
+        f.create_dataset("ea_z", data=rng.normal(size=(300, 6)).astype("<f8"), chunks=(2, 3),
+                         maxshape=(None, 6), compression="gzip")
+        # unlimited dim not first: libhdf5 1.10.6's H5Dget_chunk_info reports
+        # these chunks' offsets swizzled, so the test checks chunk contents
+        # (arange data) instead of that table
+        f.create_dataset("ea_mid", data=np.arange(4 * 50 * 5, dtype="<f4").reshape(4, 50, 5),
+                         chunks=(2, 1, 5), maxshape=(4, None, 5))
+    cases += [(p, n) for n in ("fa", "fa_z", "fa_paged", "single", "single_z", "implicit",
+                               "v", "ea", "ea_big", "ea_z", "ea_mid")]
+    p = os.path.join(OUT, "latest_2unlim.h5")                 # v2 B-tree chunk index: refused
+    with h5py.File(p, "w", libver="latest") as f:
+        f.create_dataset("v", data=np.zeros((8, 8), "<f4"), chunks=(4, 4), maxshape=(None, None))
     out = {f"{os.path.basename(a)}:{b}": describe(a, b) for a, b in cases}
     with open(os.path.join(HERE, "h5synth.json"), "w") as fh:
         json.dump(out, fh, indent=1)

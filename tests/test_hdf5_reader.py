@@ -102,14 +102,23 @@ def test_reader_matches_libhdf5_synthetic(key):
             fh.seek(off)
             np.testing.assert_array_equal(np.frombuffer(fh.read(size), dtype=v.dtype),
                                           np.arange(24, dtype="<i4"))
+    elif m["var"] == "ea_mid":   # contents: arange data (see make_h5_synthetic.py)
+        full = np.arange(int(np.prod(m["shape"])), dtype="<f4").reshape(m["shape"])
+        assert len(v.chunk_index) == len(m["chunk_table"])
+        with open(path, "rb") as fh:
+            for coords, (off, size) in v.chunk_index.items():
+                fh.seek(off)
+                block = np.frombuffer(fh.read(size), dtype="<f4").reshape(v.chunks)
+                sl = tuple(slice(c * n, (c + 1) * n) for c, n in zip(coords, v.chunks))
+                np.testing.assert_array_equal(block, full[sl])
     else:
         want = {tuple(c["coords"]): (c["offset"], c["size"]) for c in m["chunk_table"]}
         assert v.chunk_index == want
 
 
-def test_reader_refuses_extensible_array_by_name():
-    with pytest.raises(NotImplementedError, match="extensible array"):
-        open_variable(os.path.join(SYN, "latest.h5"), "v")
+def test_reader_refuses_v2_btree_chunk_index_by_name():
+    with pytest.raises(NotImplementedError, match="v2 B-tree"):
+        open_variable(os.path.join(SYN, "latest_2unlim.h5"), "v")
 
 
 def test_active_remote_interfaces_refused():
