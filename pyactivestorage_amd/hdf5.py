@@ -17,8 +17,8 @@ Supported, per the HDF5 File Format Specification (v3.0):
   (fractal heap ``FRHP`` + v2 B-tree ``BTHD`` name index);
 * dataspace, datatype (fixed-point and IEEE float, either byte order),
   data layout v3 (compact, contiguous, chunked with a v1 chunk B-tree) and
-  v4 (single-chunk, implicit, fixed-array and extensible-array chunk
-  indexes; the v2-B-tree index for several unlimited dims is refused),
+  v4 (single-chunk, implicit, fixed-array, extensible-array and v2-B-tree
+  chunk indexes),
   filter pipeline v1/v2, and attributes v1-v3, compact or dense;
 * attribute values of numeric type (what ``get_missing_attributes`` needs,
   ``active.py:126-159``) and fixed-length strings.
@@ -499,7 +499,8 @@ _INDEX_NAMES = {1: "single chunk", 2: "implicit", 3: "fixed array", 4: "extensib
 
 def _layout4_chunks(f: _File, d: int, shape, dtype, maxdims=None):
     """Data layout message v4, chunked class: {chunk coords: (offset, size)}
-    for the single-chunk, implicit and fixed-array chunk indexes."""
+    for the single-chunk, implicit, fixed-array, extensible-array and
+    v2-B-tree chunk indexes."""
     flags, dimensionality, enc = f.buf[d + 2], f.buf[d + 3], f.buf[d + 4]
     q = d + 5
     dims = [f.u(q + enc * i, enc) for i in range(dimensionality)]
@@ -541,8 +542,37 @@ def _layout4_chunks(f: _File, d: int, shape, dtype, maxdims=None):
                 k = k * grid[i] + c[i]
             lin[c] = k
         return chunks, ({} if a == _UNDEF else _extensible_array(f, a, lin, nbytes))
+    if itype == 5:                                  # v2 B-tree of chunk records
+        a = f.addr(q + 6)
+        return chunks, ({} if a == _UNDEF else _btree2_chunks(f, a, len(shape), nbytes))
     raise NotImplementedError(f"chunk index type {itype} "
                               f"({_INDEX_NAMES.get(itype, 'unknown')})")
+
+
+def _btree2_chunks(f: _File, bt, rank, nbytes):
+    """Chunk records of a v2 B-tree chunk index (record type 10,
+    H5B2_CDSET_ID: address + scaled offsets; type 11, H5B2_CDSET_FILT_ID:
+    address + size + filter mask + scaled offsets), as libhdf5's
+    H5Dbtree2.c encodes them."""
+    rtype = f.buf[f.at(bt) + 5]
+    size_len = min(8, 1 + ((max(nbytes, 1).bit_length() - 1) + 8) // 8)
+    out = {}
+    for rec in f._btree2_records(bt):
+        a = int.from_bytes(rec[:f.so], "little")
+        q = f.so
+        size = nbytes
+        if rtype == 11:
+            size = int.from_bytes(rec[q:q + size_len], "little")
+            q += size_len
+            if int.from_bytes(rec[q:q + 4], "little"):
+                raise NotImplementedError("chunk with skipped filters (filter mask)")
+            q += 4
+        elif rtype != 10:
+            raise HDF5Error(f"v2 B-tree record type {rtype} in a chunk index")
+        coords = tuple(int.from_bytes(rec[q + 8 * i: q + 8 * i + 8], "little") for i in range(rank))
+        if a != _UNDEF:
+            out[coords] = (f.at(a), size)
+    return out
 
 
 def _chunk_entry(f: _File, pos, client, esz, nbytes):

@@ -134,9 +134,15 @@ def main():
                          chunks=(2, 1, 5), maxshape=(4, None, 5))
     cases += [(p, n) for n in ("fa", "fa_z", "fa_paged", "single", "single_z", "implicit",
                                "v", "ea", "ea_big", "ea_z", "ea_mid")]
-    p = os.path.join(OUT, "latest_2unlim.h5")                 # v2 B-tree chunk index: refused
+    p = os.path.join(OUT, "latest_2unlim.h5")                 # v2 B-tree chunk index
     with h5py.File(p, "w", libver="latest") as f:
-        f.create_dataset("v", data=np.zeros((8, 8), "<f4"), chunks=(4, 4), maxshape=(None, None))
+        f.create_dataset("v", data=rng.normal(size=(8, 8)).astype("<f4"), chunks=(4, 4),
+                         maxshape=(None, None))
+        f.create_dataset("many", data=np.arange(60 * 70, dtype="<i2").reshape(60, 70), chunks=(2, 3),
+                         maxshape=(None, None))                                  # internal nodes
+        f.create_dataset("many_z", data=rng.normal(size=(40, 50)).astype("<f8"), chunks=(3, 4),
+                         maxshape=(None, None), compression="gzip", shuffle=True)  # filtered records
+    cases += [(p, n) for n in ("v", "many", "many_z")]
     out = {f"{os.path.basename(a)}:{b}": describe(a, b) for a, b in cases}
     with open(os.path.join(HERE, "h5synth.json"), "w") as fh:
         json.dump(out, fh, indent=1)

@@ -116,9 +116,10 @@ def test_reader_matches_libhdf5_synthetic(key):
         assert v.chunk_index == want
 
 
-def test_reader_refuses_v2_btree_chunk_index_by_name():
-    with pytest.raises(NotImplementedError, match="v2 B-tree"):
-        open_variable(os.path.join(SYN, "latest_2unlim.h5"), "v")
+def test_reader_chunk_index_types_covered():
+    """Every chunk index kind of layout v3/v4 is among the synthetic cases."""
+    layouts = {m["var"]: m["layout"] for m in _synth().values()}
+    assert {"fa", "fa_paged", "single", "implicit", "ea_big", "many"} <= set(layouts)
 
 
 def test_active_remote_interfaces_refused():
