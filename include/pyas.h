@@ -267,6 +267,26 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
                       const pyas_grid *grid, uint32_t combine_flags, pyas_partial *out,
                       void *stream);
 
+/* Result formatting on the device: the last step of Active._from_storage
+ * (active.py:591-630) applied to n combined partials (device), so that only
+ * the result's values and mask cross PCIe (9-16 bytes per output instead of
+ * the 32-byte partial).  `values` (device) receives
+ *   PYAS_FORMAT_SUM : the sum in the variable dtype for floats (the partial's
+ *                     f64 rounded, as `out` of that dtype stores it), int64
+ *                     for signed and uint64 for unsigned ints;
+ *   PYAS_FORMAT_MIN / PYAS_FORMAT_MAX: the value in the variable dtype;
+ *   PYAS_FORMAT_MEAN: float64, bit-identical to np.ma's `out / n`
+ *                     (active.py:630): masked where n == 0, where the
+ *                     quotient is not finite, or where np.ma's safe-divide
+ *                     domain |out| * finfo(float).tiny >= |n| holds; a
+ *                     masked element holds 0.0 + f64(out) as np.ma leaves it.
+ * mask (device) receives one byte per element (1 = masked); counts (device,
+ * may be NULL) the partials' counts as int64 (the `n` of components mode). */
+enum { PYAS_FORMAT_SUM = 0, PYAS_FORMAT_MIN = 1, PYAS_FORMAT_MAX = 2, PYAS_FORMAT_MEAN = 3 };
+int pyas_format_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, int64_t n,
+                         int32_t method, void *values, uint8_t *mask, int64_t *counts,
+                         void *stream);
+
 /* Standalone HDF5/numcodecs byte un-shuffle (storage.py:121-122), device to
  * device; n_bytes % elementsize trailing bytes are copied through. */
 int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes,

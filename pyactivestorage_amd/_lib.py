@@ -21,6 +21,8 @@ I8, U8, I16, U16, I32, U32, I64, U64, F32, F64 = range(10)
 # mask flags
 MASK_EQ0, MASK_EQ1, MASK_GT, MASK_LT, MASK_TAB0, MASK_TAB1 = 1, 2, 4, 8, 16, 32
 COMBINE_ROUND_TO_VAR = 1
+# pyas_format_partials methods
+FORMAT_SUM, FORMAT_MIN, FORMAT_MAX, FORMAT_MEAN = range(4)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # PYAS_LIB selects an alternative build (tuning experiments only)
@@ -122,6 +124,7 @@ SIGNATURES = {
     "pyas_combine_partials": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_segments": [_vp, _i32, _vp, _vp, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_grid": [_vp, _i32, _vp, ctypes.POINTER(Grid), _u32, _vp, _vp],
+    "pyas_format_partials": [_vp, _i32, _vp, _i64, _i32, _vp, _vp, _vp, _vp],
     "pyas_unshuffle": [_vp, _vp, _vp, _i64, _i32, _vp],
     "pyas_inflate": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "pyas_read_ranges": [_vp, ctypes.c_int, _i64, _vp, _vp, _vp, _vp, _i32, _vp],

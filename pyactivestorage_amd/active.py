@@ -450,8 +450,11 @@ class Active:
                 plan.launch(st, chunk_partials=False)
                 final = plan.read_total(st)
             else:
-                final = self._grid_partials(ctx, st, plan, self._grid_from_dims(dims, axes, final_shape),
-                                            axes, final_shape, lo, hi)
+                grid = self._grid_from_dims(dims, axes, final_shape)
+                if self.group is None:   # one process: format on the device
+                    return self._grid_partials(ctx, st, plan, grid, axes, final_shape, lo, hi,
+                                               formatted=True)
+                final = self._grid_partials(ctx, st, plan, grid, axes, final_shape, lo, hi)
         else:
             final = np.zeros(n_final, dtype=pdt)   # count 0: neutral in every combine
         if self.group is not None:
@@ -494,14 +497,15 @@ class Active:
 
     def _grid_combine(self, ctx, st, plan, grid, axes, final_shape):
         """Partial axes over a box query, every chunk local."""
-        final = self._grid_partials(ctx, st, plan, grid, axes, final_shape, 0, plan.n_chunks)
-        return self._format(final.reshape(final_shape), final_shape)
+        return self._grid_partials(ctx, st, plan, grid, axes, final_shape, 0, plan.n_chunks,
+                                   formatted=True)
 
-    def _grid_partials(self, ctx, st, plan, grid, axes, final_shape, lo, hi):
+    def _grid_partials(self, ctx, st, plan, grid, axes, final_shape, lo, hi, formatted=False):
         """Per-chunk partial arrays of chunks [lo, hi) of the box query
         (pyas_reduce_axes over ``plan``), then pyas_combine_grid into the
         final grid; chunks outside [lo, hi) read a zeroed (count 0, neutral)
-        partial region."""
+        partial region.  ``formatted``: return the formatted result
+        (``_format_device``) instead of the host partials."""
         ds = self.ds
         dt = ds.dtype
         n_final = int(np.prod(final_shape))
@@ -544,10 +548,37 @@ class Active:
         fin = DeviceBuffer(ctx, max(n_final, 1) * _lib.PARTIAL_NBYTES)
         engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st)
         engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st)
+        if formatted:
+            return self._format_device(ctx, st, fin, n_final, final_shape)
         final = np.zeros(n_final, dtype=engine.partial_dtype(dt))
         ctx.d2h(final, fin.ptr, st)
         ctx.synchronize(st)
         return final
+
+    def _format_device(self, ctx, st, fin, n, shape):
+        """``_format`` on the device (pyas_format_partials): only the
+        result's values, mask (and counts in components mode) come back."""
+        dt = self.ds.dtype
+        method = "sum" if (self._components and self._method == "mean") else self._method
+        vdt = engine.format_dtype(dt, method)
+        vbuf = DeviceBuffer(ctx, max(n, 1) * vdt.itemsize)
+        mbuf = DeviceBuffer(ctx, max(n, 1))
+        cbuf = DeviceBuffer(ctx, max(n, 1) * 8) if self._components else None
+        engine.format_partials(ctx, dt, fin.ptr, n, method, vbuf.ptr, mbuf.ptr,
+                               cbuf.ptr if cbuf is not None else None, st)
+        vals = np.empty(n, dtype=vdt)
+        mask = np.empty(n, dtype=np.bool_)
+        ctx.d2h(vals, vbuf.ptr, st)
+        ctx.d2h(mask, mbuf.ptr, st)
+        if cbuf is not None:
+            cnt = np.empty(n, dtype=np.int64)
+            ctx.d2h(cnt, cbuf.ptr, st)
+        ctx.synchronize(st)
+        out = np.ma.MaskedArray(vals.reshape(shape), mask=mask.reshape(shape))
+        if self._components:
+            nn = np.ma.MaskedArray(cnt.reshape(shape), mask=np.zeros(shape, dtype=bool))
+            return {method: out, "n": nn}
+        return out
 
     def _reduce_general(self, indexer, compressor, filters, axes):
         """Per-chunk selection objects and host-built segments: integer-

@@ -689,6 +689,22 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, cons
     return PYAS_OK;
 }
 
+int pyas_format_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, int64_t n,
+                         int32_t method, void *values, uint8_t *mask, int64_t *counts,
+                         void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (elem_size(dtype) == 0) return fail(PYAS_ENOTSUP, "unsupported dtype code %d", dtype);
+    if (method < PYAS_FORMAT_SUM || method > PYAS_FORMAT_MEAN)
+        return fail(PYAS_EINVAL, "unknown format method %d", method);
+    if (n < 0) return fail(PYAS_EINVAL, "negative partial count");
+    if (n == 0) return PYAS_OK;
+    if (n >= (int64_t(1) << 40)) return fail(PYAS_ENOTSUP, "too many partials");
+    if (!in || !values || !mask) return fail(PYAS_EINVAL, "NULL argument");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(pyas::launch_format(dtype, in, n, method, values, mask, counts, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
 int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes, int32_t elementsize,
                    void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");

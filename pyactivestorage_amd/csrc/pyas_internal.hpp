@@ -116,6 +116,9 @@ template <typename T>
 hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
 template <typename T>
 hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st);
+template <typename T>
+hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, void *values,
+                           uint8_t *mask, int64_t *counts, hipStream_t st);
 
 // dtype dispatch (pyas_kernels.hip)
 hipError_t launch_reduce(int dtype, const ReduceArgs &a, bool shuf, bool bsw, bool masked,
@@ -133,6 +136,8 @@ hipError_t launch_combine_grid(int dtype, const pyas_partial *in, const pyas_gri
 hipError_t launch_axes_dense(int dtype, const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
 hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
+hipError_t launch_format(int dtype, const pyas_partial *in, int64_t n, int32_t method, void *values,
+                         uint8_t *mask, int64_t *counts, hipStream_t st);
 // host ingest (pyas_ingest.hip): pread ring -> pinned slots -> H2D
 struct Ingest;
 Ingest *ingest_create(int device);

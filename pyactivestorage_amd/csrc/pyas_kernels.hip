@@ -84,6 +84,12 @@ hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_format(int dtype, const pyas_partial *in, int64_t n, int32_t method, void *values,
+                         uint8_t *mask, int64_t *counts, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_format_t<T>(in, n, method, values, mask, counts, st));
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es, hipStream_t st) {
     int64_t blocks = (nbytes + kBlock - 1) / kBlock;
     if (blocks > 4096) blocks = 4096;

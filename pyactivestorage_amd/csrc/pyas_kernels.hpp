@@ -1383,6 +1383,76 @@ hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// result formatting (pyas_format_partials): active.py:591-630 on the device
+// ---------------------------------------------------------------------------
+// One thread per combined partial.  values receives what Active._format puts
+// in the masked result, mask one byte per element (1 = masked):
+//   M_SUM  : the sum in the variable dtype (floats) or int64/uint64 (ints);
+//   M_MIN/M_MAX: the value in the variable dtype;
+//   M_MEAN : np.ma's `out / n` (_DomainedBinaryOperation with
+//            _DomainSafeDivide): r = f64(out) / f64(n); masked where n == 0,
+//            r is not finite, or |out| * finfo(float).tiny >= |n|; a masked
+//            element holds 0.0 + f64(out) (np.copyto 0, then += m * out).
+template <typename T, int M>
+__global__ __launch_bounds__(kBlock) void k_format(const pyas_partial *in, int64_t n, void *values,
+                                                   uint8_t *mask, int64_t *counts) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    using S = typename std::conditional<TT<T>::kind == 0, T,
+              typename std::conditional<TT<T>::kind == 1, int64_t, uint64_t>::type>::type;
+    const pyas_partial p = in[i];
+    const int64_t cnt = p.count;
+    if (counts) counts[i] = cnt;
+    bool m = cnt == 0;
+    if constexpr (M == PYAS_FORMAT_MIN || M == PYAS_FORMAT_MAX) {
+        static_cast<T *>(values)[i] = TT<T>::from(M == PYAS_FORMAT_MIN ? p.min : p.max);
+    } else {
+        S v;
+        if constexpr (TT<T>::kind == 0) v = (T)p.sum.f;
+        else if constexpr (TT<T>::kind == 1) v = p.sum.i;
+        else v = p.sum.u;
+        if constexpr (M == PYAS_FORMAT_SUM) {
+            static_cast<S *>(values)[i] = v;
+        } else {
+            const double da = (double)v;
+            double r = da / (double)cnt;
+            double av;                                   // np.absolute(out) as f64
+            if constexpr (TT<T>::kind == 0) av = __builtin_fabs(da);
+            else if constexpr (TT<T>::kind == 1) av = (double)(v < 0 ? (int64_t)(0ull - (uint64_t)v) : v);
+            else av = da;
+            const double tiny = 2.2250738585072014e-308;
+            m = m || !__builtin_isfinite(r) || av * tiny >= (double)(cnt < 0 ? -cnt : cnt);
+            if (m) r = 0.0 + da;
+            static_cast<double *>(values)[i] = r;
+        }
+    }
+    mask[i] = m ? 1 : 0;
+}
+
+template <typename T>
+hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, void *values,
+                           uint8_t *mask, int64_t *counts, hipStream_t st) {
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock)), blk(kBlock);
+    switch (method) {
+        case PYAS_FORMAT_SUM:
+            hipLaunchKernelGGL((k_format<T, PYAS_FORMAT_SUM>), grid, blk, 0, st, in, n, values, mask, counts);
+            break;
+        case PYAS_FORMAT_MIN:
+            hipLaunchKernelGGL((k_format<T, PYAS_FORMAT_MIN>), grid, blk, 0, st, in, n, values, mask, counts);
+            break;
+        case PYAS_FORMAT_MAX:
+            hipLaunchKernelGGL((k_format<T, PYAS_FORMAT_MAX>), grid, blk, 0, st, in, n, values, mask, counts);
+            break;
+        case PYAS_FORMAT_MEAN:
+            hipLaunchKernelGGL((k_format<T, PYAS_FORMAT_MEAN>), grid, blk, 0, st, in, n, values, mask, counts);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 // Explicit instantiation of every launcher for one dtype (pyas_inst.hip).
 #define PYAS_INSTANTIATE_LAUNCHERS(T)                                                          \
     template hipError_t launch_reduce_t<T>(const ReduceArgs &, bool, bool, bool, int64_t,     \
@@ -1398,6 +1468,8 @@ hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st) {
                                                  int64_t, int64_t, uint32_t, pyas_partial *,  \
                                                  hipStream_t);                               \
     template hipError_t launch_axes_dense_t<T>(const AxesArgs &, bool, int64_t, hipStream_t); \
-    template hipError_t launch_select_t<T>(const SelectArgs &, int64_t, hipStream_t);
+    template hipError_t launch_select_t<T>(const SelectArgs &, int64_t, hipStream_t);         \
+    template hipError_t launch_format_t<T>(const pyas_partial *, int64_t, int32_t, void *,    \
+                                           uint8_t *, int64_t *, hipStream_t);
 
 }  // namespace pyas

@@ -13,7 +13,7 @@ import numpy as np
 
 from . import _lib
 from .device import Context, DeviceBuffer
-from .dtypes import dtype_code, native, needs_byteswap, value_class
+from .dtypes import dtype_code, native, needs_byteswap, sum_dtype, value_class
 from .masking import CompiledMask, table_layout
 
 _CLASS_DT = {"f": "<f8", "i": "<i8", "u": "<u8"}
@@ -125,6 +125,27 @@ def combine_grid(ctx: Context, dt, in_ptr, grid: _lib.Grid, out_ptr, round_to_va
     flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
     _lib.check(ctx.lib.pyas_combine_grid(ctx.handle, dtype_code(dt), in_ptr, ctypes.byref(grid), flags,
                                          out_ptr, stream), "pyas_combine_grid")
+
+
+_FORMAT = {"sum": _lib.FORMAT_SUM, "min": _lib.FORMAT_MIN, "max": _lib.FORMAT_MAX,
+           "mean": _lib.FORMAT_MEAN}
+
+
+def format_dtype(dt, method: str) -> np.dtype:
+    """Element type pyas_format_partials writes for ``method``."""
+    if method == "mean":
+        return np.dtype(np.float64)
+    if method == "sum":
+        return native(dt) if np.dtype(dt).kind == "f" else sum_dtype(dt)
+    return native(dt)
+
+
+def format_partials(ctx: Context, dt, in_ptr, n, method: str, values_ptr, mask_ptr, counts_ptr,
+                    stream) -> None:
+    """Device form of ``Active._format`` (active.py:591-630) over n partials."""
+    _lib.check(ctx.lib.pyas_format_partials(ctx.handle, dtype_code(dt), in_ptr, int(n), _FORMAT[method],
+                                            values_ptr, mask_ptr, counts_ptr, stream),
+               "pyas_format_partials")
 
 
 def unshuffle(ctx: Context, src_ptr, dst_ptr, nbytes, elementsize, stream) -> None:

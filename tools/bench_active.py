@@ -25,10 +25,12 @@ def main():
     ap.add_argument("--zlib", action="store_true",
                     help="chunks HDF5-shuffled + deflated (level 4, as test1.nc): 32 distinct "
                          "compressed chunks repeated over the variable (rows f2+f3 end to end)")
-    ap.add_argument("--axes", default="all", help="'all' or 'none' (full reduction only)")
+    ap.add_argument("--axes", default="all", help="'all', 'none' (full reduction only) or one axis tuple such as '0' or '1,2'")
     ap.add_argument("--resident", action="store_true",
                     help="Active(resident=True): chunks stay in HBM; the timed queries repeat a "
                          "query whose chunks the warm-up already loaded")
+    ap.add_argument("--profile", action="store_true",
+                    help="cProfile three more queries per axis; print the top host functions")
     a = ap.parse_args()
     import torch
     from pyactivestorage_amd.active import Active
@@ -71,6 +73,8 @@ def main():
                               chunk_index=index, attrs=attrs, filename=path, filter_pipeline=filters)
         nbytes = n ** 3 * 4
         axes_list = (None,) if a.axes == "none" else (None, (0,), (1,), (2,), (0, 1), (1, 2), (0, 2))
+        if a.axes not in ("all", "none"):     # one axis tuple, e.g. "0" or "1,2"
+            axes_list = (tuple(int(x) for x in a.axes.split(",")),)
         for axis in axes_list:
             act = Active(var, resident=a.resident)
             act.mean(axis=axis)
@@ -85,6 +89,16 @@ def main():
             res[str(axis)] = {"s": round(t, 4), "GBps_file_to_result": round(nbytes / t / 1e9, 2),
                               "result_shape": list(np.shape(r))}
             print(json.dumps({str(axis): res[str(axis)]}), flush=True)
+            if a.profile:
+                import cProfile
+                import pstats
+                pr = cProfile.Profile()
+                pr.enable()
+                for _ in range(3):
+                    act.mean(axis=axis)
+                    act[...]
+                pr.disable()
+                pstats.Stats(pr).sort_stats("tottime").print_stats(14)
     finally:
         if os.path.exists(path):
             os.unlink(path)
