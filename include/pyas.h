@@ -165,6 +165,10 @@ int pyas_ctx_set_inflate_window_bits(pyas_ctx *ctx, int32_t wbits);
  * in group order); 0: the total is folded by a second launch.  Results are
  * bit-identical either way. */
 int pyas_ctx_set_chained_combine(pyas_ctx *ctx, int32_t on);
+/* pyas_reduce_axes_grid launches n_cols x (workgroups per column); it splits
+ * the reduced rows further until the launch has >= n workgroups, and refuses
+ * (PYAS_ENOTSUP, two-step path) below n / 4.  0 restores the default 2048. */
+int pyas_ctx_set_fold_min_blocks(pyas_ctx *ctx, int64_t n);
 
 /* ---- memory helpers (so a non-torch host can drive the ABI) ------------- */
 int pyas_malloc(pyas_ctx *ctx, size_t nbytes, void **dptr);
@@ -266,6 +270,22 @@ typedef struct {
 int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
                       const pyas_grid *grid, uint32_t combine_flags, pyas_partial *out,
                       void *stream);
+
+/* pyas_reduce_axes + pyas_combine_grid in ONE launch, for a box query whose
+ * chunks are all whole (batch->sel == NULL) and laid out in the grid's C
+ * order (chunk n = grid position n, prod n_coords chunks), each kept dim's
+ * final extent being n_coords x the chunk extent.  The chunk layers along the
+ * reduced dims are folded inside the reduction kernel, in the same order and
+ * with the same rounding as pyas_combine_grid, so `out` (device, one partial
+ * per final element) is bit-identical to the two-step result while the
+ * per-chunk partial arrays are never written.  Only grid->ndim, axes_mask,
+ * n_coords and out_extent are read.  Returns PYAS_ENOTSUP (nothing launched)
+ * when the geometry does not admit it (element size < 4 bytes, shuffled
+ * bytes, vector mask tables, or a reduced innermost dim): the caller then
+ * takes the two-step path. */
+int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                          const pyas_grid *grid, uint32_t combine_flags, pyas_partial *out,
+                          void *stream);
 
 /* Result formatting on the device: the last step of Active._from_storage
  * (active.py:591-630) applied to n combined partials (device), so that only

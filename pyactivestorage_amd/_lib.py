@@ -108,6 +108,7 @@ SIGNATURES = {
     "pyas_ctx_set_tile_bytes": [_vp, _i64],
     "pyas_ctx_set_inflate_window_bits": [_vp, _i32],
     "pyas_ctx_set_chained_combine": [_vp, _i32],
+    "pyas_ctx_set_fold_min_blocks": [_vp, _i64],
     "pyas_malloc": [_vp, _sz, ctypes.POINTER(_vp)],
     "pyas_free": [_vp, _vp],
     "pyas_memcpy_h2d": [_vp, _vp, _vp, _sz, _vp],
@@ -124,6 +125,8 @@ SIGNATURES = {
     "pyas_combine_partials": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_segments": [_vp, _i32, _vp, _vp, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_grid": [_vp, _i32, _vp, ctypes.POINTER(Grid), _u32, _vp, _vp],
+    "pyas_reduce_axes_grid": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(Grid), _u32,
+                              _vp, _vp],
     "pyas_format_partials": [_vp, _i32, _vp, _i64, _i32, _vp, _vp, _vp, _vp],
     "pyas_unshuffle": [_vp, _vp, _vp, _i64, _i32, _vp],
     "pyas_inflate": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],

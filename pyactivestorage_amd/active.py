@@ -48,6 +48,11 @@ _ALIGN = 256
 _RESIDENT_LOCK = threading.Lock()
 
 
+# PYAS_AXES_FOLD=0 keeps whole-chunk box queries on the two-step path
+# (pyas_reduce_axes + pyas_combine_grid), for A/B measurements
+_AXES_FOLD = os.environ.get("PYAS_AXES_FOLD", "1") != "0"
+
+
 def release_resident(variable) -> None:
     """Free the HBM copy that resident-mode ``Active`` queries keep for
     ``variable`` (e.g. after the file changed)."""
@@ -540,20 +545,46 @@ class Active:
                 g.pos_local[d] = tbuf.ptr + 4 * tables["pos_local"][d]
                 g.coord_count[d] = tbuf.ptr + 4 * tables["coord_count"][d]
         g.chunk_out_offsets = abuf.ptr
-        n_parts = top - base
-        parts = DeviceBuffer(ctx, max(n_parts + neutral, 1) * _lib.PARTIAL_NBYTES)
-        if neutral:
-            zeros = np.zeros(neutral * _lib.PARTIAL_NBYTES, dtype=np.uint8)
-            ctx.h2d(parts.ptr + n_parts * _lib.PARTIAL_NBYTES, zeros, st)
         fin = DeviceBuffer(ctx, max(n_final, 1) * _lib.PARTIAL_NBYTES)
-        engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st)
-        engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st)
+        folded = False
+        if (_AXES_FOLD and lo == 0 and hi == n_all and not plan.batch.sel
+                and self._whole_chunk_grid(tables, final_shape, axes)):
+            try:   # one launch: chunk layers folded inside the reduction kernel
+                engine.reduce_axes_grid(ctx, plan.batch, plan.mask_up.struct, g, fin.ptr, True, st)
+                folded = True
+            except NotImplementedError:
+                pass   # geometry without the dense column layout: two steps
+        if not folded:
+            n_parts = top - base
+            parts = DeviceBuffer(ctx, max(n_parts + neutral, 1) * _lib.PARTIAL_NBYTES)
+            if neutral:
+                zeros = np.zeros(neutral * _lib.PARTIAL_NBYTES, dtype=np.uint8)
+                ctx.h2d(parts.ptr + n_parts * _lib.PARTIAL_NBYTES, zeros, st)
+            engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st)
+            engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st)
         if formatted:
             return self._format_device(ctx, st, fin, n_final, final_shape)
         final = np.zeros(n_final, dtype=engine.partial_dtype(dt))
         ctx.d2h(final, fin.ptr, st)
         ctx.synchronize(st)
         return final
+
+    def _whole_chunk_grid(self, tables, final_shape, axes):
+        """Every kept dim's output positions are whole chunks in coordinate
+        order (position p -> coordinate p // chunk, local p % chunk), as
+        pyas_reduce_axes_grid assumes."""
+        blob = tables["blob"]
+        for d, c in enumerate(self.ds.chunks):
+            if d in axes:
+                continue
+            F = final_shape[d]
+            if F != tables["n_coords"][d] * c:
+                return False
+            p = np.arange(F, dtype=np.int32)
+            pc, pl = tables["pos_coord"][d], tables["pos_local"][d]
+            if not (np.array_equal(blob[pc:pc + F], p // c) and np.array_equal(blob[pl:pl + F], p % c)):
+                return False
+        return True
 
     def _format_device(self, ctx, st, fin, n, shape):
         """``_format`` on the device (pyas_format_partials): only the

@@ -70,6 +70,7 @@ struct pyas_ctx {
     int64_t tile_bytes = kDefaultTileBytes;
     int32_t inflate_wbits = 13;   // LDS history ring of pyas_inflate: 2^13 B per stream
     bool chained = true;          // k_finish folds the total itself (arrival counter)
+    int64_t fold_min_blocks = 2048;   // pyas_reduce_axes_grid: fewest workgroups worth folding
     pyas::Ingest *ingest = nullptr;   // pinned staging ring of pyas_read_ranges (lazy)
     std::mutex mu;
     std::unordered_map<void *, Scratch> scratch;  // keyed by stream
@@ -284,6 +285,13 @@ int pyas_read_ranges(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offse
     const int rc = pyas::ingest_read(ingest_of(ctx), fd, n, file_offsets, sizes, (uint8_t *)dst,
                                      dst_offsets, threads, (hipStream_t)stream, msg);
     return rc ? fail(rc, "%s", msg.c_str()) : PYAS_OK;
+}
+
+int pyas_ctx_set_fold_min_blocks(pyas_ctx *ctx, int64_t n) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (n < 0) return fail(PYAS_EINVAL, "fold_min_blocks < 0");
+    ctx->fold_min_blocks = n == 0 ? 2048 : n;
+    return PYAS_OK;
 }
 
 int pyas_ctx_set_chained_combine(pyas_ctx *ctx, int32_t on) {
@@ -569,6 +577,77 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *ma
         if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
         PYAS_HIP(pyas::launch_reduce_axes(batch->dtype, x, grid, (hipStream_t)stream));
     }
+    return PYAS_OK;
+}
+
+int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                          const pyas_grid *g, uint32_t combine_flags, pyas_partial *out,
+                          void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!g || !out) return fail(PYAS_EINVAL, "NULL argument");
+    pyas::AxesArgs x;
+    std::memset(&x, 0, sizeof(x));
+    int es;
+    bool shuf, bsw, masked;
+    int rc = prepare(ctx, batch, mask, x.r, es, shuf, bsw, masked);
+    if (rc) return rc;
+    if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
+        return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
+    if (g->ndim != batch->ndim) return fail(PYAS_EINVAL, "grid rank %d != batch rank %d", g->ndim, batch->ndim);
+    const uint32_t axes_mask = g->axes_mask;
+    if (axes_mask == 0 || (axes_mask >> batch->ndim))
+        return fail(PYAS_EINVAL, "axes mask 0x%x for rank %d", axes_mask, batch->ndim);
+    if (batch->sel) return fail(PYAS_ENOTSUP, "the in-kernel layer fold needs whole chunks (sel == NULL)");
+    pyas::FoldGrid fg;
+    std::memset(&fg, 0, sizeof(fg));
+    int64_t n_pos = 1, ost = 1;
+    fg.n_layers = 1;
+    fg.n_cols = 1;
+    for (int d = batch->ndim - 1; d >= 0; --d) {
+        if (g->n_coords[d] < 1) return fail(PYAS_EINVAL, "n_coords[%d] = %lld", d, (long long)g->n_coords[d]);
+        fg.n_coords[d] = g->n_coords[d];
+        n_pos *= g->n_coords[d];
+        if ((axes_mask >> d) & 1u) {
+            fg.n_layers *= g->n_coords[d];
+        } else {
+            if (g->out_extent[d] != g->n_coords[d] * batch->chunk_shape[d])
+                return fail(PYAS_EINVAL, "out_extent[%d] = %lld is not n_coords x chunk extent", d,
+                            (long long)g->out_extent[d]);
+            fg.n_cols *= g->n_coords[d];
+            fg.ostride[d] = ost;
+            ost *= g->out_extent[d];
+        }
+    }
+    if (n_pos != batch->n_chunks)
+        return fail(PYAS_EINVAL, "%lld chunks for a grid of %lld", (long long)batch->n_chunks, (long long)n_pos);
+    fg.flags = combine_flags;
+    dense_geometry(x.d, batch, axes_mask, es, shuf || x.r.tab.on[0] || x.r.tab.on[1]);
+    if (x.d.mode != 1 || es < 4)
+        return fail(PYAS_ENOTSUP, "the in-kernel layer fold needs the dense column layout");
+    // Each workgroup walks every layer of its column, so the grid is only
+    // n_cols x bpc: trade items per pass for splits of the reduced rows
+    // until the launch fills the chip (>= 8 workgroups per CU by default).
+    const int64_t min_blocks = ctx->fold_min_blocks;
+    {
+        const int64_t items = x.d.KO * (x.d.KI / (16 / es)), rows = x.d.RO * x.d.RI;
+        while (fg.n_cols * x.d.bpc < min_blocks && x.d.it > 32 && rows >= (int64_t)x.d.split * 2 * 4 &&
+               x.d.split * 2 <= pyas::kBlock / (x.d.it / 2)) {
+            x.d.it /= 2;
+            x.d.split *= 2;
+            x.d.bpc = (items + x.d.it - 1) / x.d.it;
+        }
+    }
+    if (fg.n_cols * x.d.bpc < min_blocks / 4)
+        return fail(PYAS_ENOTSUP, "in-kernel layer fold: %lld workgroups are too few to fill the device",
+                    (long long)(fg.n_cols * x.d.bpc));
+    x.axes = axes_mask;
+    x.out = out;
+    x.shuf = shuf;
+    x.bswap = bsw;
+    const int64_t grid = fg.n_cols * x.d.bpc;
+    if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(pyas::launch_axes_fold(batch->dtype, x, fg, masked, grid, (hipStream_t)stream));
     return PYAS_OK;
 }
 

@@ -69,6 +69,15 @@ struct AxesArgs {
     bool vec;                         // geometry admits 16-B vector walks (kernel re-checks per chunk)
 };
 
+// pyas_reduce_axes_grid: the chunk layers of a whole-chunk box query folded
+// inside the dense column kernel (no per-chunk partial arrays)
+struct FoldGrid {
+    int64_t n_coords[PYAS_MAX_DIMS];  // chunk coordinates per dim (chunk n = C-order position)
+    int64_t ostride[PYAS_MAX_DIMS];   // final-output element strides (kept dims)
+    int64_t n_layers, n_cols;         // chunks along the reduced dims / kept dims
+    uint32_t flags;                   // PYAS_COMBINE_*
+};
+
 struct InflateArgs {
     const uint8_t *src;
     const int64_t *src_offsets, *src_sizes;
@@ -115,6 +124,9 @@ hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int
 template <typename T>
 hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
 template <typename T>
+hipError_t launch_axes_fold_t(const AxesArgs &a, const FoldGrid &g, bool masked, int64_t grid,
+                              hipStream_t st);
+template <typename T>
 hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st);
 template <typename T>
 hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, void *values,
@@ -134,6 +146,8 @@ hipError_t launch_combine_grid(int dtype, const pyas_partial *in, const pyas_gri
                                int64_t n_out, int64_t n_layers, uint32_t flags,
                                pyas_partial *out, hipStream_t st);
 hipError_t launch_axes_dense(int dtype, const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
+hipError_t launch_axes_fold(int dtype, const AxesArgs &a, const FoldGrid &g, bool masked, int64_t grid,
+                            hipStream_t st);
 hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
 hipError_t launch_format(int dtype, const pyas_partial *in, int64_t n, int32_t method, void *values,

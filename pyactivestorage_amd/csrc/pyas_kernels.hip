@@ -79,6 +79,12 @@ hipError_t launch_axes_dense(int dtype, const AxesArgs &a, bool masked, int64_t 
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_axes_fold(int dtype, const AxesArgs &a, const FoldGrid &g, bool masked, int64_t grid,
+                            hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_axes_fold_t<T>(a, g, masked, grid, st));
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st) {
     PYAS_DISPATCH_T(dtype, return launch_select_t<T>(a, grid, st));
     return hipErrorInvalidValue;

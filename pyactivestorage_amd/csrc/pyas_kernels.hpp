@@ -994,6 +994,51 @@ __device__ __forceinline__ void store_group(const TileAcc<T> &a, uint32_t cnt, u
 #define PYAS_DENSE_ATTR
 #endif
 
+// One pass of the column layout over one chunk: lane (il, sp) folds split
+// sp of the reduced rows of vector item i (N consecutive kept outputs) into
+// acc[N], PYAS_COL_U 16-B loads in flight.
+template <typename T, bool BSWAP, int MASKED, bool AL>
+__device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base, int64_t i, int sp,
+                                         const MaskT<T> &mk, TileAcc<T> *acc) {
+    constexpr int ES = sizeof(T), N = 16 / ES;
+    const int S = d.split;
+    const int64_t KIV = d.KI / N, R = d.RO * d.RI;
+    const int64_t sRO = d.KO * d.RI * d.KI;                    // elements per ro step
+    const int64_t dq = S / d.RI, dr = S - dq * d.RI;            // row step S = dq*RI + dr
+    const int64_t step_off = (dq * sRO + dr * d.KI) * ES;       // bytes
+    const int64_t wrap_off = (sRO - d.RI * d.KI) * ES;          // ri wrapped past RI
+    const int64_t ko = i / KIV, v = i - ko * KIV;
+    int64_t ro = sp / d.RI, ri = sp - ro * d.RI;
+    const uint8_t *p = base + ((ro * d.KO + ko) * d.RI * d.KI + ri * d.KI + v * N) * ES;
+    const int64_t nt = (R - sp + S - 1) / S;
+    auto next = [&]() {
+        p += step_off;
+        ri += dr;
+        if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
+    };
+    constexpr int U = PYAS_COL_U;
+    int64_t t = 0;
+    for (; t + U <= nt; t += U) {
+        uint4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) { w[u] = ld16<AL>(p); next(); }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            T x[N];
+            unpack16<T, BSWAP>(w[u], x);
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc[k].add_one(x[k], MASKED && mk.masked(x[k]));
+        }
+    }
+    for (; t < nt; ++t) {
+        T x[N];
+        unpack16<T, BSWAP>(ld16<AL>(p), x);
+        next();
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k].add_one(x[k], MASKED && mk.masked(x[k]));
+    }
+}
+
 template <typename T, bool BSWAP, int MASKED, bool AL>
 __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                           const MaskT<T> &mk, uint4 *stage) {
@@ -1001,49 +1046,15 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     const AxesDense &d = a.d;
     const int IT = d.it, S = d.split;
     const int il = threadIdx.x & (IT - 1), sp = threadIdx.x / IT;
-    const int64_t KIV = d.KI / N, items = d.KO * KIV, R = d.RO * d.RI;
-    const int64_t sRO = d.KO * d.RI * d.KI;                    // elements per ro step
-    const int64_t dq = S / d.RI, dr = S - dq * d.RI;            // row step S = dq*RI + dr
-    const int64_t step_off = (dq * sRO + dr * d.KI) * ES;       // bytes
-    const int64_t wrap_off = (sRO - d.RI * d.KI) * ES;          // ri wrapped past RI
+    const int64_t items = d.KO * (d.KI / N);
     pyas_partial *out = a.out + a.out_offsets[c];
     for (int64_t i0 = j * IT; i0 < items; i0 += d.bpc * IT) {   // block-uniform
         const int64_t i = i0 + il;
         TileAcc<T> acc[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) acc[k].init();
-        if (i < items && sp < S && sp < R) {
-            const int64_t ko = i / KIV, v = i - ko * KIV;
-            int64_t ro = sp / d.RI, ri = sp - ro * d.RI;
-            const uint8_t *p = base + ((ro * d.KO + ko) * d.RI * d.KI + ri * d.KI + v * N) * ES;
-            const int64_t nt = (R - sp + S - 1) / S;
-            auto next = [&]() {
-                p += step_off;
-                ri += dr;
-                if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
-            };
-            constexpr int U = PYAS_COL_U;
-            int64_t t = 0;
-            for (; t + U <= nt; t += U) {
-                uint4 w[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) { w[u] = ld16<AL>(p); next(); }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    T x[N];
-                    unpack16<T, BSWAP>(w[u], x);
-#pragma unroll
-                    for (int k = 0; k < N; ++k) acc[k].add_one(x[k], MASKED && mk.masked(x[k]));
-                }
-            }
-            for (; t < nt; ++t) {
-                T x[N];
-                unpack16<T, BSWAP>(ld16<AL>(p), x);
-                next();
-#pragma unroll
-                for (int k = 0; k < N; ++k) acc[k].add_one(x[k], MASKED && mk.masked(x[k]));
-            }
-        }
+        if (i < items && sp < S && sp < d.RO * d.RI)
+            col_rows<T, BSWAP, MASKED, AL>(d, base, i, sp, mk, acc);
         if constexpr (N <= 4) {
             // Stage the pass's IT*N partials (<= 32 KiB) in LDS, then write
             // them as consecutive 16-B stores (a lane's own N partials are
@@ -1185,6 +1196,95 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs 
     } else {
         if (al) dense_row<T, BSWAP, MASKED, true, 4>(a, c, j, base, mk);
         else dense_row<T, BSWAP, MASKED, false, 4>(a, c, j, base, mk);
+    }
+}
+
+// Whole-chunk box query, column layout, chunk layers folded in the kernel
+// (pyas_reduce_axes_grid).  Block (col, j) owns the kept-dims chunk column
+// `col` and items j, j + bpc, ... of it; for each layer (the column's chunks
+// along the reduced dims, in C order) it runs dense_col's pass and merges
+// the per-chunk partial (tile_store_lane, then k_combine_grid's merge with
+// the same rounding) into a running WAcc per output.  The arithmetic is
+// k_axes_dense + k_combine_grid's, operation for operation, so the result is
+// bit-identical; the per-chunk partial arrays are never written.
+template <typename T, bool BSWAP, int MASKED>
+__global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold(AxesArgs a, FoldGrid g) {
+    constexpr int N = 16 / sizeof(T);
+    const AxesDense &d = a.d;
+    const ReduceArgs &r = a.r;
+    const int64_t col = blockIdx.x / d.bpc;
+    const int64_t j = blockIdx.x - col * d.bpc;
+    const uint32_t red = a.axes;
+    int64_t ac[PYAS_MAX_DIMS], gstride[PYAS_MAX_DIMS];
+    int64_t rest = col, st = 1, nk = 0;
+#pragma unroll
+    for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+        ac[dd] = 0;
+        gstride[dd] = st;
+        if (dd < r.ndim) {
+            st *= g.n_coords[dd];
+            if (!((red >> dd) & 1u)) {
+                const int64_t q = rest / g.n_coords[dd];
+                ac[dd] = rest - q * g.n_coords[dd];
+                rest = q;
+                nk += ac[dd] * gstride[dd];
+            }
+        }
+    }
+    MaskT<T> mk;
+    mk.init(r.mask);
+    const int IT = d.it, S = d.split;
+    const int il = threadIdx.x & (IT - 1), sp = threadIdx.x / IT;
+    const int64_t items = d.KO * (d.KI / N);
+    const bool round = (g.flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
+    for (int64_t i0 = j * IT; i0 < items; i0 += d.bpc * IT) {   // block-uniform
+        const int64_t i = i0 + il;
+        WAcc<T> w[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) w[k].init();
+        for (int64_t l = 0; l < g.n_layers; ++l) {
+            int64_t n = nk, rr = l;
+#pragma unroll
+            for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+                if (dd < r.ndim && ((red >> dd) & 1u)) {
+                    const int64_t q = rr / g.n_coords[dd];
+                    n += (rr - q * g.n_coords[dd]) * gstride[dd];
+                    rr = q;
+                }
+            }
+            const uint8_t *base = r.data + r.offsets[n];
+            TileAcc<T> acc[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc[k].init();
+            if (i < items && sp < S && sp < d.RO * d.RI) {
+                if (((uintptr_t)base & 15) == 0) col_rows<T, BSWAP, MASKED, true>(d, base, i, sp, mk, acc);
+                else col_rows<T, BSWAP, MASKED, false>(d, base, i, sp, mk, acc);
+            }
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                if (S > 1) fold_splits(acc[k], S, IT, il, sp);
+                if (sp == 0) {
+                    pyas_partial pp;
+                    tile_store_lane(acc[k], &pp);
+                    merge(w[k], pp, round);
+                }
+            }
+        }
+        if (sp == 0 && i < items) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                int64_t loc = i * N + k, f = 0;   // kept-dims index in the chunk -> final element
+#pragma unroll
+                for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+                    if (dd < r.ndim && !((red >> dd) & 1u)) {
+                        const int64_t q = loc / r.shape[dd];
+                        f += (ac[dd] * r.shape[dd] + (loc - q * r.shape[dd])) * g.ostride[dd];
+                        loc = q;
+                    }
+                }
+                store_wpartial(a.out + f, w[k]);
+            }
+        }
     }
 }
 
@@ -1364,6 +1464,24 @@ hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hip
 }
 
 template <typename T>
+hipError_t launch_axes_fold_t(const AxesArgs &a, const FoldGrid &g, bool masked, int64_t grid,
+                              hipStream_t st) {
+    const dim3 gr((unsigned)grid), blk(kBlock);
+    if constexpr (sizeof(T) < 4) {
+        return hipErrorInvalidValue;     // dense_geometry: >= 4-byte elements only
+    } else {
+        if (a.bswap) {
+            if (masked) hipLaunchKernelGGL((k_axes_fold<T, true, 1>), gr, blk, 0, st, a, g);
+            else hipLaunchKernelGGL((k_axes_fold<T, true, 0>), gr, blk, 0, st, a, g);
+        } else {
+            if (masked) hipLaunchKernelGGL((k_axes_fold<T, false, 1>), gr, blk, 0, st, a, g);
+            else hipLaunchKernelGGL((k_axes_fold<T, false, 0>), gr, blk, 0, st, a, g);
+        }
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
 hipError_t launch_axes_t(const AxesArgs &a, int64_t grid, hipStream_t st) {
     const dim3 g((unsigned)grid), blk(kBlock);
     if constexpr (sizeof(T) == 1) {
@@ -1468,6 +1586,8 @@ hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, vo
                                                  int64_t, int64_t, uint32_t, pyas_partial *,  \
                                                  hipStream_t);                               \
     template hipError_t launch_axes_dense_t<T>(const AxesArgs &, bool, int64_t, hipStream_t); \
+    template hipError_t launch_axes_fold_t<T>(const AxesArgs &, const FoldGrid &, bool, int64_t, \
+                                              hipStream_t);                                   \
     template hipError_t launch_select_t<T>(const SelectArgs &, int64_t, hipStream_t);         \
     template hipError_t launch_format_t<T>(const pyas_partial *, int64_t, int32_t, void *,    \
                                            uint8_t *, int64_t *, hipStream_t);

@@ -123,6 +123,10 @@ class Context:
     def set_tile_bytes(self, nbytes: int) -> None:
         _lib.check(self.lib.pyas_ctx_set_tile_bytes(self.handle, int(nbytes)), "set_tile_bytes")
 
+    def set_fold_min_blocks(self, n: int) -> None:
+        """Workgroup floor of the in-kernel layer fold (0 = default 2048)."""
+        _lib.check(self.lib.pyas_ctx_set_fold_min_blocks(self.handle, int(n)), "set_fold_min_blocks")
+
     def set_chained_combine(self, on: bool) -> None:
         """Fold tiles -> chunks -> total in the reduce kernel's tail (default)
         or in separate combine launches; results are bit-identical."""

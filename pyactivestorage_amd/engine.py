@@ -93,6 +93,16 @@ def reduce_axes(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, axes_mask: int
                "pyas_reduce_axes")
 
 
+def reduce_axes_grid(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, grid: _lib.Grid, out_ptr,
+                     round_to_var: bool, stream) -> None:
+    """pyas_reduce_axes + pyas_combine_grid in one launch (whole chunks);
+    NotImplementedError when the geometry does not admit it."""
+    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
+    _lib.check(ctx.lib.pyas_reduce_axes_grid(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
+                                             ctypes.byref(grid), flags, out_ptr, stream),
+               "pyas_reduce_axes_grid")
+
+
 def select_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, out_offsets_ptr, values_ptr,
                   mask_out_ptr, stream) -> None:
     _lib.check(ctx.lib.pyas_select_chunks(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),

@@ -1,0 +1,143 @@
+"""pyas_reduce_axes_grid (chunk layers folded inside the dense column
+kernel, one launch) against the two-step path it replaces
+(pyas_reduce_axes -> per-chunk partial arrays -> pyas_combine_grid), which
+follows ``Active._from_storage``'s combine (``activestorage/active.py:
+487-516,575-598``).  The combined partials must agree bit for bit: sums,
+counts, min/max and NaN propagation, for rounded variable-dtype sums, masked
+and unmasked variables, byte-swapped dtypes, several chunk grids and axis
+sets, with and without split reduced ranges.  The final results are also
+checked against NumPy's masked reductions of the whole array.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from pyactivestorage_amd import active as active_mod
+from pyactivestorage_amd import engine
+from pyactivestorage_amd.active import Active
+from pyactivestorage_amd.variable import ChunkedVariable
+
+pytestmark = pytest.mark.gpu
+
+FILL = -999
+
+
+@pytest.fixture(autouse=True)
+def _default_floor(gpu):
+    yield
+    gpu.set_fold_min_blocks(0)
+
+
+def _variable(shape, chunks, dtype, rng, masked, nan=False):
+    dt = np.dtype(dtype)
+    if dt.kind == "f":
+        data = rng.uniform(-100, 100, size=shape).astype(dt)
+        if nan:
+            data.reshape(-1)[rng.choice(data.size, 3, replace=False)] = np.nan
+    else:
+        data = rng.integers(-50 if dt.kind == "i" else 0, 100, size=shape).astype(dt)
+    attrs = {}
+    if masked:
+        data.reshape(-1)[rng.random(data.size) < 0.2] = FILL if dt.kind != "u" else 7
+        attrs["_FillValue"] = np.array([FILL if dt.kind != "u" else 7], dtype=dt)
+    path = os.path.join(tempfile.mkdtemp(), "v.chunks")
+    index, pos = {}, 0
+    with open(path, "wb") as fh:
+        for cc in np.ndindex(*[s // c for s, c in zip(shape, chunks)]):
+            sl = tuple(slice(i * c, (i + 1) * c) for i, c in zip(cc, chunks))
+            b = np.ascontiguousarray(data[sl]).tobytes()
+            fh.write(b)
+            index[cc] = (pos, len(b))
+            pos += len(b)
+    var = ChunkedVariable(name="v", shape=shape, chunks=chunks, dtype=dt, chunk_index=index,
+                          attrs=attrs, filename=path)
+    return var, data
+
+
+def _partials(var, axis, index, fold, monkeypatch):
+    """Combined partials of an Active mean query, raw (before formatting)."""
+    monkeypatch.setattr(active_mod, "_AXES_FOLD", fold)
+    calls = []
+    real = engine.reduce_axes_grid
+
+    def spy(*a, **k):
+        real(*a, **k)
+        calls.append(1)
+    monkeypatch.setattr(engine, "reduce_axes_grid", spy)
+    a = Active(var, axis=axis)
+    a.method = "mean"
+    got = {}
+
+    def raw(ctx, st, fin, n, shape):
+        final = np.zeros(n, dtype=engine.partial_dtype(var.dtype))
+        ctx.d2h(final, fin.ptr, st)
+        ctx.synchronize(st)
+        got["final"] = final
+        return a._format(final.reshape(shape), shape)
+    a._format_device = raw
+    res = a[index]
+    return got["final"], res, len(calls)
+
+
+CASES = [
+    # shape, chunks, axis, index
+    ((64, 48, 32), (16, 16, 16), (0,), np.s_[...]),
+    ((64, 48, 32), (16, 16, 16), (1,), np.s_[...]),
+    ((64, 48, 32), (16, 16, 16), (0, 1), np.s_[...]),
+    ((32, 32, 64), (8, 16, 64), (0,), np.s_[8:24, :, :]),
+    ((32, 32, 64), (8, 16, 64), (1,), np.s_[:, 16:32, :]),
+    ((16, 12, 20, 24), (4, 6, 5, 8), (0, 2), np.s_[...]),
+    ((16, 12, 20, 24), (4, 6, 5, 8), (1,), np.s_[4:16]),
+    ((128, 8), (32, 8), (0,), np.s_[...]),
+    ((20, 256), (5, 256), (0,), np.s_[...]),       # few outputs per chunk: split reduced rows
+    ((6, 1024, 8), (3, 128, 8), (0, 1), np.s_[...]),
+]
+
+
+@pytest.mark.parametrize("dtype", ["<f4", ">f4", "<f8", "<i4", "<u4", "<i8"])
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_fold_matches_two_step(gpu, dtype, masked, case, monkeypatch):
+    gpu.set_fold_min_blocks(1)            # small test grids: fold whatever the size
+    shape, chunks, axis, index = CASES[case]
+    rng = np.random.default_rng(case * 31 + len(dtype))
+    var, data = _variable(shape, chunks, dtype, rng, masked, nan=(case == 0))
+    f1, r1, n1 = _partials(var, axis, index, True, monkeypatch)
+    f0, r0, n0 = _partials(var, axis, index, False, monkeypatch)
+    assert n1 == 1 and n0 == 0            # the fold ran, then the two-step path
+    assert f1.tobytes() == f0.tobytes()
+    # and the result against NumPy's masked mean of the selection
+    sel = data[index]
+    m = np.ma.masked_equal(sel, var.attrs["_FillValue"][0]) if masked else np.ma.MaskedArray(sel)
+    want = np.ma.mean(m.astype(np.float64), axis=axis, keepdims=True)
+    want = np.ma.masked_invalid(want)     # np.ma's out / n (active.py:630) masks NaN means
+    np.testing.assert_array_equal(np.ma.getmaskarray(r1), np.ma.getmaskarray(want))
+    ok = ~np.ma.getmaskarray(want)
+    np.testing.assert_allclose(np.ma.getdata(r1)[ok], np.ma.getdata(want)[ok], rtol=1e-5, atol=1e-4)
+
+
+def test_fold_refuses_row_layout(gpu, monkeypatch):
+    """Innermost dim reduced: no column layout, the two-step path runs."""
+    gpu.set_fold_min_blocks(1)
+    rng = np.random.default_rng(3)
+    var, data = _variable((32, 32, 64), (8, 16, 64), "<f4", rng, True)
+    f, r, n = _partials(var, (2,), np.s_[...], True, monkeypatch)
+    assert n == 0
+    f0, r0, _ = _partials(var, (2,), np.s_[...], False, monkeypatch)
+    assert f.tobytes() == f0.tobytes()
+
+
+def test_fold_refuses_too_few_workgroups(gpu, monkeypatch):
+    """Few kept-dim columns and many layers: the fold would launch too few
+    workgroups, so the two-step path runs (same result)."""
+    gpu.set_fold_min_blocks(0)            # the default floor (2048)
+    rng = np.random.default_rng(4)
+    var, data = _variable((64, 48, 32), (16, 16, 16), "<f4", rng, True)
+    f, r, n = _partials(var, (0, 1), np.s_[...], True, monkeypatch)
+    assert n == 0
+    gpu.set_fold_min_blocks(1)
+    f1, r1, n1 = _partials(var, (0, 1), np.s_[...], True, monkeypatch)
+    assert n1 == 1 and f.tobytes() == f1.tobytes()
+    gpu.set_fold_min_blocks(0)

@@ -31,6 +31,8 @@ def main():
                          "query whose chunks the warm-up already loaded")
     ap.add_argument("--profile", action="store_true",
                     help="cProfile three more queries per axis; print the top host functions")
+    ap.add_argument("--fold-blocks", type=int, default=0,
+                    help="workgroup floor of the in-kernel layer fold (0: library default)")
     a = ap.parse_args()
     import torch
     from pyactivestorage_amd.active import Active
@@ -39,6 +41,9 @@ def main():
     n, c = a.shape, 64
     shape, chunks = (n, n, n), (c, c, c)
     dev = torch.device("cuda", 0)
+    if a.fold_blocks:
+        from pyactivestorage_amd.device import get_context
+        get_context(0).set_fold_min_blocks(a.fold_blocks)
     path = os.path.join(tempfile.gettempdir(), f"pyas_active_{os.getpid()}.chunks")
     grid = [s // k for s, k in zip(shape, chunks)]
     cb = c * c * c * 4
