@@ -486,6 +486,22 @@ static void dense_geometry(pyas::AxesDense &d, const pyas_batch *b, uint32_t axe
     } else {
         if ((d.RI * es) % 16) return;
         const int64_t V = d.RI / nv;
+        // Short single runs (RO == 1, <= 256 B): through LDS, 1, 2 or 4 lanes
+        // per output (PYAS_ROW_LDS: 0 off, else the most lanes allowed; default 2)
+        const char *e_lds = getenv("PYAS_ROW_LDS");     // per call: tests switch it
+        const int row_lds = e_lds ? atoi(e_lds) : 2;
+        const char *e_tpw = getenv("PYAS_ROW_LDS_TPW");   // tiles per wave; measured on (2,): 2 best
+        const int64_t row_tpw = e_tpw && atoi(e_tpw) > 0 ? (int64_t)atoi(e_tpw) : (int64_t)2;
+        if (row_lds && d.RO == 1 && V <= 16) {
+            int h = 1;
+            while (h < row_lds && h < 4 && V % (h * 2) == 0) h *= 2;
+            d.mode = h == 1 ? 4 : h == 2 ? 5 : 6;
+            d.group = h;
+            const int64_t per_pass = (pyas::kBlock / pyas::kWave) * (pyas::kWave / h);
+            const int64_t bpc = (d.KO + row_tpw * per_pass - 1) / (row_tpw * per_pass);   // tiles per wave
+            d.bpc = bpc < 1 ? 1 : bpc;
+            return;
+        }
         // G lanes per output: the largest power of two dividing V (<= 64)
         // that still leaves each lane >= row_vecs vectors per run
         static const int64_t row_vecs = [] {

@@ -48,7 +48,8 @@ constexpr int kAxesLds = 8192;   // reduced-index offsets kept in LDS (int32, 32
 // Dense partial-axis geometry (k_axes_dense): the chunk dims merged into
 // (RO, KO, RI, KI) = (reduced outer, kept outer, reduced inner, kept inner).
 struct AxesDense {
-    int32_t mode;                     // 0 off, 1 column, 2 row, 3 row with 4 outputs per lane
+    int32_t mode;                     // 0 off, 1 column, 2 row, 3 row with 4 outputs per lane,
+                                      // 4/5/6 row through LDS with 1/2/4 lanes per output
     int32_t it, split;                // column: items per pass (power of 2), row splits
     int32_t group;                    // row: lanes per output (power of 2)
     int64_t RO, KO, RI, KI;

@@ -1168,6 +1168,74 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     }
 }
 
+// Row layout through LDS (RO == 1, KI == 1, runs of V <= 16 16-B vectors;
+// e.g. axis (2,) of 64^3 f32): a wave loads kWave/H consecutive runs with
+// coalesced 16-B loads (1 KiB per instruction), writes them to its own LDS
+// tile (run stride V + 1 vectors: b128 reads and writes are bank-conflict
+// free), then H lanes per output fold the run from LDS.  No butterfly for
+// H == 1, log2(H) DPP steps otherwise.  The next tile's loads are issued before
+// the current tile is folded.
+constexpr int kRowLdsStride = 17;   // 16-B vectors per LDS run (V <= 16, + 1 pad)
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T, bool BSWAP, int MASKED, bool AL, int H>
+__device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
+                              const MaskT<T> &mk, uint4 *tile) {
+    constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, UL = 16 / H;
+    const AxesDense &d = a.d;
+    const int V = (int)(d.RI / N);                  // vectors per run, V % H == 0
+    const int VH = V / H;                           // vectors per lane
+    const int lane = threadIdx.x & (kWave - 1), r = lane / H, h = lane - r * H;
+    uint4 *t = tile + (threadIdx.x / kWave) * RPW * kRowLdsStride;
+    const int64_t wave = j * (kBlock / kWave) + threadIdx.x / kWave;
+    const int64_t nwaves = d.bpc * (kBlock / kWave);
+    pyas_partial *out = a.out + a.out_offsets[c];
+    // tile vector q = u * kWave + lane lands in run q / V, column q % V
+    int lrow[UL], lcol[UL];
+#pragma unroll
+    for (int u = 0; u < UL; ++u) {
+        const int q = u * kWave + lane;
+        lrow[u] = q / V;
+        lcol[u] = q - lrow[u] * V;
+    }
+    uint4 w[UL];
+    auto load = [&](int64_t o0) {
+        const int64_t nvec = (d.KO - o0 < RPW ? d.KO - o0 : RPW) * V;
+        const uint8_t *src = base + o0 * d.RI * ES;
+#pragma unroll
+        for (int u = 0; u < UL; ++u)
+            if (u * kWave + lane < nvec) w[u] = ld16<AL>(src + (int64_t)(u * kWave + lane) * 16);
+    };
+    int64_t o0 = wave * RPW;
+    if (o0 < d.KO) load(o0);
+    for (; o0 < d.KO; o0 += nwaves * RPW) {   // wave-uniform
+        const int64_t nvec = (d.KO - o0 < RPW ? d.KO - o0 : RPW) * V;
+#pragma unroll
+        for (int u = 0; u < UL; ++u)
+            if (u * kWave + lane < nvec) t[lrow[u] * kRowLdsStride + lcol[u]] = w[u];
+        wave_sync_lds();
+        if (o0 + nwaves * RPW < d.KO) load(o0 + nwaves * RPW);
+        TileAcc<T> acc;
+        acc.init();
+        const uint4 *row = t + r * kRowLdsStride + h * VH;
+        for (int i = 0; i < VH; ++i) {
+            T x[N];
+            unpack16<T, BSWAP>(row[i], x);
+            acc.template add_n<N, MASKED, false>(x, mk);
+        }
+        if constexpr (!MASKED) acc.count += (uint32_t)(VH * N);
+        uint32_t cnt, nan;
+        group_reduce(acc, H, cnt, nan);
+        if (h == 0 && o0 + r < d.KO) store_group(acc, cnt, nan, out + o0 + r);
+        wave_sync_lds();
+    }
+}
+
 // Which kernel owns chunk c: the dense one when the chunk is fully selected.
 __device__ __forceinline__ bool dense_owns(const AxesArgs &a, const Sel &s) {
     return a.d.mode != 0 && chunk_is_full(s, a.r.shape, a.r.ndim);
@@ -1190,6 +1258,11 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs 
         __shared__ uint4 stage[sizeof(T) >= 4 ? kBlock * 4 * 2 : 1];
         if (al) dense_col<T, BSWAP, MASKED, true>(a, c, j, base, mk, stage);
         else dense_col<T, BSWAP, MASKED, false>(a, c, j, base, mk, stage);
+    } else if constexpr (MODE >= 4) {
+        constexpr int H = MODE == 4 ? 1 : MODE == 5 ? 2 : 4;
+        __shared__ uint4 tile[(kBlock / kWave) * (kWave / H) * kRowLdsStride];
+        if (al) dense_row_lds<T, BSWAP, MASKED, true, H>(a, c, j, base, mk, tile);
+        else dense_row_lds<T, BSWAP, MASKED, false, H>(a, c, j, base, mk, tile);
     } else if constexpr (MODE == 2) {
         if (al) dense_row<T, BSWAP, MASKED, true, 1>(a, c, j, base, mk);
         else dense_row<T, BSWAP, MASKED, false, 1>(a, c, j, base, mk);
@@ -1459,6 +1532,9 @@ hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hip
     const dim3 g((unsigned)grid);
     if (a.d.mode == 1) launch_dense_m<T, 1>(a, masked, g, st);
     else if (a.d.mode == 2) launch_dense_m<T, 2>(a, masked, g, st);
+    else if (a.d.mode == 4) launch_dense_m<T, 4>(a, masked, g, st);
+    else if (a.d.mode == 5) launch_dense_m<T, 5>(a, masked, g, st);
+    else if (a.d.mode == 6) launch_dense_m<T, 6>(a, masked, g, st);
     else launch_dense_m<T, 3>(a, masked, g, st);
     return hipGetLastError();
 }
