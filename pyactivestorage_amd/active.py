@@ -553,7 +553,7 @@ class Active:
                 engine.reduce_axes_grid(ctx, plan.batch, plan.mask_up.struct, g, fin.ptr, True, st)
                 folded = True
             except NotImplementedError:
-                pass   # geometry without the dense column layout: two steps
+                pass   # geometry without the dense column or LDS row layout: two steps
         if not folded:
             n_parts = top - base
             parts = DeviceBuffer(ctx, max(n_parts + neutral, 1) * _lib.PARTIAL_NBYTES)

@@ -638,13 +638,16 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
         return fail(PYAS_EINVAL, "%lld chunks for a grid of %lld", (long long)batch->n_chunks, (long long)n_pos);
     fg.flags = combine_flags;
     dense_geometry(x.d, batch, axes_mask, es, shuf || x.r.tab.on[0] || x.r.tab.on[1]);
-    if (x.d.mode != 1 || es < 4)
-        return fail(PYAS_ENOTSUP, "the in-kernel layer fold needs the dense column layout");
+    if ((x.d.mode != 1 && x.d.mode < 4) || es < 4)
+        return fail(PYAS_ENOTSUP, "the in-kernel layer fold needs the dense column or LDS row layout");
     // Each workgroup walks every layer of its column, so the grid is only
     // n_cols x bpc: trade items per pass for splits of the reduced rows
     // until the launch fills the chip (>= 8 workgroups per CU by default).
     const int64_t min_blocks = ctx->fold_min_blocks;
-    {
+    if (x.d.mode >= 4) {   // LDS row layout: one output tile per wave
+        const int64_t rpw = pyas::kWave / x.d.group, per_block = (pyas::kBlock / pyas::kWave) * rpw;
+        x.d.bpc = (x.d.KO + per_block - 1) / per_block;
+    } else {
         const int64_t items = x.d.KO * (x.d.KI / (16 / es)), rows = x.d.RO * x.d.RI;
         while (fg.n_cols * x.d.bpc < min_blocks && x.d.it > 32 && rows >= (int64_t)x.d.split * 2 * 4 &&
                x.d.split * 2 <= pyas::kBlock / (x.d.it / 2)) {

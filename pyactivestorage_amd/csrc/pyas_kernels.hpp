@@ -1361,6 +1361,123 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold(AxesArgs a
     }
 }
 
+// Whole-chunk box query, LDS row layout (modes 4/5/6), chunk layers folded
+// in the kernel (pyas_reduce_axes_grid).  Block (col, j), wave w owns the
+// output tiles j*4 + w, + 4*bpc, ... of kept-dims chunk column `col`; for
+// each layer (the column's chunks along the reduced dims, in C order) it
+// stages the layer chunk's runs through LDS and folds them as dense_row_lds
+// does, then merges the partial store_group would write into a running WAcc
+// (k_combine_grid's merge, same rounding).  Bit-identical to k_axes_dense +
+// k_combine_grid; the next layer's tile is loaded while this one is folded.
+template <typename T, bool BSWAP, int MASKED, int H>
+__global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold_row(AxesArgs a, FoldGrid g) {
+    constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, UL = 16 / H;
+    __shared__ uint4 tile[(kBlock / kWave) * RPW * kRowLdsStride];
+    const AxesDense &d = a.d;
+    const ReduceArgs &r = a.r;
+    const int64_t col = blockIdx.x / d.bpc;
+    const int64_t j = blockIdx.x - col * d.bpc;
+    const uint32_t red = a.axes;
+    int64_t ac[PYAS_MAX_DIMS], gstride[PYAS_MAX_DIMS];
+    int64_t rest = col, st = 1, nk = 0;
+#pragma unroll
+    for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+        ac[dd] = 0;
+        gstride[dd] = st;
+        if (dd < r.ndim) {
+            st *= g.n_coords[dd];
+            if (!((red >> dd) & 1u)) {
+                const int64_t q = rest / g.n_coords[dd];
+                ac[dd] = rest - q * g.n_coords[dd];
+                rest = q;
+                nk += ac[dd] * gstride[dd];
+            }
+        }
+    }
+    auto layer_base = [&](int64_t l) {
+        int64_t n = nk, rr = l;
+#pragma unroll
+        for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+            if (dd < r.ndim && ((red >> dd) & 1u)) {
+                const int64_t q = rr / g.n_coords[dd];
+                n += (rr - q * g.n_coords[dd]) * gstride[dd];
+                rr = q;
+            }
+        }
+        return r.data + r.offsets[n];
+    };
+    MaskT<T> mk;
+    mk.init(r.mask);
+    const bool round = (g.flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
+    const int V = (int)(d.RI / N), VH = V / H;
+    const int lane = threadIdx.x & (kWave - 1), rw = lane / H, h = lane - rw * H;
+    uint4 *t = tile + (threadIdx.x / kWave) * RPW * kRowLdsStride;
+    const int64_t wave = j * (kBlock / kWave) + threadIdx.x / kWave;
+    const int64_t nwaves = d.bpc * (kBlock / kWave);
+    int lrow[UL], lcol[UL];
+#pragma unroll
+    for (int u = 0; u < UL; ++u) {
+        const int q = u * kWave + lane;
+        lrow[u] = q / V;
+        lcol[u] = q - lrow[u] * V;
+    }
+    uint4 w[UL];
+    auto load = [&](const uint8_t *base, int64_t o0, int64_t nvec) {
+        const uint8_t *src = base + o0 * d.RI * ES;
+        if (((uintptr_t)src & 15) == 0) {
+#pragma unroll
+            for (int u = 0; u < UL; ++u)
+                if (u * kWave + lane < nvec) w[u] = ld16<true>(src + (int64_t)(u * kWave + lane) * 16);
+        } else {
+#pragma unroll
+            for (int u = 0; u < UL; ++u)
+                if (u * kWave + lane < nvec) w[u] = ld16<false>(src + (int64_t)(u * kWave + lane) * 16);
+        }
+    };
+    for (int64_t o0 = wave * RPW; o0 < d.KO; o0 += nwaves * RPW) {   // wave-uniform
+        const int64_t nvec = (d.KO - o0 < RPW ? d.KO - o0 : RPW) * V;
+        WAcc<T> wacc;
+        wacc.init();
+        load(layer_base(0), o0, nvec);
+        for (int64_t l = 0; l < g.n_layers; ++l) {
+#pragma unroll
+            for (int u = 0; u < UL; ++u)
+                if (u * kWave + lane < nvec) t[lrow[u] * kRowLdsStride + lcol[u]] = w[u];
+            wave_sync_lds();
+            if (l + 1 < g.n_layers) load(layer_base(l + 1), o0, nvec);
+            TileAcc<T> acc;
+            acc.init();
+            const uint4 *row = t + rw * kRowLdsStride + h * VH;
+            for (int i = 0; i < VH; ++i) {
+                T x[N];
+                unpack16<T, BSWAP>(row[i], x);
+                acc.template add_n<N, MASKED, false>(x, mk);
+            }
+            if constexpr (!MASKED) acc.count += (uint32_t)(VH * N);
+            uint32_t cnt, nan;
+            group_reduce(acc, H, cnt, nan);
+            if (h == 0) {
+                pyas_partial pp;
+                store_group(acc, cnt, nan, &pp);
+                merge(wacc, pp, round);
+            }
+            wave_sync_lds();
+        }
+        if (h == 0 && o0 + rw < d.KO) {
+            int64_t loc = o0 + rw, f = 0;   // kept-dims index in the chunk -> final element
+#pragma unroll
+            for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+                if (dd < r.ndim && !((red >> dd) & 1u)) {
+                    const int64_t q = loc / r.shape[dd];
+                    f += (ac[dd] * r.shape[dd] + (loc - q * r.shape[dd])) * g.ostride[dd];
+                    loc = q;
+                }
+            }
+            store_wpartial(a.out + f, wacc);
+        }
+    }
+}
+
 template <typename T, bool SHUF, bool BSWAP>
 __global__ __launch_bounds__(kBlock) void k_reduce_axes(AxesArgs a) {
     __shared__ int32_t roff[kAxesLds];
@@ -1539,12 +1656,28 @@ hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hip
     return hipGetLastError();
 }
 
+template <typename T, int H>
+static void launch_fold_row(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
+    const dim3 blk(kBlock);
+    if (a.bswap) {
+        if (masked) hipLaunchKernelGGL((k_axes_fold_row<T, true, 1, H>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_row<T, true, 0, H>), gr, blk, 0, st, a, g);
+    } else {
+        if (masked) hipLaunchKernelGGL((k_axes_fold_row<T, false, 1, H>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_row<T, false, 0, H>), gr, blk, 0, st, a, g);
+    }
+}
+
 template <typename T>
 hipError_t launch_axes_fold_t(const AxesArgs &a, const FoldGrid &g, bool masked, int64_t grid,
                               hipStream_t st) {
     const dim3 gr((unsigned)grid), blk(kBlock);
     if constexpr (sizeof(T) < 4) {
         return hipErrorInvalidValue;     // dense_geometry: >= 4-byte elements only
+    } else if (a.d.mode >= 4) {
+        if (a.d.mode == 4) launch_fold_row<T, 1>(a, g, masked, gr, st);
+        else if (a.d.mode == 5) launch_fold_row<T, 2>(a, g, masked, gr, st);
+        else launch_fold_row<T, 4>(a, g, masked, gr, st);
     } else {
         if (a.bswap) {
             if (masked) hipLaunchKernelGGL((k_axes_fold<T, true, 1>), gr, blk, 0, st, a, g);

@@ -1,5 +1,5 @@
 """pyas_reduce_axes_grid (chunk layers folded inside the dense column
-kernel, one launch) against the two-step path it replaces
+or LDS row kernel, one launch) against the two-step path it replaces
 (pyas_reduce_axes -> per-chunk partial arrays -> pyas_combine_grid), which
 follows ``Active._from_storage``'s combine (``activestorage/active.py:
 487-516,575-598``).  The combined partials must agree bit for bit: sums,
@@ -93,6 +93,12 @@ CASES = [
     ((128, 8), (32, 8), (0,), np.s_[...]),
     ((20, 256), (5, 256), (0,), np.s_[...]),       # few outputs per chunk: split reduced rows
     ((6, 1024, 8), (3, 128, 8), (0, 1), np.s_[...]),
+    # innermost dims reduced, runs <= 256 B: the LDS row layout's fold
+    ((32, 32, 32), (8, 16, 32), (2,), np.s_[...]),
+    ((16, 12, 40), (4, 6, 20), (2,), np.s_[...]),   # 5 vectors per f4 run: one lane per output
+    ((16, 12, 20, 24), (4, 6, 5, 8), (3,), np.s_[4:16]),
+    ((24, 96), (8, 32), (1,), np.s_[...]),
+    ((40, 8, 32), (8, 8, 32), (2,), np.s_[...]),   # 64 outputs per chunk: a partial last tile
 ]
 
 
@@ -118,11 +124,12 @@ def test_fold_matches_two_step(gpu, dtype, masked, case, monkeypatch):
     np.testing.assert_allclose(np.ma.getdata(r1)[ok], np.ma.getdata(want)[ok], rtol=1e-5, atol=1e-4)
 
 
-def test_fold_refuses_row_layout(gpu, monkeypatch):
-    """Innermost dim reduced: no column layout, the two-step path runs."""
+def test_fold_refuses_long_rows(gpu, monkeypatch):
+    """Innermost dim reduced with 512-B runs: neither the column nor the LDS
+    row layout, so the two-step path runs."""
     gpu.set_fold_min_blocks(1)
     rng = np.random.default_rng(3)
-    var, data = _variable((32, 32, 64), (8, 16, 64), "<f4", rng, True)
+    var, data = _variable((32, 32, 128), (8, 16, 128), "<f4", rng, True)
     f, r, n = _partials(var, (2,), np.s_[...], True, monkeypatch)
     assert n == 0
     f0, r0, _ = _partials(var, (2,), np.s_[...], False, monkeypatch)
