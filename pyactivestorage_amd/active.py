@@ -211,11 +211,14 @@ class Active:
     # -- host ingest -------------------------------------------------------
     def _ingest(self, coords, compressor, filters):
         """Device buffer + per-chunk offsets of every touched chunk (decoded,
-        still byte-shuffled when the shuffle is fused into the kernels)."""
+        still byte-shuffled when the shuffle is fused into the kernels).
+        ``coords``: chunk coordinate tuples, or an int64 array (n, ndim)."""
         if self.resident:
             got = self._ingest_resident(coords, compressor, filters)
             if got is not None:
                 return got
+        if isinstance(coords, np.ndarray):
+            coords = [tuple(c) for c in coords.tolist()]
         return self._ingest_fresh(coords, compressor, filters)
 
     def _ingest_resident(self, coords, compressor, filters):
@@ -243,7 +246,7 @@ class Active:
             c = np.asarray(coords, dtype=np.int64).reshape(len(coords), len(grid))
             slots = np.ravel_multi_index(c.T, grid) if len(coords) else np.zeros(0, dtype=np.int64)
             todo = np.nonzero(~store["loaded"][slots])[0]
-        _, st, _, _, fused = self._ingest_fresh([coords[i] for i in todo.tolist()], compressor, filters,
+        _, st, _, _, fused = self._ingest_fresh([tuple(x) for x in c[todo].tolist()], compressor, filters,
                                                 dst=store["buf"], dst_offsets=slots[todo] * stride)
         if todo.size:
             # another thread's kernels (on its own stream) may read these slots
@@ -444,8 +447,7 @@ class Active:
             weights = np.prod(table[:, :ds.ndim, 2].astype(np.int64), axis=1)
             lo, hi = shard_ranges(weights, dist.get_world_size(self.group))[dist.get_rank(self.group)]
         if hi > lo:
-            ctx, st, buf, offsets, fused = self._ingest([tuple(c) for c in coords[lo:hi].tolist()],
-                                                        compressor, filters)
+            ctx, st, buf, offsets, fused = self._ingest(coords[lo:hi], compressor, filters)
             sub = table[lo:hi]
             full = _all_full(sub, ds.chunks)   # whole chunks: no table, lean/dense kernels
             plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused,
@@ -811,7 +813,7 @@ class Active:
             coords[:, d] = np.array([p.chunk_ix for p in dims[d]], dtype=np.int64)[idx[d]]
         pool = np.concatenate(pool_parts) if pool_parts else np.zeros(1, dtype=np.int32)
         pos = np.concatenate(pos_parts)
-        ctx, st, buf, offsets, fused = self._ingest([tuple(c) for c in coords.tolist()], compressor, filters)
+        ctx, st, buf, offsets, fused = self._ingest(coords, compressor, filters)
         full = _all_full(table, ds.chunks)
         plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused,
                              sel_table=None if full else table, index_pool=None if full else pool,
