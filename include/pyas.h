@@ -173,6 +173,11 @@ int pyas_ctx_set_fold_min_blocks(pyas_ctx *ctx, int64_t n);
 /* ---- memory helpers (so a non-torch host can drive the ABI) ------------- */
 int pyas_malloc(pyas_ctx *ctx, size_t nbytes, void **dptr);
 int pyas_free(pyas_ctx *ctx, void *dptr);
+/* Pinned (page-locked) host memory: H2D copies from it are DMA, without the
+ * runtime's pageable staging.  The per-chunk drop-in reads each chunk
+ * (storage.py:51-53 read_block) straight into a per-thread pinned buffer. */
+int pyas_host_alloc(pyas_ctx *ctx, size_t nbytes, void **hptr);
+int pyas_host_free(pyas_ctx *ctx, void *hptr);
 int pyas_memcpy_h2d(pyas_ctx *ctx, void *dst, const void *src, size_t n, void *stream);
 int pyas_memcpy_d2h(pyas_ctx *ctx, void *dst, const void *src, size_t n, void *stream);
 int pyas_stream_create(pyas_ctx *ctx, void **stream);

@@ -111,6 +111,8 @@ SIGNATURES = {
     "pyas_ctx_set_fold_min_blocks": [_vp, _i64],
     "pyas_malloc": [_vp, _sz, ctypes.POINTER(_vp)],
     "pyas_free": [_vp, _vp],
+    "pyas_host_alloc": [_vp, _sz, ctypes.POINTER(_vp)],
+    "pyas_host_free": [_vp, _vp],
     "pyas_memcpy_h2d": [_vp, _vp, _vp, _sz, _vp],
     "pyas_memcpy_d2h": [_vp, _vp, _vp, _sz, _vp],
     "pyas_stream_create": [_vp, ctypes.POINTER(_vp)],

@@ -323,6 +323,22 @@ int pyas_free(pyas_ctx *ctx, void *dptr) {
     return PYAS_OK;
 }
 
+int pyas_host_alloc(pyas_ctx *ctx, size_t nbytes, void **hptr) {
+    if (!ctx || !hptr) return fail(PYAS_EINVAL, "NULL argument");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    *hptr = nullptr;
+    PYAS_HIP(hipHostMalloc(hptr, nbytes ? nbytes : 1, hipHostMallocDefault));
+    return PYAS_OK;
+}
+
+int pyas_host_free(pyas_ctx *ctx, void *hptr) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!hptr) return PYAS_OK;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(hipHostFree(hptr));
+    return PYAS_OK;
+}
+
 int pyas_memcpy_h2d(pyas_ctx *ctx, void *dst, const void *src, size_t n, void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     if (n == 0) return PYAS_OK;

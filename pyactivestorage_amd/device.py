@@ -103,6 +103,22 @@ class Context:
             b = bufs[slot] = DeviceBuffer(self, max(int(nbytes), 256))
         return b
 
+    def thread_host_buffer(self, nbytes: int) -> np.ndarray:
+        """Per-thread pinned host staging (uint8, at least ``nbytes``); H2D
+        copies from it are DMA.  Reused by the thread's next call: callers
+        synchronize the thread stream before refilling it."""
+        hb = getattr(self._tls, "host_buf", None)
+        if hb is None or hb[1] < nbytes:
+            if hb is not None:
+                self.synchronize(self.thread_stream())
+                _lib.check(self.lib.pyas_host_free(self.handle, hb[0]), "pyas_host_free")
+            size = max(int(nbytes), 1 << 20)
+            p = ctypes.c_void_p()
+            _lib.check(self.lib.pyas_host_alloc(self.handle, size, ctypes.byref(p)), "pyas_host_alloc")
+            arr = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(p.value))
+            hb = self._tls.host_buf = (p.value, size, arr)
+        return hb[2]
+
     # -- copies --------------------------------------------------------------
     def h2d(self, dst_ptr: int, host: np.ndarray, stream: int | None) -> None:
         """Async copy; the host array is kept alive until the next

@@ -126,7 +126,7 @@ def reduce_chunk(rfile, offset, size, compression, filters, missing, dtype, shap
     else:
         try:
             with open(rfile, "rb") as fh:
-                raw = read_block(fh, offset, size)
+                raw = _read_pinned(fh, offset, size)
         except FileNotFoundError:
             # storage.py:63-76 falls back to an HTTP(S) read through fsspec
             import fsspec  # optional dependency of the reference
@@ -135,6 +135,19 @@ def reduce_chunk(rfile, offset, size, compression, filters, missing, dtype, shap
                 raw = read_block(fh, offset, size)
     return reduce_chunk_bytes(raw, compression, filters, missing, dtype, shape, order,
                               chunk_selection, axis, method)
+
+
+def _read_pinned(fh, offset, size):
+    """read_block (storage.py:156-162) into the calling thread's pinned
+    staging buffer (the chunk's H2D copy is then DMA).  The view is valid
+    until this thread's next call; reduce_chunk_bytes synchronizes before
+    returning.  A short read (past the end of the file) returns the bytes
+    that exist, as ``fh.read`` does."""
+    ctx = get_context(0)
+    host = ctx.thread_host_buffer(int(size))
+    fh.seek(offset)
+    n = fh.readinto(memoryview(host)[: int(size)])
+    return memoryview(host)[: n or 0]
 
 
 def reduce_opens3_chunk(fh, offset, size, compression, filters, missing, dtype, shape, order,
