@@ -317,6 +317,16 @@ int pyas_format_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, i
 int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes,
                    int32_t elementsize, void *stream);
 
+/* Batched un-shuffle of n_chunks whole chunks of chunk_bytes each, device to
+ * device: chunk i from src + src_offsets[i] to dst + dst_offsets[i] (both
+ * offset arrays in device memory); elementsize 2, 4 or 8 (PYAS_ENOTSUP
+ * otherwise); trailing chunk_bytes % elementsize bytes are copied through.
+ * Resident variables keep their chunks un-shuffled this way, so later
+ * queries take the dense kernels (storage.py:121-122 once per chunk). */
+int pyas_unshuffle_chunks(pyas_ctx *ctx, const void *src, const int64_t *src_offsets, void *dst,
+                          const int64_t *dst_offsets, int64_t n_chunks, int64_t chunk_bytes,
+                          int32_t elementsize, void *stream);
+
 /* ---- zlib inflate (row f3) ------------------------------------------------- */
 /* Per-stream outcome of pyas_inflate, mirroring zlib inflate()'s failures
  * (zlib.error from zlib.decompress in the reference, storage.py:119-120). */

@@ -131,6 +131,7 @@ SIGNATURES = {
                               _vp, _vp],
     "pyas_format_partials": [_vp, _i32, _vp, _i64, _i32, _vp, _vp, _vp, _vp],
     "pyas_unshuffle": [_vp, _vp, _vp, _i64, _i32, _vp],
+    "pyas_unshuffle_chunks": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "pyas_inflate": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "pyas_read_ranges": [_vp, ctypes.c_int, _i64, _vp, _vp, _vp, _vp, _i32, _vp],
     "pyas_ctx_set_ingest_slots": [_vp, _i32, _i64],

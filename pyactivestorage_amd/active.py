@@ -246,8 +246,25 @@ class Active:
             c = np.asarray(coords, dtype=np.int64).reshape(len(coords), len(grid))
             slots = np.ravel_multi_index(c.T, grid) if len(coords) else np.zeros(0, dtype=np.int64)
             todo = np.nonzero(~store["loaded"][slots])[0]
-        _, st, _, _, fused = self._ingest_fresh([tuple(x) for x in c[todo].tolist()], compressor, filters,
-                                                dst=store["buf"], dst_offsets=slots[todo] * stride)
+        todo_coords = [tuple(x) for x in c[todo].tolist()]
+        fused = self._fused_shuffle(filters)
+        if fused in (2, 4, 8):
+            # the store keeps chunks un-shuffled (one batched pass as they
+            # arrive), so every later query takes the unshuffled kernels
+            # (dense partial-axis layouts and the in-kernel layer fold)
+            st = ctx.thread_stream()
+            if todo.size:
+                _, st, tmp, toffs, _ = self._ingest_fresh(todo_coords, compressor, filters)
+                offs = np.concatenate([toffs, slots[todo] * stride]).astype(np.int64)
+                meta = DeviceBuffer(ctx, offs.nbytes)
+                ctx.h2d(meta.ptr, offs, st)
+                engine.unshuffle_chunks(ctx, tmp.ptr, meta.ptr, store["buf"].ptr, meta.ptr + 8 * todo.size,
+                                        todo.size, nbytes, fused, st)
+                ctx.synchronize(st)   # tmp and meta are freed on return
+            fused = 0
+        else:
+            _, st, _, _, fused = self._ingest_fresh(todo_coords, compressor, filters,
+                                                    dst=store["buf"], dst_offsets=slots[todo] * stride)
         if todo.size:
             # another thread's kernels (on its own stream) may read these slots
             # as soon as they are marked: mark them once the copies have landed

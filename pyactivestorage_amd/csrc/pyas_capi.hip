@@ -830,6 +830,22 @@ int pyas_unshuffle(pyas_ctx *ctx, const void *src, void *dst, int64_t n_bytes, i
     return PYAS_OK;
 }
 
+int pyas_unshuffle_chunks(pyas_ctx *ctx, const void *src, const int64_t *src_offsets, void *dst,
+                          const int64_t *dst_offsets, int64_t n_chunks, int64_t chunk_bytes,
+                          int32_t elementsize, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (n_chunks < 0 || chunk_bytes < 0) return fail(PYAS_EINVAL, "bad n_chunks/chunk_bytes");
+    if (elementsize != 2 && elementsize != 4 && elementsize != 8)
+        return fail(PYAS_ENOTSUP, "pyas_unshuffle_chunks: elementsize %d (2, 4 or 8)", elementsize);
+    if (n_chunks == 0 || chunk_bytes == 0) return PYAS_OK;
+    if (!src || !dst || !src_offsets || !dst_offsets) return fail(PYAS_EINVAL, "NULL buffer");
+    if (n_chunks * ((chunk_bytes + 4095) / 4096) >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(pyas::launch_unshuffle_chunks(src, src_offsets, dst, dst_offsets, n_chunks, chunk_bytes,
+                                           elementsize, (hipStream_t)stream));
+    return PYAS_OK;
+}
+
 int pyas_inflate(pyas_ctx *ctx, const uint8_t *src, const int64_t *src_offsets,
                  const int64_t *src_sizes, int64_t n, uint8_t *dst,
                  const int64_t *dst_offsets, const int64_t *dst_capacity,

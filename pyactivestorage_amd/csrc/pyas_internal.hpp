@@ -162,6 +162,8 @@ int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const
                 uint8_t *dst, const int64_t *dst_offsets, int32_t threads, hipStream_t st,
                 std::string &msg);
 
+hipError_t launch_unshuffle_chunks(const void *src, const int64_t *soff, void *dst, const int64_t *doff,
+                                   int64_t n_chunks, int64_t nbytes, int64_t es, hipStream_t st);
 hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es,
                             hipStream_t st);
 

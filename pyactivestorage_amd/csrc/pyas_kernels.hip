@@ -23,6 +23,50 @@ __global__ __launch_bounds__(kBlock) void k_unshuffle(const uint8_t *src, uint8_
     }
 }
 
+// Batched un-shuffle of whole chunks (pyas_unshuffle_chunks): block (c, j)
+// of chunk c takes groups of 4 elements; a lane reads one dword from each of
+// the ES byte planes (a wave reads 256 contiguous bytes of every plane) and
+// writes its 4 elements as ES dwords.  Chunks whose planes are not dword
+// aligned, and the n % 4 tail, go byte by byte.
+template <int ES>
+__global__ __launch_bounds__(kBlock) void k_unshuffle_chunks(const uint8_t *src, const int64_t *soff,
+                                                             uint8_t *dst, const int64_t *doff,
+                                                             int64_t nbytes, int64_t bpc) {
+    const int64_t c = blockIdx.x / bpc, j = blockIdx.x - c * bpc;
+    const uint8_t *s = src + soff[c];
+    uint8_t *d = dst + doff[c];
+    const int64_t n = nbytes / ES;
+    const bool vec = (((uintptr_t)s | (uintptr_t)d) & 3) == 0 && (n & 3) == 0;
+    const int64_t groups = vec ? n / 4 : 0;
+    for (int64_t g = j * kBlock + threadIdx.x; g < groups; g += bpc * kBlock) {
+        uint32_t w[ES];
+#pragma unroll
+        for (int b = 0; b < ES; ++b) w[b] = *reinterpret_cast<const uint32_t *>(s + b * n + g * 4);
+        uint32_t o[ES];
+#pragma unroll
+        for (int q = 0; q < ES; ++q) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {        // output byte 4q + t = element k, plane b
+                const int ob = 4 * q + t, k = ob / ES, b = ob - k * ES;
+                v |= ((w[b] >> (8 * k)) & 0xffu) << (8 * t);
+            }
+            o[q] = v;
+        }
+        uint32_t *dp = reinterpret_cast<uint32_t *>(d + g * 4 * ES);
+#pragma unroll
+        for (int q = 0; q < ES; ++q) dp[q] = o[q];
+    }
+    for (int64_t q = groups * 4 * ES + j * kBlock + threadIdx.x; q < nbytes; q += bpc * kBlock) {
+        if (q < n * ES) {
+            const int64_t i = q / ES, b = q - i * ES;
+            d[q] = s[b * n + i];
+        } else {
+            d[q] = s[q];
+        }
+    }
+}
+
 #define PYAS_DISPATCH_T(DT, CALL)                                  \
     switch (DT) {                                                  \
         case PYAS_I8: { using T = int8_t; CALL; } break;           \
@@ -102,6 +146,21 @@ hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t 
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_unshuffle, dim3((unsigned)blocks), dim3(kBlock), 0, st,
                        (const uint8_t *)src, (uint8_t *)dst, nbytes, es);
+    return hipGetLastError();
+}
+
+hipError_t launch_unshuffle_chunks(const void *src, const int64_t *soff, void *dst, const int64_t *doff,
+                                   int64_t n_chunks, int64_t nbytes, int64_t es, hipStream_t st) {
+    int64_t bpc = (nbytes / 16 + kBlock - 1) / kBlock;   // ~16 output bytes per lane
+    if (bpc > 64) bpc = 64;
+    if (bpc < 1) bpc = 1;
+    const dim3 g((unsigned)(n_chunks * bpc)), b(kBlock);
+    const uint8_t *s = (const uint8_t *)src;
+    uint8_t *d = (uint8_t *)dst;
+    if (es == 2) hipLaunchKernelGGL(k_unshuffle_chunks<2>, g, b, 0, st, s, soff, d, doff, nbytes, bpc);
+    else if (es == 4) hipLaunchKernelGGL(k_unshuffle_chunks<4>, g, b, 0, st, s, soff, d, doff, nbytes, bpc);
+    else if (es == 8) hipLaunchKernelGGL(k_unshuffle_chunks<8>, g, b, 0, st, s, soff, d, doff, nbytes, bpc);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -161,3 +161,11 @@ def format_partials(ctx: Context, dt, in_ptr, n, method: str, values_ptr, mask_p
 def unshuffle(ctx: Context, src_ptr, dst_ptr, nbytes, elementsize, stream) -> None:
     _lib.check(ctx.lib.pyas_unshuffle(ctx.handle, src_ptr, dst_ptr, int(nbytes), int(elementsize),
                                       stream), "pyas_unshuffle")
+
+
+def unshuffle_chunks(ctx: Context, src_ptr, src_offsets_ptr, dst_ptr, dst_offsets_ptr, n_chunks,
+                     chunk_bytes, elementsize, stream) -> None:
+    """Batched device un-shuffle of whole chunks (offset arrays on the device)."""
+    _lib.check(ctx.lib.pyas_unshuffle_chunks(ctx.handle, src_ptr, src_offsets_ptr, dst_ptr, dst_offsets_ptr,
+                                             int(n_chunks), int(chunk_bytes), int(elementsize), stream),
+               "pyas_unshuffle_chunks")

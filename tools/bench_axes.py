@@ -21,11 +21,14 @@ def main():
     ctx = get_context(0)
     st = torch.cuda.current_stream().cuda_stream
     shape, chunks = (1024, 1024, 1024), (64, 64, 64)
-    data, offsets, _ = chunk_major_device(torch, shape, chunks, np.float32, dev, fill=-999.0, fill_frac=0.01)
+    shuffled = "--shuffle" in sys.argv   # chunks stored HDF5-byte-shuffled (the generic kernel's path)
+    data, offsets, _ = chunk_major_device(torch, shape, chunks, np.float32, dev, fill=-999.0, fill_frac=0.01,
+                                          shuffle=shuffled)
     missing = (np.float32(-999.0), None, np.float32(1000.0), np.float32(5e8))
     if "--unmasked" in sys.argv:
         missing = None
-    plan = ReductionPlan(ctx, np.float32, chunks, data.data_ptr(), offsets, missing=missing, stream=st)
+    plan = ReductionPlan(ctx, np.float32, chunks, data.data_ptr(), offsets, missing=missing, stream=st,
+                         shuffle=4 if shuffled else 0)
     nbytes = data.numel()
     res = {}
     for axes in ((0,), (1,), (2,), (0, 1), (1, 2), (0, 2)):
@@ -47,7 +50,8 @@ def main():
         res[str(axes)] = {"ms": round(dt * 1e3, 3), "GBps": round(nbytes / dt / 1e9, 1),
                           "outputs_per_chunk": n_out}
         del out
-    print(json.dumps({"workload": "c3 partial-axis per-chunk reduce_axes", "results": res}))
+    print(json.dumps({"workload": "c3 partial-axis per-chunk reduce_axes" + (", byte-shuffled chunks" if shuffled else ""),
+                      "results": res}))
 
 
 if __name__ == "__main__":
