@@ -7,6 +7,7 @@ ten netCDF numeric dtypes, both byte orders, with and without the shuffle
 filter, and every masking attribute.
 """
 import itertools
+import zlib
 
 import numpy as np
 import pytest
@@ -179,3 +180,53 @@ def test_file_reduce_chunk_roundtrip(gpu, tmp_path):
                                (4, 8, 8), "C", sel, (0, 1, 2), np.ma.max)
     assert_same(want, got, "max")
     assert_counts(wn, gn)
+
+
+def test_file_reduce_chunk_pinned_staging(gpu, tmp_path):
+    """reduce_chunk's file read goes into a per-thread pinned staging buffer
+    (storage.py:51-53 read_block): growing chunk sizes from one thread, a
+    zlib + shuffle chunk (device inflate straight from the staging view),
+    eight threads at once on different chunks, and a read past the end of
+    the file (storage.py:57-62 raises ValueError on the short reshape)."""
+    import concurrent.futures
+    from oracle.storage_ref import Shuffle, Zlib
+    rng = np.random.default_rng(9)
+    shapes = [(2, 4, 4), (16, 32, 32), (8, 8, 8), (64, 64, 64), (4, 4, 4)]
+    arrs = [rng.uniform(-5, 5, size=s).astype("<f4") for s in shapes]
+    comp = zlib.compress(shuffle_bytes(arrs[1], 4), 4)
+    blobs = [a.tobytes() for a in arrs] + [comp]
+    offs, pos = [], 7
+    path = tmp_path / "mixed.bin"
+    with open(path, "wb") as fh:
+        fh.write(b"\x01" * 7)
+        for b in blobs:
+            offs.append(pos)
+            fh.write(b)
+            pos += len(b)
+    miss = (None, None, -4.0, 4.0)
+    sel_of = lambda s: tuple(slice(0, n, 1) for n in s)
+
+    def one(k):
+        s = shapes[k]
+        want, wn = ref.reduce_chunk(str(path), offs[k], len(blobs[k]), None, None, miss, "<f4", s, "C",
+                                    sel_of(s), (0, 1, 2), np.ma.sum)
+        got, gn = pas.reduce_chunk(str(path), offs[k], len(blobs[k]), None, None, miss, "<f4", s, "C",
+                                   sel_of(s), (0, 1, 2), np.ma.sum)
+        assert_same(want, got, "sum")
+        assert_counts(wn, gn, f"chunk {k}")
+
+    for k in range(len(shapes)):            # one thread, staging grows and is reused
+        one(k)
+    zc, filt = Zlib(4), [Shuffle(4)]
+    want, wn = ref.reduce_chunk(str(path), offs[-1], len(comp), zc, filt, miss, "<f4", shapes[1], "C",
+                                sel_of(shapes[1]), (0, 1, 2), np.ma.max)
+    got, gn = pas.reduce_chunk(str(path), offs[-1], len(comp), zc, filt, miss, "<f4", shapes[1], "C",
+                               sel_of(shapes[1]), (0, 1, 2), np.ma.max)
+    assert_same(want, got, "max")
+    assert_counts(wn, gn, "zlib+shuffle")
+    with concurrent.futures.ThreadPoolExecutor(max_workers=8) as ex:
+        list(ex.map(one, [k % len(shapes) for k in range(40)]))
+    for fn in (ref.reduce_chunk, pas.reduce_chunk):   # past the end of the file
+        with pytest.raises(ValueError):
+            fn(str(path), pos - 100, len(blobs[0]) + 200, None, None, miss, "<f4", (2, 4, 4), "C",
+               sel_of((2, 4, 4)), (0, 1, 2), np.ma.sum)
