@@ -626,20 +626,47 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
 #pragma unroll
     for (int d = 0; d < PYAS_MAX_DIMS; ++d)
         if (d < g.ndim && !((g.axes_mask >> d) & 1u)) nk += a[d] * gstride[d];
+    // Layers in C order over the reduced dims: a radix counter walks the
+    // chunk positions (no division per layer), and U layers' offset and
+    // partial loads are issued before they are merged (in the same order, so
+    // the result does not change): with few outputs and many layers (C3
+    // axes (0,1): 1024 outputs x 256 layers) the fold is latency-bound.
     WAcc<T> acc;
     acc.init();
-    for (int64_t l = 0; l < n_layers; ++l) {
-        int64_t n = nk, r = l;
+    int64_t digit[PYAS_MAX_DIMS];
 #pragma unroll
-        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-            if (d < g.ndim && ((g.axes_mask >> d) & 1u)) {
-                const int64_t c = g.n_coords[d];
-                const int64_t q = r / c;
-                n += (r - q * c) * gstride[d];
-                r = q;
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) digit[d] = 0;
+    int64_t n = nk;
+    constexpr int U = 8;
+    for (int64_t l0 = 0; l0 < n_layers; l0 += U) {
+        int64_t off[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            off[u] = 0;
+            if (l0 + u < n_layers) {
+                off[u] = g.chunk_out_offsets[n];
+                bool carry = true;
+#pragma unroll
+                for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+                    if (carry && d < g.ndim && ((g.axes_mask >> d) & 1u)) {
+                        n += gstride[d];
+                        if (++digit[d] == g.n_coords[d]) {
+                            digit[d] = 0;
+                            n -= g.n_coords[d] * gstride[d];
+                        } else {
+                            carry = false;
+                        }
+                    }
+                }
             }
         }
-        merge(acc, in[g.chunk_out_offsets[n] + j], round);
+        pyas_partial p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (l0 + u < n_layers) p[u] = in[off[u] + j];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (l0 + u < n_layers) merge(acc, p[u], round);
     }
     store_wpartial(out + f, acc);
 }
