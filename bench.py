@@ -9,13 +9,27 @@ per-GPU partials are exchanged with one RCCL all-gather and combined in rank
 order.  Those statistics give mean, max and min (C3's three methods).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+
+Multi-GPU: either ``python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N`` (WORLD_SIZE/RANK/LOCAL_RANK from the launcher), or plain
+``python bench.py --gpus N``: with no WORLD_SIZE in the environment this
+process starts N rank processes itself (before anything touches the GPU) and
+exits with their status.  It never runs fewer ranks than ``--gpus`` asks for.
+
+The JSON line's headline (``value``) is C3 at the chosen scaling (weak by
+default: each GPU adds a 1024^3 slab).  ``extra`` adds the two 8-GPU configs
+of BASELINE.json measured at the same N, both strong scaling (one fixed
+variable split over the ranks): C4 2048^3 f32 128^3 shuffled + masked
+(4096 chunks, 4096/N per rank) and C5 4096x2048x1024 f64 32^3 hyperslab
+masked mean (262,144 chunks).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -46,7 +60,7 @@ VMIN = 1000.0
 VMAX = 5e8
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -56,6 +70,10 @@ def parse():
     p.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                    help="weak: each GPU adds its own slab of the variable (dim 0); "
                         "strong: one variable of the config's shape split across GPUs")
+    p.add_argument("--extra", default="c4,c5",
+                   help="comma list of configs also measured at this N with strong scaling "
+                        "(reported under 'extra'; 'none' to skip)")
+    p.add_argument("--extra-steps", type=int, default=10)
     p.add_argument("--cpu-chunks", type=int, default=4096,
                    help="chunks in the CPU-baseline sample (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=30)
@@ -68,9 +86,117 @@ def parse():
                    help="also time file (page cache) -> native pread ring -> H2D -> reduce -> scalar "
                         "(rank 0, N=1)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    return p.parse_args()
+    p.add_argument("--selftest-launch", action="store_true",
+                   help="CPU-only rehearsal of the N-rank launcher (gloo, no GPU): each rank "
+                        "reduces its shard of a small variable with NumPy, the partials are "
+                        "all-gathered and folded in rank order, rank 0 prints the wiring")
+    return p.parse_args(argv)
 
 
+# ---------------------------------------------------------------------------
+# launcher
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv, check_devices: bool = True, timeout: float | None = None) -> int:
+    """Start ``n`` rank processes of this script (one per GPU) and wait.
+
+    Runs in a process that has not touched the GPU (counting devices does
+    not initialise it), and starts children rather than exec'ing, so no
+    GPU-initialised process is ever replaced.  Exits non-zero if fewer than
+    ``n`` devices are visible: the bench never silently runs fewer ranks.
+    If one rank fails the others are stopped (they would wait forever in
+    the next collective)."""
+    if check_devices:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    t0 = time.monotonic()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:
+                    q.terminate()
+        if timeout is not None and time.monotonic() - t0 > timeout and live:
+            rc = rc or 124
+            for q in live:
+                q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rc
+
+
+def selftest_launch(rank: int, world: int) -> None:
+    """Rank body of ``--selftest-launch`` (CPU, gloo): the sharding and the
+    rank-order fold of the GPU path, with NumPy per-chunk partials."""
+    import torch
+    import torch.distributed as dist
+
+    from pyactivestorage_amd.distributed import exchange_partials, fold_partials_host, shard_ranges
+    from pyactivestorage_amd.engine import partial_dtype
+    from pyactivestorage_amd.synthetic import chunk_major_host
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shape, chunks = (32, 16, 24), (8, 8, 8)
+    buf, offsets = chunk_major_host(shape, chunks, np.float32)
+    vals = buf.view(np.float32).reshape(len(offsets), -1)
+    vals = np.where(np.arange(vals.size).reshape(vals.shape) % 7 == 0, np.float32(FILL), vals)
+    pdt = partial_dtype("<f4")
+    parts = np.zeros(len(offsets), dtype=pdt)
+    for c in range(len(offsets)):
+        ok = vals[c][(vals[c] != FILL) & (vals[c] >= 3.0)]
+        parts[c]["count"] = ok.size
+        parts[c]["sum"] = float(ok.astype(np.float64).sum())
+        parts[c]["min"] = float(ok.min()) if ok.size else 0.0
+        parts[c]["max"] = float(ok.max()) if ok.size else 0.0
+    lo, hi = shard_ranges(np.ones(len(offsets)), world)[rank]
+    local = fold_partials_host(parts[lo:hi])
+    gathered = exchange_partials(torch, torch.from_numpy(local.view(np.uint8).copy()))
+    final = fold_partials_host(np.frombuffer(gathered.numpy().tobytes(), dtype=pdt))
+    ranges = [None] * world
+    dist.all_gather_object(ranges, {"rank": rank, "env_rank": int(os.environ["RANK"]),
+                                    "local_rank": int(os.environ["LOCAL_RANK"]),
+                                    "world": int(os.environ["WORLD_SIZE"]),
+                                    "range": [lo, hi]})
+    if rank == 0:
+        single = fold_partials_host(parts)
+        print(json.dumps({"selftest": "launch", "n_ranks": world, "ranks": ranges,
+                          "final": {k: final[k][0].item() for k in pdt.names},
+                          "single": {k: single[k][0].item() for k in pdt.names}}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
+# workload
+# ---------------------------------------------------------------------------
 def chunk_selections(cfg, gshape, lo, hi):
     """Selection table (ABI layout, int32 [n, MAX_DIMS, 3]) of chunks [lo, hi)
     for configs with a hyperslab (margin m selects [m:-m] in every dim), and
@@ -223,14 +349,198 @@ def file_inclusive(torch, ctx, data, cfg, dt, missing, reps=3, threads=16):
             os.unlink(path)
 
 
+def _partials_dict(p):
+    return {"sum": float(p["sum"]), "count": int(p["count"]), "min": float(p["min"]),
+            "max": float(p["max"])}
+
+
+def _same(a, b, rel=1e-6):
+    """count/min/max exact, sum within ``rel`` (north_star's f32 bar)."""
+    return (a["count"] == b["count"] and a["min"] == b["min"] and a["max"] == b["max"]
+            and abs(a["sum"] - b["sum"]) <= rel * max(abs(b["sum"]), 1e-300))
+
+
+def run_config(env, name, scaling, steps, warmup, args, full_check=False):
+    """Build one config's data and plan on this rank, time ``steps`` steps
+    (barrier + synchronize on both sides, max over ranks), then self-check
+    the sharded result against the single-rank combine of all chunk
+    partials.  Returns the per-config report (on every rank)."""
+    torch, dist, ctx, dev, stream = env["torch"], env["dist"], env["ctx"], env["dev"], env["stream"]
+    rank, world, use_dist = env["rank"], env["world"], env["use_dist"]
+    from pyactivestorage_amd import _lib, engine
+    from pyactivestorage_amd.batch import ReductionPlan
+    from pyactivestorage_amd.distributed import reduce_sharded, shard_ranges
+    from pyactivestorage_amd.synthetic import chunk_major_device
+
+    cfg = CONFIGS[name]
+    dt = np.dtype(cfg["dtype"])
+    gshape = list(cfg["shape"])
+    if scaling == "weak":
+        gshape[0] *= world
+    gshape = tuple(gshape)
+    grid = [s // c for s, c in zip(gshape, cfg["chunks"])]
+    n_all = int(np.prod(grid))
+    _, weights = chunk_selections(cfg, gshape, 0, n_all)
+    lo, hi = shard_ranges(weights, world)[rank]
+    t_gen = time.perf_counter()
+    data, offsets, n_fill = chunk_major_device(
+        torch, gshape, cfg["chunks"], dt, dev, chunk_range=(lo, hi),
+        fill=FILL if cfg["masked"] else None, fill_frac=0.01 if cfg["masked"] else 0.0,
+        seed=0, shuffle=cfg["shuffle"])
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t_gen
+    missing = ((dt.type(FILL), None, dt.type(VMIN), dt.type(VMAX)) if cfg["masked"]
+               else (None, None, None, None))
+    sels, counts = chunk_selections(cfg, gshape, lo, hi)
+    plan = ReductionPlan(ctx, dt, cfg["chunks"], data.data_ptr(), offsets,
+                         shuffle=dt.itemsize if cfg["shuffle"] else 0, sel_table=sels,
+                         missing=missing, round_to_var=True, stream=stream)
+    n_chunks = plan.n_chunks
+    bytes_per_launch = int(counts.sum()) * dt.itemsize
+
+    check = None
+    if full_check and not cfg["shuffle"] and sels is None:
+        # independent device check of count/sum/min/max with plain torch ops
+        tdt = torch.float32 if dt.itemsize == 4 else torch.float64
+        v = data[: bytes_per_launch].view(tdt)
+        ok = (v != FILL) & (v >= VMIN) & (v <= VMAX) if cfg["masked"] else None
+        sel = v[ok] if ok is not None else v
+        check = {"torch": {"count": int(sel.numel()), "sum": float(sel.sum(dtype=torch.float64)),
+                           "min": float(sel.min()), "max": float(sel.max())}}
+        del v, ok, sel
+
+    final = torch.zeros(_lib.PARTIAL_NBYTES, dtype=torch.uint8, device=dev)
+    ex_events = []
+
+    def step(record=False):
+        if use_dist:
+            plan.launch(stream, chunk_partials=False)
+            if record:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            gathered = reduce_sharded(torch, plan, ctx, stream, final, launch=False)
+            if record:
+                e1.record()
+                ex_events.append((e0, e1))
+            return gathered
+        plan.launch(stream, chunk_partials=False)
+        return None
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.check(ctx.lib.pyas_timing_enable(ctx.handle, steps), "timing_enable")
+    if use_dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    if use_dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    import ctypes
+    ms = (ctypes.c_float * steps)()
+    nrec = ctypes.c_int32(0)
+    _lib.check(ctx.lib.pyas_timing_read(ctx.handle, ms, steps, ctypes.byref(nrec)), "timing_read")
+    _lib.check(ctx.lib.pyas_timing_enable(ctx.handle, 0), "timing_disable")
+    kern_ms = float(np.mean(np.array(ms[: nrec.value]))) if nrec.value else float("nan")
+    ex_ms = float(np.mean([a.elapsed_time(b) for a, b in ex_events])) if ex_events else None
+
+    # per-rank figures, gathered to every rank
+    mine = [elapsed, kern_ms, ex_ms if ex_ms is not None else -1.0, float(bytes_per_launch),
+            float(n_chunks), t_gen]
+    if use_dist:
+        t = torch.tensor(mine, dtype=torch.float64, device=dev)
+        allr = torch.empty(world * len(mine), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(allr, t)
+        per = allr.view(world, len(mine)).cpu().numpy()
+    else:
+        per = np.array([mine])
+    elapsed_max = float(per[:, 0].max())
+    total_bytes, total_chunks = float(per[:, 3].sum()), float(per[:, 4].sum())
+
+    # result + self-check: one more sharded step, then the single-rank
+    # combine (pyas_combine_partials, variable-dtype rounding) over every
+    # chunk partial of every rank in global chunk order must give the same
+    # count/min/max and the sum within 1e-6
+    plan.launch(stream, chunk_partials=True)
+    local_total = _partials_dict(plan.read_total(stream)[0])
+    if use_dist:
+        reduce_sharded(torch, plan, ctx, stream, final, launch=False)
+        torch.cuda.synchronize()
+        result = _partials_dict(np.frombuffer(final.cpu().numpy().tobytes(),
+                                              dtype=engine.partial_dtype(dt))[0])
+    else:
+        result = local_total
+    cparts = plan.read_chunk_partials(stream)
+    if use_dist:
+        allparts = [None] * world
+        dist.all_gather_object(allparts, cparts.tobytes())
+        cat = b"".join(allparts)
+    else:
+        cat = cparts.tobytes()
+    selfcheck = None
+    if rank == 0:
+        n_tot = len(cat) // _lib.PARTIAL_NBYTES
+        inp = torch.frombuffer(bytearray(cat), dtype=torch.uint8).to(dev)
+        one = torch.zeros(_lib.PARTIAL_NBYTES, dtype=torch.uint8, device=dev)
+        engine.combine_partials(ctx, dt, inp.data_ptr(), n_tot, one.data_ptr(), True, stream)
+        torch.cuda.synchronize()
+        single = _partials_dict(np.frombuffer(one.cpu().numpy().tobytes(),
+                                              dtype=engine.partial_dtype(dt))[0])
+        selfcheck = {"single_rank_combine": single, "chunks": n_tot, "ok": _same(result, single)}
+        if check is not None:  # rank 0's own chunks
+            check["kernel"] = local_total
+            check["ok"] = _same(local_total, check["torch"])
+        del inp, one
+    del data, plan, final
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    rep = {
+        "config": name, "desc": cfg["desc"], "scaling": scaling, "variable": list(gshape),
+        "chunk_shape": list(cfg["chunks"]), "dtype": "f64" if dt.itemsize == 8 else "f32",
+        "steps": steps, "warmup": warmup,
+        "value": round(total_bytes / (elapsed_max / steps) / 1e9, 2), "unit": "GB/s",
+        "ms_per_step": round(elapsed_max / steps * 1e3, 4),
+        "chunks_per_s": round(total_chunks / (elapsed_max / steps), 1),
+        "chunks_total": int(total_chunks), "bytes_total": int(total_bytes),
+        "per_rank": {"kernel_ms": [round(float(x), 5) for x in per[:, 1]],
+                     "exchange_combine_ms": ([round(float(x), 5) for x in per[:, 2]]
+                                             if use_dist else None),
+                     "chunks": [int(x) for x in per[:, 4]],
+                     "gen_s": [round(float(x), 2) for x in per[:, 5]]},
+        "kernel": "pyas::k_reduce", "kernel_ms_rank0": round(kern_ms, 5),
+        "bytes_rank0": bytes_per_launch, "chunks_rank0": n_chunks,
+        "frac_rank0": round(achieved / HBM_PEAK_GBS, 4),
+        "frac_min_rank": round(float((per[:, 3] / (per[:, 1] * 1e-3) / 1e9).min()) / HBM_PEAK_GBS, 4),
+        "result": result, "selfcheck": selfcheck, "check": check,
+    }
+    return rep, achieved
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # plain `python bench.py --gpus N`: become the launcher of N ranks
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], check_devices=not args.selftest_launch))
+    world = int(world_env or 1)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    if args.selftest_launch:
+        selftest_launch(rank, world)
+        return
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     use_dist = world > 1 or args.force_dist
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -240,108 +550,19 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from pyactivestorage_amd import _lib, engine
-    from pyactivestorage_amd.batch import ReductionPlan
-    from pyactivestorage_amd.distributed import reduce_sharded
     from pyactivestorage_amd.device import get_context
-    from pyactivestorage_amd.synthetic import chunk_major_device
 
-    cfg = CONFIGS[args.config]
-    dt = np.dtype(cfg["dtype"])
     ctx = get_context(local)
     if args.tile_bytes:
         ctx.set_tile_bytes(args.tile_bytes)
-    stream = torch.cuda.current_stream().cuda_stream
+    env = dict(torch=torch, dist=dist, ctx=ctx, dev=dev, stream=torch.cuda.current_stream().cuda_stream,
+               rank=rank, world=world, use_dist=use_dist)
 
-    # the variable: weak scaling grows it along dim 0 with the GPU count
-    gshape = list(cfg["shape"])
-    if args.scaling == "weak":
-        gshape[0] *= world
-    gshape = tuple(gshape)
-    grid = [s // c for s, c in zip(gshape, cfg["chunks"])]
-    n_all = int(np.prod(grid))
-    _, weights = chunk_selections(cfg, gshape, 0, n_all)
-    from pyactivestorage_amd.distributed import shard_ranges
-    lo, hi = shard_ranges(weights, world)[rank]
-    data, offsets, n_fill = chunk_major_device(
-        torch, gshape, cfg["chunks"], dt, dev, chunk_range=(lo, hi),
-        fill=FILL if cfg["masked"] else None, fill_frac=0.01 if cfg["masked"] else 0.0,
-        seed=rank, shuffle=cfg["shuffle"])
-    torch.cuda.synchronize()
-    missing = ((dt.type(FILL), None, dt.type(VMIN), dt.type(VMAX)) if cfg["masked"]
-               else (None, None, None, None))
-    sels, counts = chunk_selections(cfg, gshape, lo, hi)
-    plan = ReductionPlan(ctx, dt, cfg["chunks"], data.data_ptr(), offsets,
-                         shuffle=dt.itemsize if cfg["shuffle"] else 0, sel_table=sels,
-                         missing=missing, round_to_var=True, stream=stream)
-    n_chunks = plan.n_chunks
-    sel_elems = int(counts.sum())
-    bytes_per_launch = sel_elems * dt.itemsize
-    check = None
-    if not cfg["shuffle"] and sels is None:
-        # independent device check of the unmasked count with plain torch ops
-        tdt = torch.float32 if dt.itemsize == 4 else torch.float64
-        v = data[: bytes_per_launch].view(tdt)
-        ok = (v != FILL) & (v >= VMIN) & (v <= VMAX) if cfg["masked"] else torch.ones_like(v, dtype=torch.bool)
-        check = {"torch_count": int(ok.sum().item())}
-        del v, ok
+    cfg = CONFIGS[args.config]
+    dt = np.dtype(cfg["dtype"])
+    head, achieved = run_config(env, args.config, args.scaling, args.steps, args.warmup, args,
+                                full_check=True)
 
-    final = torch.zeros(_lib.PARTIAL_NBYTES, dtype=torch.uint8, device=dev)
-
-    def step():
-        if use_dist:
-            reduce_sharded(torch, plan, ctx, stream, final)
-        else:
-            plan.launch(stream, chunk_partials=False)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    _lib.check(ctx.lib.pyas_timing_enable(ctx.handle, args.steps), "timing_enable")
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if use_dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    import ctypes
-    ms = (ctypes.c_float * args.steps)()
-    nrec = ctypes.c_int32(0)
-    _lib.check(ctx.lib.pyas_timing_read(ctx.handle, ms, args.steps, ctypes.byref(nrec)), "timing_read")
-    kern_ms = float(np.mean(np.array(ms[: nrec.value]))) if nrec.value else float("nan")
-    if use_dist:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms_max = float(t[0]), float(t[1])
-    else:
-        kern_ms_max = kern_ms
-
-    tot = plan.read_total(stream)[0]
-    local = {"sum": float(tot["sum"]), "count": int(tot["count"]), "min": float(tot["min"]),
-             "max": float(tot["max"])}
-    if check is not None:
-        check["kernel_count"] = local["count"]
-        check["ok"] = check["torch_count"] == local["count"]
-    result = local
-    if use_dist:
-        fin = np.frombuffer(final.cpu().numpy().tobytes(), dtype=engine.partial_dtype(dt))[0]
-        result = {"sum": float(fin["sum"]), "count": int(fin["count"]), "min": float(fin["min"]),
-                  "max": float(fin["max"])}
-
-    ms_per_step = elapsed / args.steps * 1e3
-    if use_dist:
-        agg = torch.tensor([bytes_per_launch, n_chunks], dtype=torch.float64, device=dev)
-        dist.all_reduce(agg)
-        total_bytes, total_chunks = float(agg[0]), float(agg[1])
-    else:
-        total_bytes, total_chunks = float(bytes_per_launch), float(n_chunks)
-    value = total_bytes / (elapsed / args.steps) / 1e9
-    chunks_per_s = total_chunks / (elapsed / args.steps)
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     traffic = None
     try:
         with open(args.traffic_file) as f:
@@ -352,54 +573,78 @@ def main():
     except (OSError, ValueError):
         pass
 
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_chunks > 0:
-        nc = min(args.cpu_chunks, n_chunks)
+    # CPU baseline and host/file-inclusive legs: rank 0 at N=1 only
+    cpu = hostinc = fileinc = None
+    if rank == 0 and world == 1 and (args.cpu_chunks > 0 or args.host_inclusive or args.file_inclusive):
+        from pyactivestorage_amd.synthetic import chunk_major_device
+        data, _, _ = chunk_major_device(torch, cfg["shape"], cfg["chunks"], dt, dev,
+                                        fill=FILL if cfg["masked"] else None,
+                                        fill_frac=0.01 if cfg["masked"] else 0.0, seed=0,
+                                        shuffle=cfg["shuffle"])
+        missing = ((dt.type(FILL), None, dt.type(VMIN), dt.type(VMAX)) if cfg["masked"]
+                   else (None, None, None, None))
+        n_chunks = head["chunks_rank0"]
         cb = int(np.prod(cfg["chunks"])) * dt.itemsize
-        host = data[: nc * cb].cpu().numpy()
-        secs, _ = cpu_baseline(cfg, host, nc, missing, args.cpu_threads)
-        ncores = len(os.sched_getaffinity(0))
-        cpu = {"value": round(nc * cb / secs / 1e9, 4), "unit": "GB/s",
-               "cores": min(args.cpu_threads, ncores), "kind": "port",
-               "sample": f"{nc} of {n_chunks} chunks ({nc * cb / 2**20:.0f} MiB) of the same "
-                         f"workload, oracle storage_ref.reduce_chunk per chunk from a page-cache-hot "
-                         f"file on a {args.cpu_threads}-thread pool (active.py:557), "
-                         f"{secs:.2f} s, host has {ncores} usable cores",
-               "chunks_per_s": round(nc / secs, 1)}
+        if args.cpu_chunks > 0:
+            nc = min(args.cpu_chunks, n_chunks)
+            host = data[: nc * cb].cpu().numpy()
+            secs, _ = cpu_baseline(cfg, host, nc, missing, args.cpu_threads)
+            ncores = len(os.sched_getaffinity(0))
+            cpu = {"value": round(nc * cb / secs / 1e9, 4), "unit": "GB/s",
+                   "cores": min(args.cpu_threads, ncores), "kind": "port",
+                   "sample": f"{nc} of {n_chunks} chunks ({nc * cb / 2**20:.0f} MiB) of the same "
+                             f"workload, oracle storage_ref.reduce_chunk per chunk from a page-cache-hot "
+                             f"file on a {args.cpu_threads}-thread pool (active.py:557), "
+                             f"{secs:.2f} s; 'cores' = pool threads used, the host has {ncores} "
+                             f"usable cores",
+                   "chunks_per_s": round(nc / secs, 1)}
+            del host
+        if args.host_inclusive and data.numel() <= (8 << 30):
+            ser, ovl = host_inclusive(torch, ctx, data, cfg, dt, missing)
+            hostinc = {"serial_GBps": round(ser, 2), "overlapped_GBps": round(ovl, 2),
+                       "path": "pinned host -> H2D (16 slices, copy stream) -> fused reduce "
+                               "(compute stream) -> D2H 32 B"}
+        if args.file_inclusive and data.numel() <= (8 << 30):
+            gbs, sec = file_inclusive(torch, ctx, data, cfg, dt, missing)
+            fileinc = {"GBps": round(gbs, 2), "s_per_pass": round(sec, 4),
+                       "path": "chunk-major file in page cache -> pyas_read_ranges (16 pread threads, "
+                               "16 x 64 MiB pinned slots, H2D as slots fill) -> fused reduce -> D2H 32 B"}
+        del data
+        torch.cuda.empty_cache()
 
-    hostinc = None
-    if rank == 0 and world == 1 and args.host_inclusive and data.numel() <= (8 << 30):
-        ser, ovl = host_inclusive(torch, ctx, data, cfg, dt, missing)
-        hostinc = {"serial_GBps": round(ser, 2), "overlapped_GBps": round(ovl, 2),
-                   "path": "pinned host -> H2D (16 slices, copy stream) -> fused reduce "
-                           "(compute stream) -> D2H 32 B"}
-
-    fileinc = None
-    if rank == 0 and world == 1 and args.file_inclusive and data.numel() <= (8 << 30):
-        gbs, sec = file_inclusive(torch, ctx, data, cfg, dt, missing)
-        fileinc = {"GBps": round(gbs, 2), "s_per_pass": round(sec, 4),
-                   "path": "chunk-major file in page cache -> pyas_read_ranges (16 pread threads, "
-                           "16 x 64 MiB pinned slots, H2D as slots fill) -> fused reduce -> D2H 32 B"}
+    extra = {}
+    names = [] if args.extra in ("", "none") else [c.strip() for c in args.extra.split(",")]
+    for name in names:
+        if name not in CONFIGS:
+            raise SystemExit(f"bench.py: unknown --extra config {name!r}")
+        rep, _ = run_config(env, name, "strong", args.extra_steps, 2, args)
+        rep.pop("check", None)
+        extra[f"{name}_strong"] = rep
 
     if rank == 0:
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "metric": METRIC, "value": head["value"], "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
-            "dtype": "f64" if dt.itemsize == 8 else "f32", "data": "synthetic",
-            "config": {"workload": f"{args.config}: {cfg['desc']}", "variable": list(gshape),
-                       "chunk_shape": list(cfg["chunks"]), "chunks_rank0": n_chunks,
-                       "bytes_rank0": bytes_per_launch, "parallelism": f"chunk-shard x{world}",
+            "dtype": head["dtype"], "data": "synthetic",
+            "config": {"workload": f"{args.config}: {cfg['desc']}", "variable": head["variable"],
+                       "chunk_shape": head["chunk_shape"], "chunks_total": head["chunks_total"],
+                       "chunks_rank0": head["chunks_rank0"], "bytes_rank0": head["bytes_rank0"],
+                       "parallelism": f"chunk-shard x{world}",
                        "methods": "sum,count,min,max in one pass (mean = sum/count)"},
-            "chunks_per_s": round(chunks_per_s, 1),
+            "chunks_per_s": head["chunks_per_s"],
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": "pyas::k_reduce",
-                         "kernel_ms_avg": round(kern_ms, 5), "kernel_ms_avg_max_rank": round(kern_ms_max, 5),
-                         "bytes_per_launch": bytes_per_launch},
+                         "traffic": traffic,
+                         "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                                           "pass of this config, per launch)",
+                         "kernel": "pyas::k_reduce", "kernel_ms_avg": head["kernel_ms_rank0"],
+                         "bytes_per_launch": head["bytes_rank0"]},
+            "per_rank": head["per_rank"],
             "cpu_baseline": cpu,
-            "result": result, "check": check, "host_inclusive": hostinc,
-            "file_inclusive": fileinc,
+            "result": head["result"], "check": head["check"], "selfcheck": head["selfcheck"],
+            "host_inclusive": hostinc, "file_inclusive": fileinc,
+            "extra": extra or None,
         }
         print(json.dumps(line), flush=True)
     if use_dist:

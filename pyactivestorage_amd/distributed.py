@@ -43,6 +43,25 @@ def equal_ranges(n_chunks: int, world: int):
     return shard_ranges(np.ones(n_chunks), world)
 
 
+def fold_partials_host(parts: np.ndarray) -> np.ndarray:
+    """Host statement of the rank-order fold (``k_combine``'s semantics on
+    a handful of 32-byte partials): sums added in order, counts added,
+    min/max over partials with count > 0.  Used where no device is present
+    (the CPU launcher rehearsal); the GPU path folds with
+    :func:`device_combine`."""
+    tot = np.zeros(1, dtype=parts.dtype)
+    s = parts["sum"].dtype.type(0)
+    for v in parts["sum"]:
+        s = s + v
+    tot["sum"] = s
+    tot["count"] = parts["count"].sum()
+    valid = parts["count"] > 0
+    if valid.any():
+        tot["min"] = parts["min"][valid].min()
+        tot["max"] = parts["max"][valid].max()
+    return tot
+
+
 def exchange_partials(torch, local_total, group=None):
     """All-gather the 32-byte per-rank partial (uint8 tensor) over the
     process group (RCCL for CUDA tensors, gloo for CPU tensors).  Returns a
@@ -61,14 +80,16 @@ def device_combine(ctx, dtype, gathered, out, stream):
     engine.combine_partials(ctx, dtype, gathered.data_ptr(), world, out.data_ptr(), False, stream)
 
 
-def reduce_sharded(torch, plan, ctx, stream, final, group=None, combine=None):
+def reduce_sharded(torch, plan, ctx, stream, final, group=None, combine=None, launch=True):
     """One sharded step: local fused reduce -> RCCL all-gather -> combine.
 
     ``plan`` is this rank's :class:`~pyactivestorage_amd.batch.ReductionPlan`
     over its chunk range; ``final`` a 32-byte uint8 device tensor that
     receives the global partial.  ``combine`` defaults to the device kernel.
+    ``launch=False`` skips the local reduce (the caller already queued it).
     """
-    plan.launch(stream, chunk_partials=False)
+    if launch:
+        plan.launch(stream, chunk_partials=False)
     local = plan.total_tensor(torch)
     gathered = exchange_partials(torch, local, group)
     (combine or device_combine)(ctx, plan.dtype, gathered, final, stream)

@@ -12,6 +12,8 @@ from __future__ import annotations
 
 import numpy as np
 
+FILL_BLOCK = 64  # chunks per independently seeded fill-planting block
+
 
 def chunk_grid(shape, chunks):
     return tuple(-(-s // c) for s, c in zip(shape, chunks))
@@ -72,11 +74,19 @@ def chunk_major_device(torch, shape, chunks, dtype, device, chunk_range=None, fi
         vals[b0:b1] = v.to(torch.float64).to(tdt)
     n_fill = 0
     if fill is not None and fill_frac > 0 and nch:
-        rng = np.random.default_rng(seed)
-        total = nch * celems
-        n_fill = int(total * fill_frac)
-        pos = torch.from_numpy(rng.integers(0, total, size=n_fill, dtype=np.int64)).to(device)
-        vals.view(-1)[pos] = torch.tensor(fill, dtype=tdt, device=device)
+        # planted per block of FILL_BLOCK chunks, seeded by (seed, global block
+        # index): a chunk's bytes do not depend on how the chunk list is
+        # sharded, so a strong-scaling run at any N reduces the same variable
+        fv = torch.tensor(fill, dtype=tdt, device=device)
+        flat = vals.view(-1)
+        per = int(FILL_BLOCK * celems * fill_frac)
+        for blk in range(lo // FILL_BLOCK, -(-hi // FILL_BLOCK)):
+            rng = np.random.default_rng([seed, blk])
+            pos = rng.integers(0, FILL_BLOCK * celems, size=per, dtype=np.int64)
+            pos += (blk * FILL_BLOCK - lo) * celems
+            pos = pos[(pos >= 0) & (pos < nch * celems)]
+            n_fill += pos.size
+            flat[torch.from_numpy(pos).to(device)] = fv
     if shuffle and es > 1 and nch:
         for b0 in range(0, nch, batch):  # in place, batch by batch
             b1 = min(nch, b0 + batch)
