@@ -375,6 +375,53 @@ int pyas_read_ranges(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offse
  * memory (default 16 x 64 MiB; each slot is pinned on first use). */
 int pyas_ctx_set_ingest_slots(pyas_ctx *ctx, int32_t n_slots, int64_t slot_bytes);
 
+/* ---- per-chunk drop-in, coalesced across threads ------------------------- */
+/* The reference's Active._from_storage calls reduce_chunk once per chunk from
+ * a 30-thread pool (active.py:556-589 -> :765-776 -> storage.py:8-104), each
+ * call opening the file and reading its chunk (storage.py:51-53,156-162).
+ * pyas_coalesced_reduce is that per-chunk call, thread-safe and blocking: the
+ * calling thread preads its chunk into a pinned ring shared by all callers,
+ * and a dispatcher thread reduces every chunk whose read has completed in one
+ * H2D copy, one zlib-inflate launch and one reduce launch per (layout, mask,
+ * axes) group, then wakes the callers.  Same per-chunk results as
+ * pyas_reduce_chunks / pyas_reduce_axes on that chunk. */
+typedef struct {
+    int32_t dtype;                     /* pyas_dtype */
+    int32_t byteswap;                  /* 1: stored non-native (big-endian) */
+    int32_t shuffle;                   /* fused HDF5 shuffle (== itemsize) or 0 */
+    int32_t ndim;
+    int64_t chunk_shape[PYAS_MAX_DIMS];
+    int32_t zlib;                      /* 1: the file bytes are one zlib stream
+                                          (hdf2numcodec.py:34-35, storage.py:119-120) */
+    uint32_t axes_mask;                /* chunk dims reduced (all dims: one partial) */
+} pyas_chunk_desc;
+
+typedef struct pyas_coalescer pyas_coalescer;
+
+/* ring_bytes: pinned host ring + device mirror (0 = 256 MiB); max_batch:
+ * most chunks per dispatch (0 = 4096).  Starts the dispatcher thread. */
+int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch,
+                          pyas_coalescer **out);
+int pyas_coalescer_destroy(pyas_coalescer *c);
+/* stats (int64[6]): batches dispatched, chunks reduced, largest batch,
+ * dispatcher busy ns, callers' file-read ns, callers' wait-for-batch ns */
+int pyas_coalescer_stats(pyas_coalescer *c, int64_t *stats);
+/* Reduce file `path` bytes [offset, offset + size) as one chunk described by
+ * desc/mask (mask without vector tables), selection `sel` (host
+ * [PYAS_MAX_DIMS*3] as in pyas_batch, NULL = whole chunk) with `pool`
+ * (host, pool_len entries) for listed dims.  `out` (host) receives n_out
+ * partials (n_out must equal the kept selected extents' product, 1 when
+ * every dim is reduced).  info (host int64[3]): bytes read (or -errno if the
+ * open failed), inflate status, inflated size.  Returns PYAS_OK, or
+ * PYAS_EIO for an open/read failure, short read or failed/mis-sized inflate,
+ * PYAS_ENOTSUP for what the coalescer does not take (vector mask tables, a
+ * chunk larger than the ring, uncompressed size != chunk bytes): the caller
+ * then runs the per-call path, which raises the reference's exact error. */
+int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, int64_t size,
+                          const pyas_chunk_desc *desc, const pyas_mask *mask,
+                          const int32_t *sel, const int32_t *pool, int32_t pool_len,
+                          int64_t n_out, pyas_partial *out, int64_t *info);
+
 /* ---- measurement ---------------------------------------------------------- */
 /* When enabled, the main reduce kernel of each pyas_reduce_chunks call is
  * bracketed by HIP events on the launch stream (up to max_launches calls). */

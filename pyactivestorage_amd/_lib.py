@@ -89,6 +89,19 @@ class Scatter(ctypes.Structure):
     ]
 
 
+class ChunkDesc(ctypes.Structure):
+    """pyas_chunk_desc: one chunk's layout for pyas_coalesced_reduce."""
+    _fields_ = [
+        ("dtype", ctypes.c_int32),
+        ("byteswap", ctypes.c_int32),
+        ("shuffle", ctypes.c_int32),
+        ("ndim", ctypes.c_int32),
+        ("chunk_shape", ctypes.c_int64 * MAX_DIMS),
+        ("zlib", ctypes.c_int32),
+        ("axes_mask", ctypes.c_uint32),
+    ]
+
+
 PARTIAL_NBYTES = ctypes.sizeof(Partial)
 assert PARTIAL_NBYTES == 32
 
@@ -135,6 +148,11 @@ SIGNATURES = {
     "pyas_inflate": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "pyas_read_ranges": [_vp, ctypes.c_int, _i64, _vp, _vp, _vp, _vp, _i32, _vp],
     "pyas_ctx_set_ingest_slots": [_vp, _i32, _i64],
+    "pyas_coalescer_create": [_vp, _i64, _i32, ctypes.POINTER(_vp)],
+    "pyas_coalescer_destroy": [_vp],
+    "pyas_coalescer_stats": [_vp, _vp],
+    "pyas_coalesced_reduce": [_vp, ctypes.c_char_p, _i64, _i64, ctypes.POINTER(ChunkDesc), ctypes.POINTER(Mask),
+                              _vp, _vp, _i32, _i64, _vp, _vp],
     "pyas_timing_enable": [_vp, _i32],
     "pyas_timing_read": [_vp, ctypes.POINTER(ctypes.c_float), _i32, ctypes.POINTER(_i32)],
 }

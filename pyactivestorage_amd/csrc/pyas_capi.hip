@@ -211,6 +211,22 @@ int combine_into(int dtype, const pyas_partial *in, int64_t n, uint32_t flags, p
 
 }  // namespace
 
+namespace pyas {
+
+int set_error(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int ctx_device(const pyas_ctx *ctx) { return ctx->device; }
+
+}  // namespace pyas
+
 extern "C" {
 
 int pyas_abi_version(void) { return PYAS_ABI_VERSION; }

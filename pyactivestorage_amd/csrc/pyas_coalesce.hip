@@ -1,0 +1,617 @@
+// pyas_coalesce.hip — batching runtime behind the per-chunk drop-in.
+//
+// The reference calls reduce_chunk once per chunk from a 30-thread pool
+// (activestorage/active.py:556-589 -> _process_chunk :765-776 ->
+// storage.py:8-104), and every call opens the file and reads its chunk
+// (storage.py:51-53, read_block :156-162).  Run one by one on the GPU, each
+// such call pays its own H2D copy, launches, D2H copy and stream sync: the
+// device would sit idle between tiny launches.
+//
+// Here concurrent calls are coalesced without changing the calling pattern:
+//   caller thread  : open + pread(2) of its chunk straight into a pinned host
+//                    ring (ctypes released the GIL), then sleep;
+//                    and enqueue its H2D copy on the coalescer's stream;
+//   dispatcher     : take the longest prefix of the ring whose reads are done
+//                    (their copies are already queued), inflate
+//                    every zlib stream of the batch in one launch, reduce every
+//                    chunk in one launch per (layout, mask, axes) group, copy
+//                    every partial back in one copy, synchronise once, wake the
+//                    callers.
+// Batches grow with load (callers keep filling the ring while the previous
+// batch runs) and there are no timers.  Anything the batch cannot express —
+// vector mask tables, a chunk larger than the ring, a short read, a zlib
+// failure — is handed back to the caller (PYAS_ENOTSUP / PYAS_EIO / info[])
+// so that the per-call path raises the reference's exact exception.
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pyas.h"
+#include "pyas_internal.hpp"
+
+namespace {
+
+constexpr int64_t kAlign = 256;
+constexpr int64_t kDefaultRing = int64_t(256) << 20;
+
+int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int es_of(int dtype) {
+    switch (dtype) {
+        case PYAS_I8: case PYAS_U8: return 1;
+        case PYAS_I16: case PYAS_U16: return 2;
+        case PYAS_I32: case PYAS_U32: case PYAS_F32: return 4;
+        case PYAS_I64: case PYAS_U64: case PYAS_F64: return 8;
+        default: return 0;
+    }
+}
+
+enum State { RESERVED = 0, FILLED = 1, SKIP = 2, SUBMITTED = 3, DONE = 4 };
+
+// What one launch group shares; compared bytewise (zero-initialised).
+struct Key {
+    pyas_chunk_desc desc;
+    pyas_mask mask;
+};
+
+struct Req {
+    Key key;
+    int32_t sel[PYAS_MAX_DIMS * 3];
+    bool has_sel = false;
+    const int32_t *pool = nullptr;  // caller memory, valid while it waits
+    int32_t pool_len = 0;
+    int64_t ring_off = 0, nbytes = 0, span = 0;
+    int64_t n_out = 0;
+    int64_t chunk_bytes = 0;        // decoded bytes
+    pyas_partial *out = nullptr;    // caller memory
+    int64_t *info = nullptr;
+    int state = RESERVED;
+    int rc = PYAS_OK;
+    std::string err;
+};
+
+struct Group {
+    Key key;
+    std::vector<Req *> reqs;
+};
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    int64_t n = 0;
+    hipError_t ensure(int64_t want) {
+        if (want <= n) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        int64_t m = want < 1024 ? 1024 : want + want / 2;
+        hipError_t e = hipMalloc((void **)&p, (size_t)m * sizeof(T));
+        if (e == hipSuccess) n = m;
+        return e;
+    }
+};
+
+template <typename T>
+struct HostBuf {
+    T *p = nullptr;
+    int64_t n = 0;
+    hipError_t ensure(int64_t want) {
+        if (want <= n) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        int64_t m = want < 1024 ? 1024 : want + want / 2;
+        hipError_t e = hipHostMalloc((void **)&p, (size_t)m * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = m;
+        return e;
+    }
+};
+
+}  // namespace
+
+struct pyas_coalescer {
+    pyas_ctx *ctx = nullptr;
+    int device = 0;
+    int64_t ring_bytes = 0;
+    int32_t max_batch = 4096;
+    uint8_t *hring = nullptr;   // pinned
+    uint8_t *dring = nullptr;   // device mirror (same offsets)
+    int64_t head = 0;           // next free byte
+    std::deque<Req *> fifo;     // reservation order == ring order
+    std::mutex mu;
+    std::condition_variable cv_disp, cv_done, cv_space;
+    std::thread disp;
+    bool stop = false;
+    hipStream_t st = nullptr;
+    hipEvent_t done_ev = nullptr;
+    // dispatcher-only scratch
+    HostBuf<uint8_t> hmeta;
+    DevBuf<uint8_t> dmeta;
+    DevBuf<uint8_t> ddecode;
+    DevBuf<pyas_partial> dout;
+    HostBuf<pyas_partial> hout;
+    HostBuf<int64_t> hinf;      // inflate out_sizes + status, copied back
+    int64_t n_batches = 0, n_chunks = 0, max_seen = 0;
+    int64_t busy_ns = 0, read_ns = 0, wait_ns = 0;   // dispatcher busy; callers reading; callers waiting
+};
+
+namespace {
+
+// Reserve `span` ring bytes (lock held).  Returns the offset or -1 if the
+// request can never fit.
+int64_t ring_reserve(pyas_coalescer *c, std::unique_lock<std::mutex> &lk, int64_t span) {
+    if (span > c->ring_bytes) return -1;
+    for (;;) {
+        if (c->stop) return -1;
+        if (c->fifo.empty()) {       // everything free: restart at 0
+            c->head = span;
+            return 0;
+        }
+        // in use: [front, head) when head > front, else [front, R) + [0, head)
+        // (head == front with requests queued means full)
+        const int64_t front = c->fifo.front()->ring_off;
+        if (c->head > front) {       // free: [head, R) and [0, front)
+            if (c->ring_bytes - c->head >= span) {
+                const int64_t off = c->head;
+                c->head += span;
+                return off;
+            }
+            if (front >= span) {     // wrap
+                c->head = span;
+                return 0;
+            }
+        } else if (c->head < front && front - c->head >= span) {   // free: [head, front)
+            const int64_t off = c->head;
+            c->head += span;
+            return off;
+        }
+        c->cv_space.wait(lk);
+    }
+}
+
+// Host bounds check of one selection row (the device trusts it).
+bool sel_ok(const pyas_chunk_desc &d, const int32_t *sel, const int32_t *pool, int32_t pool_len,
+            int64_t &n_sel_out, uint32_t axes) {
+    int64_t n_out = 1;
+    for (int k = 0; k < PYAS_MAX_DIMS; ++k) {
+        const int64_t ext = k < d.ndim ? d.chunk_shape[k] : 1;
+        const int64_t start = sel ? sel[k * 3 + 0] : 0;
+        const int64_t step = sel ? sel[k * 3 + 1] : 1;
+        const int64_t cnt = sel ? sel[k * 3 + 2] : ext;
+        if (cnt < 0) return false;
+        if (cnt > 0) {
+            if (step != 0) {
+                const int64_t last = start + (cnt - 1) * step;
+                if (start < 0 || start >= ext || last < 0 || last >= ext) return false;
+            } else {
+                if (!pool || start < 0 || start + cnt > pool_len) return false;
+                for (int64_t i = 0; i < cnt; ++i)
+                    if (pool[start + i] < 0 || pool[start + i] >= ext) return false;
+            }
+        }
+        if (k < d.ndim && !((axes >> k) & 1u)) n_out *= cnt;
+    }
+    n_sel_out = n_out;
+    return true;
+}
+
+// Run one batch (no lock held).  Fills each request's rc/out/info.
+void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
+    // groups of identical keys, in first-seen order
+    std::vector<Group> groups;
+    for (Req *r : batch) {
+        if (r->state == SKIP) continue;
+        Group *g = nullptr;
+        for (auto &x : groups)
+            if (std::memcmp(&x.key, &r->key, sizeof(Key)) == 0) { g = &x; break; }
+        if (!g) {
+            groups.push_back(Group{r->key, {}});
+            g = &groups.back();
+        }
+        g->reqs.push_back(r);
+    }
+    auto fail_all = [&](int rc, const std::string &msg) {
+        for (Req *r : batch)
+            if (r->state != SKIP) { r->rc = rc; r->err = msg; }
+    };
+    if (groups.empty()) return;
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) { fail_all(PYAS_EDEVICE, hipGetErrorString(e)); return; }
+
+    // host meta block: per group [offsets n][out_offsets n][src_off n][src_size n]
+    // [dst_off n][dst_cap n] (int64) [sel n*24][pool] (int32); partial bases
+    int64_t meta_bytes = 0, total_out = 0, decode_bytes = 0, n_inf = 0;
+    struct GMeta { int64_t off, sel_off, pool_off, n, pool_len, out_base, dec_base, inf_base; bool any_sel; };
+    std::vector<GMeta> gm(groups.size());
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        Group &g = groups[gi];
+        GMeta &m = gm[gi];
+        m.n = (int64_t)g.reqs.size();
+        m.off = meta_bytes;
+        meta_bytes += 6 * m.n * 8;
+        m.any_sel = false;
+        m.pool_len = 0;
+        for (Req *r : g.reqs) { m.any_sel |= r->has_sel; m.pool_len += r->pool_len; }
+        m.sel_off = meta_bytes;
+        if (m.any_sel) meta_bytes += m.n * PYAS_MAX_DIMS * 3 * 4;
+        m.pool_off = meta_bytes;
+        meta_bytes = align_up(meta_bytes + (m.pool_len > 0 ? m.pool_len : 1) * 4, 16);
+        m.out_base = total_out;
+        for (Req *r : g.reqs) total_out += r->n_out;
+        m.dec_base = decode_bytes;
+        m.inf_base = n_inf;
+        if (g.key.desc.zlib) {
+            for (Req *r : g.reqs) decode_bytes += align_up(r->chunk_bytes, kAlign);
+            n_inf += m.n;
+        }
+    }
+    if ((e = c->hmeta.ensure(meta_bytes)) != hipSuccess || (e = c->dmeta.ensure(meta_bytes)) != hipSuccess ||
+        (e = c->dout.ensure(total_out > 0 ? total_out : 1)) != hipSuccess ||
+        (e = c->hout.ensure(total_out > 0 ? total_out : 1)) != hipSuccess ||
+        (e = c->hinf.ensure(2 * (n_inf > 0 ? n_inf : 1))) != hipSuccess ||
+        (decode_bytes > 0 && (e = c->ddecode.ensure(decode_bytes)) != hipSuccess)) {
+        fail_all(e == hipErrorOutOfMemory ? PYAS_ENOMEM : PYAS_EDEVICE, hipGetErrorString(e));
+        return;
+    }
+    // inflate out_sizes + status: a device-only region after the meta block
+    const int64_t inf_dev_off = align_up(meta_bytes, 16);
+    if (n_inf > 0 && (e = c->dmeta.ensure(inf_dev_off + 2 * n_inf * 8)) != hipSuccess) {
+        fail_all(PYAS_EDEVICE, hipGetErrorString(e));
+        return;
+    }
+    uint8_t *hm = c->hmeta.p;
+    uint8_t *dm = c->dmeta.p;
+    int64_t dec_cursor = 0;
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        Group &g = groups[gi];
+        GMeta &m = gm[gi];
+        int64_t *offs = (int64_t *)(hm + m.off);
+        int64_t *oofs = offs + m.n;
+        int64_t *soff = oofs + m.n, *ssz = soff + m.n, *doff = ssz + m.n, *dcap = doff + m.n;
+        int32_t *sel = (int32_t *)(hm + m.sel_off);
+        int32_t *pool = (int32_t *)(hm + m.pool_off);
+        int64_t ob = m.out_base, pp = 0;
+        for (int64_t i = 0; i < m.n; ++i) {
+            Req *r = g.reqs[i];
+            if (g.key.desc.zlib) {
+                soff[i] = r->ring_off;
+                ssz[i] = r->nbytes;
+                doff[i] = dec_cursor;
+                dcap[i] = r->chunk_bytes;
+                offs[i] = dec_cursor;
+                dec_cursor += align_up(r->chunk_bytes, kAlign);
+            } else {
+                offs[i] = r->ring_off;
+                soff[i] = ssz[i] = doff[i] = dcap[i] = 0;
+            }
+            oofs[i] = ob;
+            ob += r->n_out;
+            if (m.any_sel) {
+                int32_t *row = sel + i * PYAS_MAX_DIMS * 3;
+                if (r->has_sel) {
+                    std::memcpy(row, r->sel, sizeof(r->sel));
+                    for (int k = 0; k < PYAS_MAX_DIMS; ++k)
+                        if (row[k * 3 + 1] == 0) row[k * 3 + 0] += (int32_t)pp;   // pool offset
+                    if (r->pool_len > 0) std::memcpy(pool + pp, r->pool, (size_t)r->pool_len * 4);
+                    pp += r->pool_len;
+                } else {
+                    for (int k = 0; k < PYAS_MAX_DIMS; ++k) {
+                        row[k * 3 + 0] = 0;
+                        row[k * 3 + 1] = 1;
+                        row[k * 3 + 2] = k < g.key.desc.ndim ? (int32_t)g.key.desc.chunk_shape[k] : 1;
+                    }
+                }
+            }
+        }
+        if (m.pool_len == 0) pool[0] = 0;
+    }
+    // 1. the chunk bytes are already on their way: each caller enqueued
+    //    its own H2D copy on c->st right after its read, before it marked
+    //    the request FILLED, so the launches below are ordered after them
+    // 2. meta H2D
+    if ((e = hipMemcpyAsync(dm, hm, (size_t)meta_bytes, hipMemcpyHostToDevice, c->st)) != hipSuccess) {
+        fail_all(PYAS_EDEVICE, hipGetErrorString(e));
+        return;
+    }
+    int64_t *dinf = (int64_t *)(dm + inf_dev_off);   // [out_sizes n_inf][status n_inf (int32 in 8 B slots)]
+    // 3. per group: inflate, reduce
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        Group &g = groups[gi];
+        GMeta &m = gm[gi];
+        const int64_t *d_offs = (const int64_t *)(dm + m.off);
+        const int64_t *d_oofs = d_offs + m.n;
+        const int64_t *d_soff = d_oofs + m.n, *d_ssz = d_soff + m.n, *d_doff = d_ssz + m.n,
+                      *d_dcap = d_doff + m.n;
+        int rc = PYAS_OK;
+        if (g.key.desc.zlib) {
+            rc = pyas_inflate(c->ctx, c->dring, d_soff, d_ssz, m.n, c->ddecode.p, d_doff, d_dcap,
+                              dinf + m.inf_base, (int32_t *)(dinf + n_inf) + m.inf_base, c->st);
+        }
+        pyas_batch b;
+        std::memset(&b, 0, sizeof(b));
+        b.dtype = g.key.desc.dtype;
+        b.byteswap = g.key.desc.byteswap;
+        b.shuffle = g.key.desc.shuffle;
+        b.ndim = g.key.desc.ndim;
+        for (int k = 0; k < PYAS_MAX_DIMS; ++k) b.chunk_shape[k] = g.key.desc.chunk_shape[k];
+        b.n_chunks = m.n;
+        b.data = g.key.desc.zlib ? (const void *)c->ddecode.p : (const void *)c->dring;
+        b.offsets = d_offs;
+        b.sel = m.any_sel ? (const int32_t *)(dm + m.sel_off) : nullptr;
+        b.index_pool = (const int32_t *)(dm + m.pool_off);
+        const uint32_t full = (g.key.desc.ndim >= 32) ? 0xffffffffu : ((1u << g.key.desc.ndim) - 1u);
+        if (rc == PYAS_OK) {
+            if ((g.key.desc.axes_mask & full) == full)
+                rc = pyas_reduce_chunks(c->ctx, &b, &g.key.mask, c->dout.p + m.out_base, nullptr, 0u, c->st);
+            else
+                rc = pyas_reduce_axes(c->ctx, &b, &g.key.mask, g.key.desc.axes_mask, d_oofs, c->dout.p, c->st);
+        }
+        if (rc != PYAS_OK) {
+            const std::string msg = pyas_last_error();
+            for (Req *r : g.reqs) { r->rc = rc; r->err = msg; }
+        }
+    }
+    // 4. partials (and inflate results) back, one sync
+    if (total_out > 0 &&
+        (e = hipMemcpyAsync(c->hout.p, c->dout.p, (size_t)total_out * sizeof(pyas_partial),
+                            hipMemcpyDeviceToHost, c->st)) != hipSuccess) {
+        fail_all(PYAS_EDEVICE, hipGetErrorString(e));
+        return;
+    }
+    if (n_inf > 0 &&
+        (e = hipMemcpyAsync(c->hinf.p, dinf, (size_t)(2 * n_inf) * 8, hipMemcpyDeviceToHost, c->st)) !=
+            hipSuccess) {
+        fail_all(PYAS_EDEVICE, hipGetErrorString(e));
+        return;
+    }
+    // wait for this batch only (callers keep enqueueing copies behind it)
+    if ((e = hipEventRecord(c->done_ev, c->st)) != hipSuccess ||
+        (e = hipEventSynchronize(c->done_ev)) != hipSuccess) {
+        fail_all(PYAS_EDEVICE, hipGetErrorString(e));
+        return;
+    }
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        Group &g = groups[gi];
+        GMeta &m = gm[gi];
+        int64_t ob = m.out_base;
+        for (int64_t i = 0; i < m.n; ++i) {
+            Req *r = g.reqs[i];
+            if (g.key.desc.zlib) {
+                const int64_t osz = c->hinf.p[m.inf_base + i];
+                const int32_t stt = ((int32_t *)(c->hinf.p + n_inf))[m.inf_base + i];
+                r->info[1] = stt;
+                r->info[2] = osz;
+                if (r->rc == PYAS_OK && (stt != PYAS_INFLATE_OK || osz != r->chunk_bytes)) {
+                    r->rc = PYAS_EIO;   // the caller re-runs the per-call path for zlib's exact error
+                    r->err = "inflate failed or size mismatch";
+                }
+            }
+            if (r->rc == PYAS_OK)
+                std::memcpy(r->out, c->hout.p + ob, (size_t)r->n_out * sizeof(pyas_partial));
+            ob += r->n_out;
+        }
+    }
+}
+
+void dispatcher(pyas_coalescer *c) {
+    (void)hipSetDevice(c->device);
+    std::unique_lock<std::mutex> lk(c->mu);
+    for (;;) {
+        c->cv_disp.wait(lk, [&] {
+            return (c->stop && c->fifo.empty()) ||
+                   (!c->fifo.empty() && c->fifo.front()->state != RESERVED);
+        });
+        if (c->fifo.empty()) break;   // stopping, nothing queued
+        std::vector<Req *> batch;
+        for (Req *r : c->fifo) {
+            if ((int32_t)batch.size() >= c->max_batch) break;
+            if (r->state != FILLED && r->state != SKIP) break;
+            batch.push_back(r);
+        }
+        for (Req *r : batch)
+            if (r->state == FILLED) r->state = SUBMITTED;
+        lk.unlock();
+        const int64_t t0 = now_ns();
+        run_batch(c, batch);
+        const int64_t t1 = now_ns();
+        lk.lock();
+        c->busy_ns += t1 - t0;
+        int64_t nch = 0;
+        for (Req *r : batch) {
+            if (r->state == SUBMITTED) ++nch;
+            r->state = DONE;
+        }
+        for (size_t i = 0; i < batch.size(); ++i) c->fifo.pop_front();
+        c->n_batches += 1;
+        c->n_chunks += nch;
+        if (nch > c->max_seen) c->max_seen = nch;
+        c->cv_done.notify_all();
+        c->cv_space.notify_all();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch, pyas_coalescer **out) {
+    if (!ctx || !out) return pyas::set_error(PYAS_EINVAL, "NULL argument");
+    if (ring_bytes < 0 || max_batch < 0) return pyas::set_error(PYAS_EINVAL, "negative ring size or batch");
+    pyas_coalescer *c = new pyas_coalescer();
+    c->ctx = ctx;
+    c->device = pyas::ctx_device(ctx);
+    c->ring_bytes = align_up(ring_bytes > 0 ? ring_bytes : kDefaultRing, kAlign);
+    c->max_batch = max_batch > 0 ? max_batch : 4096;
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&c->hring, (size_t)c->ring_bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void **)&c->dring, (size_t)c->ring_bytes);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        if (c->hring) (void)hipHostFree(c->hring);
+        if (c->dring) (void)hipFree(c->dring);
+        delete c;
+        return pyas::set_error(e == hipErrorOutOfMemory ? PYAS_ENOMEM : PYAS_EDEVICE, hipGetErrorString(e));
+    }
+    c->disp = std::thread(dispatcher, c);
+    *out = c;
+    return PYAS_OK;
+}
+
+int pyas_coalescer_destroy(pyas_coalescer *c) {
+    if (!c) return PYAS_OK;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->stop = true;
+    }
+    c->cv_disp.notify_all();
+    c->cv_space.notify_all();
+    if (c->disp.joinable()) c->disp.join();
+    (void)hipSetDevice(c->device);
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    if (c->st) (void)hipStreamDestroy(c->st);
+    if (c->done_ev) (void)hipEventDestroy(c->done_ev);
+    (void)hipHostFree(c->hring);
+    (void)hipFree(c->dring);
+    if (c->hmeta.p) (void)hipHostFree(c->hmeta.p);
+    if (c->hout.p) (void)hipHostFree(c->hout.p);
+    if (c->hinf.p) (void)hipHostFree(c->hinf.p);
+    if (c->dmeta.p) (void)hipFree(c->dmeta.p);
+    if (c->ddecode.p) (void)hipFree(c->ddecode.p);
+    if (c->dout.p) (void)hipFree(c->dout.p);
+    delete c;
+    return PYAS_OK;
+}
+
+int pyas_coalescer_stats(pyas_coalescer *c, int64_t *stats) {
+    if (!c || !stats) return pyas::set_error(PYAS_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    stats[0] = c->n_batches;
+    stats[1] = c->n_chunks;
+    stats[2] = c->max_seen;
+    stats[3] = c->busy_ns;
+    stats[4] = c->read_ns;
+    stats[5] = c->wait_ns;
+    return PYAS_OK;
+}
+
+int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, int64_t size,
+                          const pyas_chunk_desc *desc, const pyas_mask *mask, const int32_t *sel,
+                          const int32_t *pool, int32_t pool_len, int64_t n_out, pyas_partial *out,
+                          int64_t *info) {
+    if (!c || !path || !desc || !mask || !out || !info) return pyas::set_error(PYAS_EINVAL, "NULL argument");
+    info[0] = info[1] = info[2] = 0;
+    const int es = es_of(desc->dtype);
+    if (es == 0) return pyas::set_error(PYAS_ENOTSUP, "unsupported dtype code %d", desc->dtype);
+    if (desc->ndim < 1 || desc->ndim > PYAS_MAX_DIMS) return pyas::set_error(PYAS_EINVAL, "bad chunk rank");
+    if (mask->flags & (PYAS_MASK_TAB0 | PYAS_MASK_TAB1))
+        return pyas::set_error(PYAS_ENOTSUP, "vector mask tables are not coalesced");
+    if (desc->axes_mask >> desc->ndim) return pyas::set_error(PYAS_EINVAL, "axes beyond the chunk rank");
+    if (offset < 0 || size < 0) return pyas::set_error(PYAS_EINVAL, "negative offset/size");
+    Req r;
+    std::memset(&r.key, 0, sizeof(r.key));
+    std::memcpy(&r.key.desc, desc, sizeof(*desc));
+    std::memcpy(&r.key.mask, mask, sizeof(*mask));
+    int64_t elems = 1;
+    for (int k = 0; k < desc->ndim; ++k) {
+        if (desc->chunk_shape[k] <= 0) return pyas::set_error(PYAS_EINVAL, "bad chunk shape");
+        elems *= desc->chunk_shape[k];
+    }
+    for (int k = desc->ndim; k < PYAS_MAX_DIMS; ++k) r.key.desc.chunk_shape[k] = 0;
+    r.chunk_bytes = elems * es;
+    if (!desc->zlib && size != r.chunk_bytes)
+        return pyas::set_error(PYAS_ENOTSUP, "size %lld is not the chunk's %lld bytes", (long long)size,
+                               (long long)r.chunk_bytes);
+    int64_t n_sel_out = 0;
+    if (!sel_ok(*desc, sel, pool, pool_len, n_sel_out, desc->axes_mask))
+        return pyas::set_error(PYAS_EINDEX, "selection reaches outside the chunk");
+    if (n_sel_out != n_out) return pyas::set_error(PYAS_EINVAL, "n_out %lld != selection's %lld",
+                                                   (long long)n_out, (long long)n_sel_out);
+    if (sel) {
+        r.has_sel = true;
+        std::memcpy(r.sel, sel, sizeof(r.sel));
+    }
+    r.pool = pool;
+    r.pool_len = sel ? pool_len : 0;
+    r.n_out = n_out;
+    r.out = out;
+    r.info = info;
+    r.nbytes = size;
+    r.span = align_up(size > 0 ? size : 1, kAlign);
+    if (r.span > c->ring_bytes) return pyas::set_error(PYAS_ENOTSUP, "chunk larger than the coalescing ring");
+
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+        info[0] = -errno;
+        return pyas::set_error(PYAS_EIO, "open failed: %s", strerror(errno));
+    }
+    std::unique_lock<std::mutex> lk(c->mu);
+    const int64_t off = ring_reserve(c, lk, r.span);
+    if (off < 0) {
+        lk.unlock();
+        close(fd);
+        return pyas::set_error(PYAS_EDEVICE, "coalescer stopped");
+    }
+    r.ring_off = off;
+    r.state = RESERVED;
+    c->fifo.push_back(&r);
+    lk.unlock();
+
+    const int64_t t_read = now_ns();
+    int64_t got = 0;
+    int read_errno = 0;
+    while (got < size) {
+        const ssize_t k = pread(fd, c->hring + off + got, (size_t)(size - got), (off_t)(offset + got));
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            read_errno = errno;
+            break;
+        }
+        if (k == 0) break;
+        got += k;
+    }
+    close(fd);
+    info[0] = got;
+    hipError_t ce = hipSuccess;
+    if (got == size && !read_errno && size > 0) {
+        // this chunk's H2D copy, issued by the caller so that copies overlap
+        // other callers' reads; ordered before the batch's launches on c->st
+        ce = hipSetDevice(c->device);
+        if (ce == hipSuccess)
+            ce = hipMemcpyAsync(c->dring + off, c->hring + off, (size_t)size, hipMemcpyHostToDevice, c->st);
+    }
+
+    const int64_t t_wait = now_ns();
+    lk.lock();
+    r.state = (got == size && !read_errno && ce == hipSuccess) ? FILLED : SKIP;
+    if (r.state == SKIP) r.rc = ce == hipSuccess ? PYAS_EIO : PYAS_EDEVICE;
+    if (ce != hipSuccess) r.err = hipGetErrorString(ce);
+    c->cv_disp.notify_one();
+    c->cv_done.wait(lk, [&] { return r.state == DONE; });
+    c->read_ns += t_wait - t_read;
+    c->wait_ns += now_ns() - t_wait;
+    lk.unlock();
+    if (r.rc != PYAS_OK) {
+        if (r.err.empty()) r.err = read_errno ? strerror(read_errno) : "short read";
+        return pyas::set_error(r.rc, "%s", r.err.c_str());
+    }
+    return PYAS_OK;
+}
+
+}  // extern "C"

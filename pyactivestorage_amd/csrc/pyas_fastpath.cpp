@@ -1,0 +1,421 @@
+// pyas_fastpath.cpp — CPython hot path of the per-chunk drop-in.
+//
+// The reference's Active._from_storage calls reduce_chunk once per chunk from
+// a 30-thread pool (activestorage/active.py:556-589 -> :765-776 ->
+// storage.py:8-104).  Behind pyas_coalesced_reduce the GPU side of such a call
+// costs a few microseconds of dispatcher time; what limits the pattern is the
+// Python work each call does while holding the GIL.  This module is that
+// work in C: it recognises a call it has seen before (same missing / dtype /
+// compression / filters / shape / method objects, same order, same slice
+// selection and axis), releases the GIL for the coalesced call, and builds
+// the reference's return objects with the NumPy C API:
+//   tmp = method(chunk[sel] masked, axis=all, keepdims=True)   (storage.py:99-100)
+//   N   = np.ma.count(..., keepdims=True)                        (storage.py:98)
+// A call it has not seen returns None; pyactivestorage_amd.storage then plans
+// it in Python, runs it, and registers the plan here for the next chunk.
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
+#include <numpy/arrayobject.h>
+
+#include <cstdint>
+#include <cstring>
+#include <unordered_map>
+#include <vector>
+
+#include "pyas.h"
+
+namespace {
+
+typedef int (*reduce_fn_t)(pyas_coalescer *, const char *, int64_t, int64_t, const pyas_chunk_desc *,
+                           const pyas_mask *, const int32_t *, const int32_t *, int32_t, int64_t,
+                           pyas_partial *, int64_t *);
+
+reduce_fn_t g_fn = nullptr;
+pyas_coalescer *g_co = nullptr;
+PyTypeObject *g_ma_type = nullptr;
+PyObject *g_str_mask = nullptr, *g_str_shared = nullptr;
+
+constexpr int kMaxEntries = 4096;
+
+// key of one call shape (everything but rfile/offset/size)
+struct Key {
+    PyObject *missing, *compression, *filters, *shape, *method;
+    uint64_t dtype;                          // np.dtype by value, anything else by identity
+    int order;                               // 'C' / 'F'
+    int nsel;                                // slices in the selection
+    Py_ssize_t sel[3 * PYAS_MAX_DIMS];       // PySlice_Unpack'ed (start, stop, step)
+    int axis_kind;                           // 0 None, 1 int, 2 sequence
+    int naxis;
+    long axis[PYAS_MAX_DIMS];
+};
+
+struct Result {
+    int nd;                                  // ndim of the keepdims result
+    int kind;                                // 0 sum, 1 min, 2 max
+    bool is_ma, has_rule;
+    int64_t n_sel;
+    int vclass;                              // partial class: 0 f, 1 i, 2 u
+    int typenum;                             // result dtype (native)
+};
+
+struct Entry {
+    Key key;
+    PyObject *dtype_ref;
+    pyas_chunk_desc desc;
+    pyas_mask mask;
+    bool has_sel;
+    int32_t sel[PYAS_MAX_DIMS * 3];
+    std::vector<int32_t> pool;
+    Result res;
+};
+
+uint64_t dtype_key(PyObject *dt) {
+    if (PyArray_DescrCheck(dt)) {
+        PyArray_Descr *d = (PyArray_Descr *)dt;
+        if (!PyDataType_HASFIELDS(d) && !PyDataType_HASSUBARRAY(d))
+            return (1ull << 63) | ((uint64_t)d->type_num << 16) | ((uint64_t)(unsigned char)d->byteorder << 8) |
+                   (uint64_t)(unsigned char)d->kind;
+    }
+    return (uint64_t)(uintptr_t)dt;
+}
+
+std::unordered_map<uint64_t, std::vector<Entry *>> g_cache;
+size_t g_n = 0;
+
+uint64_t mix(uint64_t h, uint64_t v) {
+    h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+    return h;
+}
+
+// Parse the non-identity parts of the key.  Returns false (no exception set)
+// when the call is not of a cacheable shape.
+bool parse_key(PyObject *order, PyObject *sel, PyObject *axis, Key &k) {
+    if (!PyUnicode_Check(order) || PyUnicode_GET_LENGTH(order) != 1) return false;
+    k.order = (int)PyUnicode_READ_CHAR(order, 0);
+    if (k.order != 'C' && k.order != 'F') return false;
+    PyObject *const *items;
+    Py_ssize_t n;
+    if (PyTuple_Check(sel)) {
+        items = &PyTuple_GET_ITEM(sel, 0);
+        n = PyTuple_GET_SIZE(sel);
+    } else if (PySlice_Check(sel)) {
+        items = &sel;
+        n = 1;
+    } else {
+        return false;
+    }
+    if (n < 1 || n > PYAS_MAX_DIMS) return false;
+    k.nsel = (int)n;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        if (!PySlice_Check(items[i])) return false;
+        Py_ssize_t a, b, c;
+        if (PySlice_Unpack(items[i], &a, &b, &c) < 0) {
+            PyErr_Clear();
+            return false;
+        }
+        k.sel[3 * i] = a;
+        k.sel[3 * i + 1] = b;
+        k.sel[3 * i + 2] = c;
+    }
+    if (axis == Py_None) {
+        k.axis_kind = 0;
+        k.naxis = 0;
+    } else if (PyLong_CheckExact(axis)) {
+        k.axis_kind = 1;
+        k.naxis = 1;
+        k.axis[0] = PyLong_AsLong(axis);
+        if (k.axis[0] == -1 && PyErr_Occurred()) { PyErr_Clear(); return false; }
+    } else if (PyTuple_Check(axis)) {
+        Py_ssize_t m = PyTuple_GET_SIZE(axis);
+        if (m > PYAS_MAX_DIMS) return false;
+        k.axis_kind = 2;
+        k.naxis = (int)m;
+        for (Py_ssize_t i = 0; i < m; ++i) {
+            PyObject *v = PyTuple_GET_ITEM(axis, i);
+            if (!PyLong_CheckExact(v)) return false;
+            k.axis[i] = PyLong_AsLong(v);
+            if (k.axis[i] == -1 && PyErr_Occurred()) { PyErr_Clear(); return false; }
+        }
+    } else {
+        return false;
+    }
+    return true;
+}
+
+uint64_t hash_key(const Key &k) {
+    uint64_t h = 1469598103934665603ull;
+    h = mix(h, (uint64_t)(uintptr_t)k.missing);
+    h = mix(h, k.dtype);
+    h = mix(h, (uint64_t)(uintptr_t)k.compression);
+    h = mix(h, (uint64_t)(uintptr_t)k.filters);
+    h = mix(h, (uint64_t)(uintptr_t)k.shape);
+    h = mix(h, (uint64_t)(uintptr_t)k.method);
+    h = mix(h, (uint64_t)k.order);
+    h = mix(h, (uint64_t)k.nsel);
+    for (int i = 0; i < 3 * k.nsel; ++i) h = mix(h, (uint64_t)k.sel[i]);
+    h = mix(h, (uint64_t)k.axis_kind);
+    for (int i = 0; i < k.naxis; ++i) h = mix(h, (uint64_t)k.axis[i]);
+    return h;
+}
+
+bool same_key(const Key &a, const Key &b) {
+    if (a.missing != b.missing || a.dtype != b.dtype || a.compression != b.compression ||
+        a.filters != b.filters || a.shape != b.shape || a.method != b.method || a.order != b.order ||
+        a.nsel != b.nsel || a.axis_kind != b.axis_kind || a.naxis != b.naxis)
+        return false;
+    for (int i = 0; i < 3 * a.nsel; ++i)
+        if (a.sel[i] != b.sel[i]) return false;
+    for (int i = 0; i < a.naxis; ++i)
+        if (a.axis[i] != b.axis[i]) return false;
+    return true;
+}
+
+void free_entry(Entry *e) {
+    Py_XDECREF(e->key.missing);
+    Py_XDECREF(e->dtype_ref);
+    Py_XDECREF(e->key.compression);
+    Py_XDECREF(e->key.filters);
+    Py_XDECREF(e->key.shape);
+    Py_XDECREF(e->key.method);
+    delete e;
+}
+
+void clear_cache() {
+    for (auto &kv : g_cache)
+        for (Entry *e : kv.second) free_entry(e);
+    g_cache.clear();
+    g_n = 0;
+}
+
+// np.ma.MaskedArray(vals[, mask=mask]) as the constructor leaves it: a view
+// of vals, _mask = mask (or nomask), _sharedmask = True.
+PyObject *as_masked(PyObject *vals, PyObject *mask) {
+    PyObject *r = PyArray_View((PyArrayObject *)vals, nullptr, g_ma_type);
+    if (!r) return nullptr;
+    if (mask && PyObject_GenericSetAttr(r, g_str_mask, mask) < 0) {
+        Py_DECREF(r);
+        return nullptr;
+    }
+    if (PyObject_GenericSetAttr(r, g_str_shared, Py_True) < 0) {
+        Py_DECREF(r);
+        return nullptr;
+    }
+    return r;
+}
+
+void store_value(void *dst, int typenum, const pyas_scalar &v, int vclass) {
+    switch (typenum) {
+        case NPY_FLOAT32: *(float *)dst = (float)v.f; break;
+        case NPY_FLOAT64: *(double *)dst = v.f; break;
+        case NPY_INT8: *(int8_t *)dst = (int8_t)v.i; break;
+        case NPY_INT16: *(int16_t *)dst = (int16_t)v.i; break;
+        case NPY_INT32: *(int32_t *)dst = (int32_t)v.i; break;
+        case NPY_UINT8: *(uint8_t *)dst = (uint8_t)v.u; break;
+        case NPY_UINT16: *(uint16_t *)dst = (uint16_t)v.u; break;
+        case NPY_UINT32: *(uint32_t *)dst = (uint32_t)v.u; break;
+        default:   // 8-byte ints (NPY_LONG / NPY_LONGLONG and unsigned)
+            if (vclass == 2) *(uint64_t *)dst = v.u;
+            else *(int64_t *)dst = v.i;
+            break;
+    }
+}
+
+PyObject *build(const Result &e, const pyas_partial &p) {
+    npy_intp dims[PYAS_MAX_DIMS];
+    for (int i = 0; i < e.nd; ++i) dims[i] = 1;
+    PyObject *count = PyArray_SimpleNew(e.nd, dims, NPY_INT64);
+    if (!count) return nullptr;
+    *(int64_t *)PyArray_DATA((PyArrayObject *)count) = p.count;
+    PyObject *vals = PyArray_SimpleNew(e.nd, dims, e.typenum);
+    if (!vals) { Py_DECREF(count); return nullptr; }
+    const pyas_scalar &v = e.kind == 0 ? p.sum : (e.kind == 1 ? p.min : p.max);
+    store_value(PyArray_DATA((PyArrayObject *)vals), e.typenum, v, e.vclass);
+    PyObject *tmp = vals;
+    if (e.has_rule && p.count < e.n_sel) {
+        PyObject *mask = PyArray_SimpleNew(e.nd, dims, NPY_BOOL);
+        if (!mask) { Py_DECREF(vals); Py_DECREF(count); return nullptr; }
+        *(npy_bool *)PyArray_DATA((PyArrayObject *)mask) = p.count == 0;
+        tmp = as_masked(vals, mask);
+        Py_DECREF(mask);
+        Py_DECREF(vals);
+    } else if (e.has_rule || e.is_ma) {
+        tmp = as_masked(vals, nullptr);
+        Py_DECREF(vals);
+    }
+    if (!tmp) { Py_DECREF(count); return nullptr; }
+    PyObject *res = PyTuple_Pack(2, tmp, count);
+    Py_DECREF(tmp);
+    Py_DECREF(count);
+    return res;
+}
+
+// reduce(rfile, offset, size, compression, filters, missing, dtype, shape,
+//        order, chunk_selection, axis, method) -> (tmp, N) or None
+PyObject *py_reduce(PyObject *, PyObject *const *a, Py_ssize_t n) {
+    if (n != 12) {
+        PyErr_SetString(PyExc_TypeError, "reduce() takes 12 arguments");
+        return nullptr;
+    }
+    if (!g_fn || !g_co) Py_RETURN_NONE;
+    Key k;
+    k.compression = a[3];
+    k.filters = a[4];
+    k.missing = a[5];
+    k.dtype = dtype_key(a[6]);
+    k.shape = a[7];
+    k.method = a[11];
+    if (!parse_key(a[8], a[9], a[10], k)) Py_RETURN_NONE;
+    auto it = g_cache.find(hash_key(k));
+    if (it == g_cache.end()) Py_RETURN_NONE;
+    const Entry *e = nullptr;
+    for (Entry *x : it->second)
+        if (same_key(x->key, k)) { e = x; break; }
+    if (!e) Py_RETURN_NONE;
+    PyObject *path;
+    if (PyUnicode_Check(a[0])) {
+        path = PyUnicode_EncodeFSDefault(a[0]);
+        if (!path) { PyErr_Clear(); Py_RETURN_NONE; }
+    } else if (PyBytes_Check(a[0])) {
+        path = a[0];
+        Py_INCREF(path);
+    } else {
+        Py_RETURN_NONE;
+    }
+    const long long off = PyLong_AsLongLong(a[1]);
+    const long long size = off == -1 && PyErr_Occurred() ? -1 : PyLong_AsLongLong(a[2]);
+    if (PyErr_Occurred()) {
+        PyErr_Clear();
+        Py_DECREF(path);
+        Py_RETURN_NONE;
+    }
+    // copies: another thread may drop the cache entry while the GIL is released
+    pyas_chunk_desc desc = e->desc;
+    pyas_mask mask = e->mask;
+    int32_t sel[PYAS_MAX_DIMS * 3];
+    std::memcpy(sel, e->sel, sizeof(sel));
+    const bool has_sel = e->has_sel;
+    std::vector<int32_t> pool(e->pool);
+    const Result res = e->res;
+    pyas_partial part;
+    int64_t info[3];
+    const char *cpath = PyBytes_AS_STRING(path);
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = g_fn(g_co, cpath, off, size, &desc, &mask, has_sel ? sel : nullptr,
+              pool.empty() ? nullptr : pool.data(), (int32_t)pool.size(), 1, &part, info);
+    Py_END_ALLOW_THREADS
+    Py_DECREF(path);
+    if (rc != PYAS_OK) Py_RETURN_NONE;   // the Python path re-runs it and raises the reference's error
+    return build(res, part);
+}
+
+// register(missing, dtype, compression, filters, shape, order, chunk_selection,
+//          axis, method, desc: bytes, mask: bytes, sel: bytes|None, pool: bytes,
+//          nd, kind, is_ma, has_rule, n_sel, vclass, typenum) -> bool
+PyObject *py_register(PyObject *, PyObject *args) {
+    PyObject *missing, *dtype, *compression, *filters, *shape, *order, *sel, *axis, *method, *selobj;
+    const char *desc, *mask, *pool;
+    Py_ssize_t ldesc, lmask, lpool;
+    int nd, kind, is_ma, has_rule, vclass, typenum;
+    long long n_sel;
+    if (!PyArg_ParseTuple(args, "OOOOOOOOOy#y#Oy#iippLii", &missing, &dtype, &compression, &filters,
+                          &shape, &order, &sel, &axis, &method, &desc, &ldesc, &mask, &lmask, &selobj,
+                          &pool, &lpool, &nd, &kind, &is_ma, &has_rule, &n_sel, &vclass, &typenum))
+        return nullptr;
+    if (ldesc != (Py_ssize_t)sizeof(pyas_chunk_desc) || lmask != (Py_ssize_t)sizeof(pyas_mask) || nd < 1 ||
+        nd > PYAS_MAX_DIMS || kind < 0 || kind > 2 || lpool % 4 != 0)
+        Py_RETURN_FALSE;
+    const bool have_sel = selobj != Py_None;
+    if (have_sel && (!PyBytes_Check(selobj) || PyBytes_GET_SIZE(selobj) != (Py_ssize_t)(PYAS_MAX_DIMS * 3 * 4)))
+        Py_RETURN_FALSE;
+    Entry *e = new Entry();
+    e->key.missing = missing;
+    e->key.dtype = dtype_key(dtype);
+    e->key.compression = compression;
+    e->key.filters = filters;
+    e->key.shape = shape;
+    e->key.method = method;
+    e->dtype_ref = nullptr;
+    if (!parse_key(order, sel, axis, e->key)) {
+        delete e;
+        Py_RETURN_FALSE;
+    }
+    std::memcpy(&e->desc, desc, sizeof(e->desc));
+    std::memcpy(&e->mask, mask, sizeof(e->mask));
+    e->has_sel = have_sel;
+    if (have_sel) std::memcpy(e->sel, PyBytes_AS_STRING(selobj), sizeof(e->sel));
+    e->pool.assign((const int32_t *)pool, (const int32_t *)pool + lpool / 4);
+    e->res = Result{nd, kind, is_ma != 0, has_rule != 0, (int64_t)n_sel, vclass, typenum};
+    if (g_n >= (size_t)kMaxEntries) clear_cache();
+    Py_INCREF(missing);
+    Py_INCREF(dtype);
+    e->dtype_ref = dtype;
+    Py_INCREF(compression);
+    Py_INCREF(filters);
+    Py_INCREF(shape);
+    Py_INCREF(method);
+    auto &bucket = g_cache[hash_key(e->key)];
+    for (size_t i = 0; i < bucket.size(); ++i) {
+        if (same_key(bucket[i]->key, e->key)) {
+            free_entry(bucket[i]);
+            bucket.erase(bucket.begin() + (long)i);
+            --g_n;
+            break;
+        }
+    }
+    bucket.push_back(e);
+    ++g_n;
+    Py_RETURN_TRUE;
+}
+
+// bind(reduce_fn_address, coalescer_handle, MaskedArray type)
+PyObject *py_bind(PyObject *, PyObject *args) {
+    unsigned long long fn, co;
+    PyObject *ma;
+    if (!PyArg_ParseTuple(args, "KKO", &fn, &co, &ma)) return nullptr;
+    if (!PyType_Check(ma)) {
+        PyErr_SetString(PyExc_TypeError, "MaskedArray type expected");
+        return nullptr;
+    }
+    Py_INCREF(ma);
+    Py_XDECREF((PyObject *)g_ma_type);
+    g_ma_type = (PyTypeObject *)ma;
+    g_fn = (reduce_fn_t)(uintptr_t)fn;
+    g_co = (pyas_coalescer *)(uintptr_t)co;
+    Py_RETURN_NONE;
+}
+
+PyObject *py_clear(PyObject *, PyObject *) {
+    clear_cache();
+    Py_RETURN_NONE;
+}
+
+PyObject *py_size(PyObject *, PyObject *) { return PyLong_FromSize_t(g_n); }
+
+PyMethodDef kMethods[] = {
+    {"reduce", (PyCFunction)(void (*)(void))py_reduce, METH_FASTCALL,
+     "reduce(rfile, offset, size, compression, filters, missing, dtype, shape, order, "
+     "chunk_selection, axis, method) -> (tmp, N) or None when the call shape is not cached"},
+    {"register", py_register, METH_VARARGS, "cache the plan of one call shape"},
+    {"bind", py_bind, METH_VARARGS, "bind(pyas_coalesced_reduce address, coalescer, MaskedArray)"},
+    {"clear", py_clear, METH_NOARGS, "drop every cached plan"},
+    {"size", py_size, METH_NOARGS, "number of cached plans"},
+    {nullptr, nullptr, 0, nullptr},
+};
+
+PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_fastpath",
+                       "CPython hot path of the per-chunk drop-in (pyas_coalesced_reduce)", -1, kMethods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__fastpath(void) {
+    import_array();
+    PyObject *m = PyModule_Create(&kModule);
+    if (!m) return nullptr;
+    g_str_mask = PyUnicode_InternFromString("_mask");
+    g_str_shared = PyUnicode_InternFromString("_sharedmask");
+    PyModule_AddIntConstant(m, "CHUNK_DESC_SIZE", (long)sizeof(pyas_chunk_desc));
+    PyModule_AddIntConstant(m, "MASK_SIZE", (long)sizeof(pyas_mask));
+    return m;
+}

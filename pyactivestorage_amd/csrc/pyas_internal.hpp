@@ -162,6 +162,11 @@ int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const
                 uint8_t *dst, const int64_t *dst_offsets, int32_t threads, hipStream_t st,
                 std::string &msg);
 
+// pyas_capi.hip: the thread-local pyas_last_error() message, and the device a
+// context is bound to (for runtime pieces in other translation units)
+int set_error(int code, const char *fmt, ...);
+int ctx_device(const pyas_ctx *ctx);
+
 hipError_t launch_unshuffle_chunks(const void *src, const int64_t *soff, void *dst, const int64_t *doff,
                                    int64_t n_chunks, int64_t nbytes, int64_t es, hipStream_t st);
 hipError_t launch_unshuffle(const void *src, void *dst, int64_t nbytes, int64_t es,

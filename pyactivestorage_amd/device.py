@@ -1,14 +1,18 @@
 """Device context, streams and device buffers over the C ABI.
 
-One ``Context`` per GPU (process-wide, created lazily).  Every calling thread
-gets its own HIP stream so that concurrent ``reduce_chunk`` calls from the
-reference's 30-thread pool (``activestorage/active.py:557-572``) never share
-scratch memory; the C library keys its scratch by stream.
+One ``Context`` per GPU (process-wide, created lazily).  A calling thread
+that needs its own HIP stream (``Active`` queries, the per-call fallback of
+the drop-in) gets one, plus scratch keyed by that stream in the C library;
+both are released when the thread ends.  The drop-in's common path
+(``storage.reduce_chunk`` from the reference's 30-thread pool,
+``activestorage/active.py:557-572``) instead goes through the context's one
+coalescer (``pyas_coalesced_reduce``) and holds no per-thread device state.
 """
 from __future__ import annotations
 
 import ctypes
 import threading
+import weakref
 
 import numpy as np
 
@@ -47,6 +51,38 @@ class DeviceBuffer:
             pass
 
 
+class _ThreadResources:
+    """What one thread holds on one context: its HIP streams, growable device
+    scratch buffers, pinned staging buffer and the pageable arrays its async
+    copies still read.  Released when the thread ends (its ``threading.local``
+    entry is dropped): the streams are synchronised, the buffers freed and
+    the streams destroyed, which also frees the C library's per-stream scratch.
+    The reference builds a new 30-thread pool per query (active.py:557), so
+    per-thread resources must not outlive their thread."""
+
+    def __init__(self, ctx: "Context"):
+        # the finalizer holds `state`, never `self`
+        self.state = state = {"stream": None, "aux": {}, "bufs": {}, "host": None, "pending": {}}
+        fin = weakref.finalize(self, _release_thread, ctx, state)
+        fin.atexit = False   # at interpreter exit the process releases everything
+
+
+def _release_thread(ctx: "Context", state) -> None:
+    lib, h = ctx.lib, ctx.handle
+    streams = ([state["stream"]] if state["stream"] else []) + list(state["aux"].values())
+    for s in streams:
+        lib.pyas_stream_synchronize(h, s)
+    for b in state["bufs"].values():
+        b.free()
+    if state["host"] is not None:
+        lib.pyas_host_free(h, state["host"][0])
+        ctx._count(pinned=-state["host"][1])
+    for s in streams:
+        lib.pyas_stream_destroy(h, s)
+        ctx._count(streams=-1)
+    state.clear()
+
+
 class Context:
     """A ``pyas_ctx`` bound to one device."""
 
@@ -57,29 +93,42 @@ class Context:
         _lib.check(self.lib.pyas_ctx_create(self.device, ctypes.byref(h)), "pyas_ctx_create")
         self.handle = h.value
         self._tls = threading.local()
+        self._stats_lock = threading.Lock()
+        self.live_streams = 0        # per-thread streams currently alive
+        self.pinned_bytes = 0        # per-thread pinned staging currently alive
+        self._coalescer = None
+
+    def _count(self, streams=0, pinned=0):
+        with self._stats_lock:
+            self.live_streams += streams
+            self.pinned_bytes += pinned
+
+    def _res(self):
+        r = getattr(self._tls, "res", None)
+        if r is None:
+            r = self._tls.res = _ThreadResources(self)
+        return r.state
+
+    def _new_stream(self) -> int:
+        p = ctypes.c_void_p()
+        _lib.check(self.lib.pyas_stream_create(self.handle, ctypes.byref(p)), "pyas_stream_create")
+        self._count(streams=1)
+        return p.value
 
     # -- streams -------------------------------------------------------------
     def thread_stream(self) -> int:
-        s = getattr(self._tls, "stream", None)
-        if s is None:
-            p = ctypes.c_void_p()
-            _lib.check(self.lib.pyas_stream_create(self.handle, ctypes.byref(p)),
-                       "pyas_stream_create")
-            s = self._tls.stream = p.value
-        return s
+        st = self._res()
+        if st["stream"] is None:
+            st["stream"] = self._new_stream()
+        return st["stream"]
 
     def thread_aux_stream(self, k: int = 0) -> int:
         """Extra stream ``k`` of the calling thread (ingest copies and inflate
         groups that overlap device work queued on :meth:`thread_stream`)."""
-        aux = getattr(self._tls, "aux_streams", None)
-        if aux is None:
-            aux = self._tls.aux_streams = {}
+        aux = self._res()["aux"]
         s = aux.get(k)
         if s is None:
-            p = ctypes.c_void_p()
-            _lib.check(self.lib.pyas_stream_create(self.handle, ctypes.byref(p)),
-                       "pyas_stream_create")
-            s = aux[k] = p.value
+            s = aux[k] = self._new_stream()
         return s
 
     def stream_wait(self, waiter: int, waitee: int) -> None:
@@ -88,13 +137,13 @@ class Context:
 
     def synchronize(self, stream: int | None) -> None:
         _lib.check(self.lib.pyas_stream_synchronize(self.handle, stream), "pyas_stream_synchronize")
-        self._tls.pending = []
+        pend = getattr(self._tls, "res", None)
+        if pend is not None:
+            pend.state["pending"].pop(stream, None)
 
     # -- per-thread growable scratch buffers ---------------------------------
     def thread_buffer(self, slot: str, nbytes: int) -> DeviceBuffer:
-        bufs = getattr(self._tls, "bufs", None)
-        if bufs is None:
-            bufs = self._tls.bufs = {}
+        bufs = self._res()["bufs"]
         b = bufs.get(slot)
         if b is None or b.nbytes < nbytes:
             if b is not None:
@@ -107,34 +156,57 @@ class Context:
         """Per-thread pinned host staging (uint8, at least ``nbytes``); H2D
         copies from it are DMA.  Reused by the thread's next call: callers
         synchronize the thread stream before refilling it."""
-        hb = getattr(self._tls, "host_buf", None)
+        st = self._res()
+        hb = st["host"]
         if hb is None or hb[1] < nbytes:
             if hb is not None:
                 self.synchronize(self.thread_stream())
                 _lib.check(self.lib.pyas_host_free(self.handle, hb[0]), "pyas_host_free")
+                self._count(pinned=-hb[1])
+                st["host"] = None
             size = max(int(nbytes), 1 << 20)
             p = ctypes.c_void_p()
             _lib.check(self.lib.pyas_host_alloc(self.handle, size, ctypes.byref(p)), "pyas_host_alloc")
+            self._count(pinned=size)
             arr = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(p.value))
-            hb = self._tls.host_buf = (p.value, size, arr)
+            hb = st["host"] = (p.value, size, arr)
         return hb[2]
 
     # -- copies --------------------------------------------------------------
     def h2d(self, dst_ptr: int, host: np.ndarray, stream: int | None) -> None:
-        """Async copy; the host array is kept alive until the next
-        ``synchronize`` of this thread (HIP may read pageable memory late)."""
+        """Async copy; the host array is kept alive until ``stream`` is next
+        synchronised through this context (HIP may read pageable memory late)."""
         host = np.ascontiguousarray(host)
         _lib.check(self.lib.pyas_memcpy_h2d(self.handle, dst_ptr, host.ctypes.data, host.nbytes, stream),
                    "pyas_memcpy_h2d")
-        pending = getattr(self._tls, "pending", None)
-        if pending is None:
-            pending = self._tls.pending = []
-        pending.append(host)
+        self._res()["pending"].setdefault(stream, []).append(host)
 
     def d2h(self, host: np.ndarray, src_ptr: int, stream: int | None) -> None:
         assert host.flags.c_contiguous
         _lib.check(self.lib.pyas_memcpy_d2h(self.handle, host.ctypes.data, src_ptr, host.nbytes, stream),
                    "pyas_memcpy_d2h")
+
+    # -- the per-chunk drop-in's batching runtime ------------------------------
+    def coalescer(self) -> int:
+        """Handle of this device's ``pyas_coalescer`` (created on first use,
+        lives as long as the process: one dispatcher thread, one pinned ring)."""
+        c = self._coalescer
+        if c is None:
+            with self._stats_lock:
+                if self._coalescer is None:
+                    p = ctypes.c_void_p()
+                    _lib.check(self.lib.pyas_coalescer_create(self.handle, 0, 0, ctypes.byref(p)),
+                               "pyas_coalescer_create")
+                    self._coalescer = p.value
+                c = self._coalescer
+        return c
+
+    def coalescer_stats(self) -> dict:
+        s = (ctypes.c_int64 * 6)()
+        if self._coalescer is not None:
+            _lib.check(self.lib.pyas_coalescer_stats(self._coalescer, s), "pyas_coalescer_stats")
+        return {"batches": s[0], "chunks": s[1], "largest": s[2], "busy_s": s[3] * 1e-9,
+                "read_s": s[4] * 1e-9, "wait_s": s[5] * 1e-9}
 
     def set_tile_bytes(self, nbytes: int) -> None:
         _lib.check(self.lib.pyas_ctx_set_tile_bytes(self.handle, int(nbytes)), "set_tile_bytes")

@@ -20,6 +20,7 @@ import numpy as np
 from .dtypes import mean_dtype, native, sum_dtype
 
 _METHODS = {}
+METHODS = _METHODS   # callable -> (kind, is_ma), for hot-path lookups
 
 
 def _register():
@@ -94,4 +95,36 @@ def build(parts: np.ndarray, kind: str, is_ma: bool, dt, has_rule: bool, n_reduc
         return np.ma.MaskedArray(vals, mask=mask), count
     if has_rule or is_ma:
         return np.ma.MaskedArray(vals), count
+    return vals, count
+
+
+def _ma(vals, mask=None):
+    """``np.ma.MaskedArray(vals[, mask=mask])`` without the constructor's
+    argument handling: a view with the constructor's exact attribute state
+    (``_mask`` the given array or nomask, ``_sharedmask`` True)."""
+    r = vals.view(np.ma.MaskedArray)
+    if mask is not None:
+        r._mask = mask
+    r._sharedmask = True
+    return r
+
+
+def build_one(p, shape, kind: str, is_ma: bool, dt, has_rule: bool, n_reduced: int,
+              n_selected: int):
+    """:func:`build` for ONE partial ``p`` (a structured scalar), i.e. every
+    selected dim reduced: the same objects with a fraction of the overhead
+    (the per-chunk drop-in's common case, storage.py:98-100 with the full
+    axis tuple)."""
+    if kind == "mean" or (kind != "sum" and n_reduced == 0):
+        return build(np.array(p).reshape(shape), kind, is_ma, dt, has_rule, n_reduced, n_selected)
+    cnt = int(p["count"])
+    count = np.array(cnt, dtype=np.int64).reshape(shape)
+    if kind == "sum":
+        vals = np.array(p["sum"], dtype=sum_dtype(dt)).reshape(shape)
+    else:
+        vals = np.array(p[kind], dtype=native(dt)).reshape(shape)
+    if has_rule and cnt < n_selected:
+        return _ma(vals, np.array(cnt == 0).reshape(shape)), count
+    if has_rule or is_ma:
+        return _ma(vals), count
     return vals, count

@@ -19,15 +19,23 @@ reduce every chunk of a query in one launch from device-resident memory.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+import threading
 import zlib
 
 import numpy as np
 
 from . import _lib, engine, results, selection
 from .device import get_context
-from .dtypes import native
+from .dtypes import dtype_code, native, needs_byteswap, sum_dtype
 from .inflate import inflate_chunk, is_zlib
 from .masking import compile_missing
+
+try:   # CPython hot path of the coalesced drop-in (built by csrc/Makefile)
+    from . import _fastpath
+except ImportError:   # pragma: no cover - planning stays in Python, still on the GPU
+    _fastpath = None
 
 __all__ = ["reduce_chunk", "reduce_opens3_chunk", "reduce_chunk_bytes", "filter_pipeline",
            "read_block", "Shuffle", "Zlib"]
@@ -116,6 +124,20 @@ def reduce_chunk(rfile, offset, size, compression, filters, missing, dtype, shap
     the count of unmasked elements, or ``(selected masked data, None)`` when
     ``method`` is None.
     """
+    if COALESCE and method is not None:
+        # 1. a call shape seen before: planned, run and formatted in C
+        #    (pyas_fastpath.cpp -> pyas_coalesced_reduce)
+        if _fastpath is not None:
+            r = _fastpath.reduce(rfile, offset, size, compression, filters, missing, dtype, shape,
+                                 order, chunk_selection, axis, method)
+            if r is not None:
+                return r
+        # 2. plan it here (and register the plan with the C path)
+        if rfile.__class__ is str or isinstance(rfile, (bytes, os.PathLike)):
+            r = _coalesced(rfile, offset, size, compression, filters, missing, dtype, shape, order,
+                           chunk_selection, axis, method)
+            if r is not None:
+                return r
     if hasattr(rfile, "id") and hasattr(rfile.id, "_get_raw_chunk"):
         # pyfive.high_level.Dataset branch (storage.py:88-91)
         class _StoreInfo:
@@ -135,6 +157,234 @@ def reduce_chunk(rfile, offset, size, compression, filters, missing, dtype, shap
                 raw = read_block(fh, offset, size)
     return reduce_chunk_bytes(raw, compression, filters, missing, dtype, shape, order,
                               chunk_selection, axis, method)
+
+
+# ---------------------------------------------------------------------------
+# coalesced per-chunk path (pyas_coalesced_reduce)
+# ---------------------------------------------------------------------------
+# The reference's pool calls reduce_chunk with the same dtype / shape /
+# filters / missing objects for every chunk of a query (active.py:556-589),
+# so everything but the byte range is planned once and looked up by the
+# identity of those objects (the entry keeps them alive and re-checks `is`).
+COALESCE = os.environ.get("PYAS_COALESCE", "1") != "0"
+_PLAN_CAP = 256
+_plans: dict = {}
+_plan_lock = threading.Lock()
+
+
+class _Layout:
+    """Per (dtype, shape, order, filters, compression, missing): the
+    pyas_chunk_desc / pyas_mask pair and the per-(selection, axis) plans."""
+
+    __slots__ = ("refs", "ok", "dt", "pdt", "cm", "mask", "mask_ref", "desc_base", "rev", "shape",
+                 "zlib", "sels")
+
+    def __init__(self, refs, compression, filters, missing, dtype, shape, order):
+        self.refs = refs
+        self.ok = False
+        self.sels = {}
+        dt = self.dt = np.dtype(dtype)
+        self.shape = shape
+        if order not in ("C", "F") or dt.kind not in "iuf":
+            return
+        try:
+            shuffles = _shuffle_sizes(filters)
+        except NotImplementedError:
+            return
+        fused = 0
+        if shuffles:
+            if len(shuffles) != 1 or shuffles[0] != dt.itemsize:
+                return                          # a standalone un-shuffle pass: per-call path
+            fused = dt.itemsize if dt.itemsize > 1 else 0
+        self.zlib = is_zlib(compression)
+        if compression is not None and not self.zlib:
+            return
+        try:
+            cm = self.cm = compile_missing(missing, dt)
+        except Exception:
+            return                              # the per-call path raises it
+        if cm.tables[0] is not None or cm.tables[1] is not None:
+            return                              # vector mask tables: per-call path
+        self.rev = order == "F" and len(shape) > 1
+        dev_shape = shape[::-1] if self.rev else shape
+        if not 1 <= len(shape) <= _lib.MAX_DIMS:
+            return
+        self.mask = cm.to_struct()
+        self.mask_ref = ctypes.byref(self.mask)
+        d = self.desc_base = _lib.ChunkDesc()
+        d.dtype = dtype_code(dt)
+        d.byteswap = 1 if needs_byteswap(dt) else 0
+        d.shuffle = fused
+        d.ndim = len(shape)
+        for i, n in enumerate(dev_shape):
+            d.chunk_shape[i] = int(n)
+        d.zlib = 1 if self.zlib else 0
+        self.pdt = engine.partial_dtype(dt)
+        self.ok = True
+
+    def plan(self, chunk_selection, axis):
+        """(desc, sel_ptr, pool_ptr, pool_len, n_out, keep_shape, n_red, n_sel,
+        keepalive) for one selection + axis, cached when the selection is
+        made of slices (what pyfive's indexer produces)."""
+        sel = chunk_selection if chunk_selection.__class__ is tuple else (chunk_selection,)
+        try:   # slices only (ints, lists and arrays have no .start): cacheable
+            key = (tuple([(s.start, s.stop, s.step) for s in sel]),
+                   axis if axis is None or axis.__class__ is int else tuple(axis))
+        except (AttributeError, TypeError):
+            key = None
+        if key is not None:
+            hit = self.sels.get(key)
+            if hit is not None:
+                return hit
+        shape = self.shape
+        cs = selection.normalize(chunk_selection, shape)
+        axes = _normalize_axes(axis, len(cs.shape))
+        rev = self.rev
+        nd = len(shape)
+        dev_of = (lambda k: nd - 1 - k) if rev else (lambda k: k)
+        mask_bits = 0
+        for i in axes:
+            mask_bits |= 1 << dev_of(cs.kept[i])
+        for k, ds in enumerate(cs.dims):   # integer-indexed dims are reduced too (extent 1)
+            if ds.dropped:
+                mask_bits |= 1 << dev_of(k)
+        keep_shape = tuple(1 if i in axes else n for i, n in enumerate(cs.shape))
+        n_out = 1
+        for i, n in enumerate(cs.shape):
+            if i not in axes:
+                n_out *= n
+        n_red = 1
+        for i in axes:
+            n_red *= cs.shape[i]
+        desc = _lib.ChunkDesc()
+        ctypes.pointer(desc)[0] = self.desc_base
+        desc.axes_mask = mask_bits
+        dev_dims = cs.dims[::-1] if rev else cs.dims
+        full = all(ds.step == 1 and ds.start == 0 and ds.count == n and not ds.dropped
+                   for ds, n in zip(dev_dims, shape[::-1] if rev else shape))
+        if full:
+            table = pool = None
+            sel_ptr = pool_ptr = None
+            pool_len = 0
+        else:
+            table, pool = selection.pack([selection.ChunkSel(dev_dims, cs.shape, cs.kept)], nd)
+            table = np.ascontiguousarray(table.reshape(-1), dtype=np.int32)
+            pool = np.ascontiguousarray(pool, dtype=np.int32)
+            sel_ptr, pool_ptr, pool_len = table.ctypes.data, pool.ctypes.data, int(pool.size)
+        ent = (desc, ctypes.byref(desc), sel_ptr, pool_ptr, pool_len, n_out, keep_shape, n_red,
+               cs.n_selected, (table, pool))
+        if key is not None:
+            if len(self.sels) > 4096:
+                self.sels.clear()
+            self.sels[key] = ent
+        return ent
+
+
+def _layout(compression, filters, missing, dtype, shape, order):
+    if shape.__class__ is not tuple:
+        shape = tuple(shape) if isinstance(shape, list) else (shape,)
+    fkey = None if filters is None else tuple([(f.__class__, getattr(f, "elementsize", None))
+                                               for f in filters])
+    key = (id(missing), id(dtype), id(compression), fkey, shape, order)
+    lay = _plans.get(key)
+    if lay is not None and lay.refs[0] is missing and lay.refs[1] is dtype and \
+            lay.refs[2] is compression:
+        return lay
+    shape = tuple(int(s) for s in shape)
+    lay = _Layout((missing, dtype, compression), compression, filters, missing, dtype, shape, order)
+    with _plan_lock:
+        if len(_plans) >= _PLAN_CAP:
+            _plans.clear()
+        _plans[key] = lay
+    return lay
+
+
+def _coalesced(rfile, offset, size, compression, filters, missing, dtype, shape, order,
+               chunk_selection, axis, method):
+    """The per-chunk call through pyas_coalesced_reduce, or None when this
+    call must take the per-call path (which then raises the reference's
+    exact exception for bad input)."""
+    try:
+        kind, is_ma = results.METHODS.get(method) or results.method_kind(method)
+        lay = _layout(compression, filters, missing, dtype, shape, order)
+        if not lay.ok:
+            return None
+        desc, desc_ref, sel_ptr, pool_ptr, pool_len, n_out, keep_shape, n_red, n_sel, _ = \
+            lay.plan(chunk_selection, axis)
+    except Exception:
+        return None
+    if n_out == 0 or n_sel == 0:
+        return None
+    ctx = _ctx0 or _get_ctx0()
+    if n_out == 1:
+        # per-thread landing buffer for the one partial (+ info), reused
+        tb = getattr(_tls, "one", None)
+        if tb is None:
+            raw = np.zeros(64, dtype=np.uint8)
+            tb = _tls.one = (raw, raw.ctypes.data,
+                             (ctypes.c_int64 * 3).from_address(raw.ctypes.data + 32), {})
+        out_ptr, info = tb[1], tb[2]
+    else:
+        out = np.empty(n_out, dtype=lay.pdt)
+        out_ptr = out.ctypes.data
+        info = (ctypes.c_int64 * 3)()
+    rc = _reduce_fn(ctx._coalescer or ctx.coalescer(),
+                    rfile.encode("utf-8", "surrogateescape") if rfile.__class__ is str else os.fsencode(rfile),
+                    int(offset), int(size), desc_ref, lay.mask_ref, sel_ptr, pool_ptr, pool_len, n_out,
+                    out_ptr, info)
+    if rc != _lib.OK:
+        if rc in (_lib.EIO, _lib.ENOTSUP, _lib.EINDEX, _lib.EINVAL):
+            return None
+        _lib.check(rc, "pyas_coalesced_reduce")
+    if n_out == 1:
+        if _fastpath is not None and kind != "mean":
+            _register_fast(lay, compression, filters, missing, dtype, shape, order, chunk_selection,
+                           axis, method, kind, is_ma, keep_shape, n_sel)
+        view = tb[3].get(lay.pdt)
+        if view is None:
+            view = tb[3][lay.pdt] = tb[0][:32].view(lay.pdt)
+        return results.build_one(view[0], keep_shape, kind, is_ma, lay.dt, lay.cm.masked, n_red,
+                                 n_sel)
+    if lay.rev:
+        parts = out.reshape(keep_shape[::-1]).transpose()
+    else:
+        parts = out.reshape(keep_shape)
+    return results.build(parts, kind, is_ma, lay.dt, lay.cm.masked, n_red, n_sel)
+
+
+_tls = threading.local()
+_ctx0 = None
+_reduce_fn = None
+
+
+def _get_ctx0():
+    global _ctx0, _reduce_fn
+    ctx = get_context(0)
+    _reduce_fn = ctx.lib.pyas_coalesced_reduce
+    if _fastpath is not None:
+        _fastpath.bind(ctypes.cast(_reduce_fn, ctypes.c_void_p).value, ctx.coalescer(),
+                       np.ma.MaskedArray)
+    _ctx0 = ctx
+    return ctx
+
+
+_KIND = {"sum": 0, "min": 1, "max": 2}
+_VCLASS = {"f": 0, "i": 1, "u": 2}
+
+
+def _register_fast(lay, compression, filters, missing, dtype, shape, order, chunk_selection, axis,
+                   method, kind, is_ma, keep_shape, n_sel):
+    """Hand one call shape's plan to the C hot path (pyas_fastpath.cpp)."""
+    desc, _, sel_ptr, _, pool_len, _, _, _, _, (table, pool) = lay.plan(chunk_selection, axis)
+    if not keep_shape:
+        return
+    rdt = sum_dtype(lay.dt) if kind == "sum" else native(lay.dt)
+    _fastpath.register(missing, dtype, compression, filters, shape, order, chunk_selection, axis,
+                       method, bytes(desc), bytes(lay.mask),
+                       None if table is None else table.tobytes(),
+                       b"" if pool is None or not pool_len else pool.tobytes(),
+                       len(keep_shape), _KIND[kind], bool(is_ma), bool(lay.cm.masked), int(n_sel),
+                       _VCLASS[lay.dt.kind], rdt.num)
 
 
 def _read_pinned(fh, offset, size):

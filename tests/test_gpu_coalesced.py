@@ -1,0 +1,155 @@
+"""The per-chunk drop-in driven the way the reference drives it.
+
+``Active._from_storage`` calls ``reduce_chunk(rfile, offset, size, ...)`` once
+per chunk from a 30-thread pool (``activestorage/active.py:556-589`` ->
+``:765-776``).  ``pyactivestorage_amd.storage.reduce_chunk`` coalesces those
+concurrent calls in ``pyas_coalesced_reduce`` (one H2D, one inflate launch and
+one reduce launch per batch).  Here every golden case (the reference's own
+``storage.py`` outputs) is written to one file and replayed through that
+pool pattern, all cases in flight at once, so batches mix dtypes, byte
+orders, shuffle, zlib, masks, selections and axes.
+"""
+import concurrent.futures
+import gc
+import os
+import tempfile
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from pyactivestorage_amd import storage as pas
+from tests import _golden as G
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def golden_file():
+    cases = G.cases()
+    arrs = G.arrays()
+    offs, sizes = {}, {}
+    fd, path = tempfile.mkstemp(suffix=".golden")
+    pos = 0
+    with os.fdopen(fd, "wb") as f:
+        for c in cases:
+            key = c["input"]
+            if key in offs:
+                continue
+            raw = arrs[key].tobytes()
+            offs[key], sizes[key] = pos, len(raw)
+            f.write(raw)
+            pos += len(raw)
+    yield path, offs, sizes
+    os.unlink(path)
+
+
+def _replay(path, offs, sizes, i):
+    c = G.cases()[i]
+    a = G.args_of(i, pas.Zlib, pas.Shuffle)
+    try:
+        return "ok", pas.reduce_chunk(path, offs[c["input"]], sizes[c["input"]], a["compression"],
+                                      a["filters"], a["missing"], a["dtype"], a["shape"], a["order"],
+                                      a["chunk_selection"], a["axis"], a["method"])
+    except Exception as e:  # noqa: BLE001 - compared with the reference's exception below
+        return "raised", e
+
+
+def test_golden_replay_through_the_pool_pattern(gpu, golden_file):
+    path, offs, sizes = golden_file
+    n = len(G.cases())
+    before = gpu.coalescer_stats()
+    with concurrent.futures.ThreadPoolExecutor(max_workers=30) as ex:
+        res = list(ex.map(lambda i: _replay(path, offs, sizes, i), range(n)))
+    after = gpu.coalescer_stats()
+    fallbacks = 0
+    for i, (kind, r) in enumerate(res):
+        exp = G.expected(i)
+        if isinstance(exp[0], str):
+            assert kind == "raised" and type(r).__name__ == exp[0], (i, G.cases()[i], r)
+            continue
+        assert kind == "ok", (i, G.cases()[i], r)
+        tmp, cnt = r
+        a = G.args_of(i, pas.Zlib, pas.Shuffle)
+        fallbacks += G.check_gpu(i, tmp, cnt, a, pas.reduce_chunk_bytes)
+    coalesced = after["chunks"] - before["chunks"]
+    print(f"\ncoalesced {coalesced} of {n} calls in {after['batches'] - before['batches']} batches "
+          f"(largest {after['largest']}); {fallbacks} float sums needed the 4e-7*sum|x| bound")
+    assert coalesced > n // 2          # most cases are coalescable (no vector masks)
+    assert after["largest"] > 1        # and calls really were batched
+
+
+def test_coalesced_equals_per_call_path(gpu, golden_file, monkeypatch):
+    """Both paths of reduce_chunk agree: containers, masks, counts, min/max
+    bit for bit.  Sums and means may differ in the last bits: a batch whose
+    chunks are all whole takes the dense kernels, whose summation order
+    differs from the selection kernels' (both within north_star's 1e-6)."""
+    path, offs, sizes = golden_file
+    idx = list(range(0, len(G.cases()), 7))
+    with concurrent.futures.ThreadPoolExecutor(max_workers=30) as ex:
+        got = list(ex.map(lambda i: _replay(path, offs, sizes, i), idx))
+    monkeypatch.setattr(pas, "COALESCE", False)
+    want = [_replay(path, offs, sizes, i) for i in idx]
+    for i, (gk, g), (wk, w) in zip(idx, got, want):
+        assert gk == wk, i
+        if gk == "raised":
+            assert type(g) is type(w), i
+            continue
+        assert type(g[0]) is type(w[0]) and g[0].dtype == w[0].dtype and g[0].shape == w[0].shape, i
+        assert np.array_equal(np.ma.getmaskarray(g[0]), np.ma.getmaskarray(w[0])), i
+        assert (np.ma.getmask(g[0]) is np.ma.nomask) == (np.ma.getmask(w[0]) is np.ma.nomask), i
+        gd, wd = np.asarray(np.ma.getdata(g[0])), np.asarray(np.ma.getdata(w[0]))
+        method = G.cases()[i]["method"]
+        if gd.dtype.kind == "f" and method.endswith(("sum", "mean")):
+            np.testing.assert_allclose(gd, wd, rtol=1e-6, atol=0, err_msg=str(i))
+        else:
+            assert gd.tobytes() == wd.tobytes(), i
+        assert np.array_equal(g[1], w[1]) and g[1].dtype == w[1].dtype, i
+
+
+def test_short_read_and_missing_file_raise_like_the_reference(gpu, tmp_path):
+    p = tmp_path / "c.bin"
+    x = np.arange(64, dtype="<f4")
+    p.write_bytes(x.tobytes())
+    sel = (slice(0, 4), slice(0, 4), slice(0, 4))
+    tmp, n = pas.reduce_chunk(str(p), 0, 256, None, None, (None,) * 4, "<f4", (4, 4, 4), "C", sel,
+                              (0, 1, 2), np.ma.sum)
+    assert float(tmp) == float(x.sum()) and int(n) == 64
+    with pytest.raises(ValueError):       # storage.py:62 reshape of a short read
+        pas.reduce_chunk(str(p), 128, 256, None, None, (None,) * 4, "<f4", (4, 4, 4), "C", sel,
+                         (0, 1, 2), np.ma.sum)
+    with pytest.raises(Exception):        # storage.py:63-76: not a file -> fsspec http path
+        pas.reduce_chunk(str(tmp_path / "nope.bin"), 0, 256, None, None, (None,) * 4, "<f4",
+                         (4, 4, 4), "C", sel, (0, 1, 2), np.ma.sum)
+
+
+def test_thread_resources_are_released(gpu, tmp_path, monkeypatch):
+    """each query of the reference builds a new ThreadPoolExecutor
+    (active.py:557).  The per-call path's per-thread streams, scratch and
+    pinned staging must be released when those threads end."""
+    monkeypatch.setattr(pas, "COALESCE", False)
+    p = tmp_path / "c.bin"
+    p.write_bytes(np.arange(4 * 32 ** 3, dtype="<f4").tobytes())
+    sel = (slice(0, 32),) * 3
+    cb = 32 ** 3 * 4
+
+    def one(k):
+        return pas.reduce_chunk(str(p), (k % 4) * cb, cb, None, None, (np.float32(3.0), None, None, None),
+                                "<f4", (32, 32, 32), "C", sel, (0, 1, 2), np.ma.sum)
+
+    gc.collect()
+    base_streams, base_pinned = gpu.live_streams, gpu.pinned_bytes
+    peak = 0
+    for q in range(200):
+        with concurrent.futures.ThreadPoolExecutor(max_workers=4) as ex:
+            list(ex.map(one, range(8)))
+        peak = max(peak, gpu.live_streams - base_streams)
+    deadline = time.time() + 10
+    while (gpu.live_streams > base_streams or gpu.pinned_bytes > base_pinned) and time.time() < deadline:
+        gc.collect()
+        time.sleep(0.05)
+    assert peak <= 4 * 2, peak        # at most the live threads' streams
+    assert gpu.live_streams == base_streams, (gpu.live_streams, base_streams)
+    assert gpu.pinned_bytes == base_pinned, (gpu.pinned_bytes, base_pinned)
+    assert threading.active_count() < 8

@@ -223,6 +223,7 @@ def test_capi_struct_layouts():
     assert ctypes.sizeof(_lib.Scalar) == 8
     assert _lib.Batch.data.offset == 4 * 4 + 8 * _lib.MAX_DIMS + 8
     assert ctypes.sizeof(_lib.Mask) == 4 + 8 + 16 + 16 + 8 + 8 + 16 + 16 + 2 * 8 * _lib.MAX_DIMS + 4  # padding
+    assert ctypes.sizeof(_lib.ChunkDesc) == 4 * 4 + 8 * _lib.MAX_DIMS + 4 + 4
 
 
 def test_capi_errors_without_gpu_are_reported():
@@ -261,3 +262,37 @@ def test_inflate_status_mapping_and_packing():
     host, offs, sizes = pack_streams([b"abc", b"", b"defgh"], align=4)
     assert list(offs) == [0, 4, 4] and list(sizes) == [3, 0, 5]
     assert host[:3].tobytes() == b"abc" and host[4:9].tobytes() == b"defgh"
+
+
+def _state(x):
+    if isinstance(x, np.ma.MaskedArray):
+        d = dict(x.__dict__)
+        m = d.pop("_mask")
+        return (type(x), x.dtype.str, x.shape, np.asarray(x.data).tobytes(), m is np.ma.nomask,
+                np.asarray(m).tobytes(), sorted(d.items(), key=lambda kv: kv[0]).__repr__())
+    return (type(x), x.dtype.str, x.shape, np.asarray(x).tobytes())
+
+
+@pytest.mark.parametrize("dt", ["<f4", ">f8", "<i2", "<u4", "<i8", "u1"])
+def test_build_one_matches_build(dt):
+    """The drop-in's single-partial result builder returns objects identical
+    to the generic one (type, dtype, shape, data, mask, MaskedArray state)."""
+    from pyactivestorage_amd.engine import partial_dtype
+    pdt = partial_dtype(dt)
+    p = np.zeros(1, dtype=pdt)
+    cls = pdt["sum"].type
+    for cnt, n_sel in ((5, 5), (3, 5), (0, 5)):
+        p["count"] = cnt
+        p["sum"] = cls(1234) if np.dtype(dt).kind != "f" else 1234.5678901234
+        p["min"] = cls(7)
+        p["max"] = cls(99)
+        for shape in ((1,), (1, 1, 1)):
+            for kind in ("sum", "min", "max", "mean"):
+                for is_ma in (True, False):
+                    for rule in (True, False):
+                        if not rule and cnt < n_sel:
+                            continue
+                        want = results.build(p.reshape(shape), kind, is_ma, np.dtype(dt), rule, n_sel, n_sel)
+                        got = results.build_one(p[0], shape, kind, is_ma, np.dtype(dt), rule, n_sel, n_sel)
+                        assert _state(got[0]) == _state(want[0]), (dt, cnt, kind, is_ma, rule)
+                        assert _state(got[1]) == _state(want[1])
