@@ -46,6 +46,8 @@ from .variable import ChunkedVariable, decode_filters, get_missing_attributes
 
 _ALIGN = 256
 _RESIDENT_LOCK = threading.Lock()
+_RESIDENT_CV = threading.Condition(_RESIDENT_LOCK)   # slot state changes
+_EMPTY, _LOADING, _LOADED = 0, 1, 2
 
 
 # PYAS_AXES_FOLD=0 keeps whole-chunk box queries on the two-step path
@@ -55,12 +57,26 @@ _AXES_FOLD = os.environ.get("PYAS_AXES_FOLD", "1") != "0"
 
 def release_resident(variable) -> None:
     """Free the HBM copy that resident-mode ``Active`` queries keep for
-    ``variable`` (e.g. after the file changed)."""
-    store = getattr(variable, "_pyas_resident", None)
-    if store is not None:
-        get_context(store["device"]).synchronize(get_context(store["device"]).thread_stream())
-        store["buf"].free()
+    ``variable`` (e.g. after the file changed).  Queries already using the
+    copy keep it until they finish; the last one frees it."""
+    with _RESIDENT_LOCK:
+        store = getattr(variable, "_pyas_resident", None)
+        if store is None:
+            return
         variable._pyas_resident = None
+        store["released"] = True
+        free = store["users"] == 0
+    if free:
+        store["buf"].free()
+
+
+def _unhold(store) -> None:
+    """A query that used ``store`` has finished (its stream is synchronised)."""
+    with _RESIDENT_LOCK:
+        store["users"] -= 1
+        free = store["users"] == 0 and store["released"]
+    if free:
+        store["buf"].free()
 
 
 # read -> inflate pipeline stages of a compressed query (PYAS_INFLATE_GROUPS)
@@ -135,6 +151,7 @@ class Active:
         self.resident = bool(resident)
         self.missing = None
         self.data_read = 0
+        self._held = threading.local()
 
     # -- API mirrored from active.py:355-418 ------------------------------
     @property
@@ -177,10 +194,14 @@ class Active:
     def __getitem__(self, index):
         self.missing = get_missing_attributes(self.ds.attrs)
         self.data_read = 0
+        held = self._held.stores = []    # resident stores this query uses (this thread)
         try:
             return self._get_selection(index)
         finally:
             self._method = None          # active.py:633
+            for store in held:
+                _unhold(store)
+            self._held.stores = []
 
     def _get_selection(self, index):
         ds = self.ds
@@ -241,37 +262,64 @@ class Active:
             if store is None or store["device"] != self.device:
                 n_all = int(np.prod(grid))
                 store = {"device": self.device, "buf": DeviceBuffer(ctx, max(n_all, 1) * stride),
-                         "loaded": np.zeros(n_all, dtype=bool)}
+                         "state": np.zeros(n_all, dtype=np.int8), "users": 0, "released": False}
                 ds._pyas_resident = store
-            c = np.asarray(coords, dtype=np.int64).reshape(len(coords), len(grid))
-            slots = np.ravel_multi_index(c.T, grid) if len(coords) else np.zeros(0, dtype=np.int64)
-            todo = np.nonzero(~store["loaded"][slots])[0]
-        todo_coords = [tuple(x) for x in c[todo].tolist()]
+            store["users"] += 1
+        held = getattr(self._held, "stores", None)
+        if held is None:
+            held = self._held.stores = []
+        held.append(store)
+        c = np.asarray(coords, dtype=np.int64).reshape(len(coords), len(grid))
+        slots = np.ravel_multi_index(c.T, grid) if len(coords) else np.zeros(0, dtype=np.int64)
         fused = self._fused_shuffle(filters)
+        st = ctx.thread_stream()
+        while True:
+            # claim the empty slots; slots another query is loading are waited for
+            with _RESIDENT_LOCK:
+                state = store["state"]
+                todo = np.nonzero(state[slots] == _EMPTY)[0]
+                state[slots[todo]] = _LOADING
+            try:
+                st = self._load_slots(ctx, store, c[todo], slots[todo], stride, nbytes, compressor,
+                                      filters, fused)
+            except BaseException:
+                with _RESIDENT_CV:
+                    store["state"][slots[todo]] = _EMPTY
+                    _RESIDENT_CV.notify_all()
+                raise
+            with _RESIDENT_CV:
+                store["state"][slots[todo]] = _LOADED
+                _RESIDENT_CV.notify_all()
+                while (store["state"][slots] == _LOADING).any():
+                    _RESIDENT_CV.wait()
+                if (store["state"][slots] == _LOADED).all():
+                    break
+                # a loader failed: its slots are empty again, claim them
+        return ctx, st, store["buf"], slots.astype(np.int64) * stride, 0 if fused in (2, 4, 8) else fused
+
+    def _load_slots(self, ctx, store, coords, slots, stride, nbytes, compressor, filters, fused):
+        """Read + decode chunks ``coords`` into resident ``slots``; returns
+        the stream, synchronised (other queries read the slots once marked)."""
+        st = ctx.thread_stream()
+        if not len(slots):
+            return st
+        todo_coords = [tuple(x) for x in coords.tolist()]
         if fused in (2, 4, 8):
             # the store keeps chunks un-shuffled (one batched pass as they
             # arrive), so every later query takes the unshuffled kernels
             # (dense partial-axis layouts and the in-kernel layer fold)
-            st = ctx.thread_stream()
-            if todo.size:
-                _, st, tmp, toffs, _ = self._ingest_fresh(todo_coords, compressor, filters)
-                offs = np.concatenate([toffs, slots[todo] * stride]).astype(np.int64)
-                meta = DeviceBuffer(ctx, offs.nbytes)
-                ctx.h2d(meta.ptr, offs, st)
-                engine.unshuffle_chunks(ctx, tmp.ptr, meta.ptr, store["buf"].ptr, meta.ptr + 8 * todo.size,
-                                        todo.size, nbytes, fused, st)
-                ctx.synchronize(st)   # tmp and meta are freed on return
-            fused = 0
+            _, st, tmp, toffs, _ = self._ingest_fresh(todo_coords, compressor, filters)
+            offs = np.concatenate([toffs, slots * stride]).astype(np.int64)
+            meta = DeviceBuffer(ctx, offs.nbytes)
+            ctx.h2d(meta.ptr, offs, st)
+            engine.unshuffle_chunks(ctx, tmp.ptr, meta.ptr, store["buf"].ptr, meta.ptr + 8 * len(slots),
+                                    len(slots), nbytes, fused, st)
+            ctx.synchronize(st)   # tmp and meta are freed on return
         else:
-            _, st, _, _, fused = self._ingest_fresh(todo_coords, compressor, filters,
-                                                    dst=store["buf"], dst_offsets=slots[todo] * stride)
-        if todo.size:
-            # another thread's kernels (on its own stream) may read these slots
-            # as soon as they are marked: mark them once the copies have landed
+            _, st, _, _, _ = self._ingest_fresh(todo_coords, compressor, filters,
+                                                dst=store["buf"], dst_offsets=slots * stride)
             ctx.synchronize(st)
-            with _RESIDENT_LOCK:
-                store["loaded"][slots[todo]] = True
-        return ctx, st, store["buf"], slots.astype(np.int64) * stride, fused
+        return st
 
     def _ingest_fresh(self, coords, compressor, filters, dst=None, dst_offsets=None):
         """Read + inflate every touched chunk into one device buffer (``dst``

@@ -224,6 +224,7 @@ class CompiledMask:
 
 
 _cache: dict = {}
+_CACHE_CAP = 512   # compiled masks kept; keys can come from clients (reductionist_server)
 
 
 def compile_missing(missing, dt) -> CompiledMask:
@@ -294,6 +295,8 @@ def compile_missing(missing, dt) -> CompiledMask:
         nxt = space.value(space.lo + 1)
         cm.lt = nxt if cm.lt is None or cm.lt < nxt else cm.lt
         cm.flags |= _lib.MASK_LT
+    if len(_cache) >= _CACHE_CAP:
+        _cache.pop(next(iter(_cache)))   # oldest first (dicts keep insertion order)
     _cache[key] = cm
     return cm
 

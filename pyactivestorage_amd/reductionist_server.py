@@ -201,14 +201,29 @@ _METHODS = {"sum": np.ma.sum, "min": np.ma.min, "max": np.ma.max, "mean": np.ma.
             "count": np.ma.sum, "select": None}
 
 
+# Largest decoded chunk a request may ask for (its shape x itemsize): the
+# server sizes device and pinned buffers from it, so a client must not be
+# able to request arbitrary allocations.
+MAX_CHUNK_BYTES = int(os.environ.get("PYAS_SERVER_MAX_CHUNK_BYTES", str(1 << 30)))
+
+
 def execute(operation: str, req: dict, root: str):
     """Run the request on the GPU; returns ``(values ndarray, count ndarray)``."""
     path = resolve_url(req["url"], root)
     dt = req["dtype"]
     size = req["size"]
+    length = os.path.getsize(path)
+    if req["offset"] > length:
+        raise RequestError(f"offset {req['offset']} beyond the object's {length} bytes")
     if size is None or size == 0:   # Reductionist: 0/absent = to the end of the object
-        size = os.path.getsize(path) - req["offset"]
+        size = length - req["offset"]
+    if req["offset"] + size > length:
+        raise RequestError(f"byte range [{req['offset']}, {req['offset'] + size}) beyond the "
+                           f"object's {length} bytes")
     shape = req["shape"] or (size // dt.itemsize,)
+    if int(np.prod(shape, dtype=np.float64)) * dt.itemsize > MAX_CHUNK_BYTES or \
+            (req["compression"] is None and size > MAX_CHUNK_BYTES):
+        raise RequestError(f"chunk larger than the server's {MAX_CHUNK_BYTES}-byte limit")
     sel = req["selection"]
     if sel is None:
         sel = tuple(slice(0, n, 1) for n in shape)

@@ -394,6 +394,10 @@ def _read_pinned(fh, offset, size):
     returning.  A short read (past the end of the file) returns the bytes
     that exist, as ``fh.read`` does."""
     ctx = get_context(0)
+    try:   # never pin more than the file can return
+        size = max(0, min(int(size), os.fstat(fh.fileno()).st_size - int(offset)))
+    except (OSError, AttributeError, ValueError):
+        pass
     host = ctx.thread_host_buffer(int(size))
     fh.seek(offset)
     n = fh.readinto(memoryview(host)[: int(size)])

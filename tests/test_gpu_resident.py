@@ -78,3 +78,33 @@ def test_resident_concurrent_threads(gpu):
     finally:
         release_resident(var)
     assert nd == 3
+
+
+def test_release_while_queries_run(gpu):
+    """release_resident must not free HBM another thread's query
+    is reading, and two threads loading the same chunks must not both read
+    them: queries racing a release still return the fresh path's answer,
+    and the copy is gone once they finish."""
+    import concurrent.futures
+    import threading
+    var = D.make_variable()
+    ix = tuple(slice(None) for _ in var.shape)
+    want = _query(var, "mean", (0,), ix, False)[0]
+    stop = threading.Event()
+
+    def releaser():
+        while not stop.is_set():
+            release_resident(var)
+
+    t = threading.Thread(target=releaser)
+    t.start()
+    try:
+        with concurrent.futures.ThreadPoolExecutor(max_workers=6) as ex:
+            got = list(ex.map(lambda _: _query(var, "mean", (0,), ix, True)[0], range(36)))
+    finally:
+        stop.set()
+        t.join()
+    for k, g in enumerate(got):
+        _same(g, want, f"racing query {k}")
+    release_resident(var)
+    assert getattr(var, "_pyas_resident", None) is None

@@ -150,3 +150,22 @@ def test_encode_response_roundtrip():
     assert count == [[[7]]]
     res, count = client_decode(rs.encode_response(np.int64(12), np.int64(3)))
     assert res.size == 1 and int(np.asarray(res).reshape(-1)[0]) == 12 and count == 3
+
+
+def test_execute_bounds_requests_before_any_allocation(tmp_path):
+    """client-chosen offset/size/shape must not size pinned or
+    device buffers beyond the object (400, before the GPU is touched)."""
+    (tmp_path / "b").mkdir()
+    (tmp_path / "b" / "o.bin").write_bytes(np.zeros(1024, "<f4").tobytes())
+    base = {"url": "s3://b/o.bin", "dtype": "float32"}
+
+    def run(**kw):
+        body = dict(base, **kw)
+        status, _, payload = rs.handle("sum", json.dumps(body).encode(), str(tmp_path))
+        return status, payload
+
+    for kw in ({"offset": 8192, "size": 4}, {"offset": 0, "size": 1 << 40}, {"offset": 4096, "size": 8},
+               {"offset": 0, "size": 4096, "shape": [1 << 20, 1 << 20]}):
+        status, payload = run(**kw)
+        assert status == 400, (kw, status, payload)
+        assert b"beyond" in payload or b"limit" in payload, payload
