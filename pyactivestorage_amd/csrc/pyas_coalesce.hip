@@ -10,13 +10,12 @@
 // Here concurrent calls are coalesced without changing the calling pattern:
 //   caller thread  : open + pread(2) of its chunk straight into a pinned host
 //                    ring (ctypes released the GIL), then sleep;
-//                    and enqueue its H2D copy on the coalescer's stream;
-//   dispatcher     : take the longest prefix of the ring whose reads are done
-//                    (their copies are already queued), inflate
+//   dispatcher     : take the longest prefix of the ring whose reads are done,
+//                    copy it H2D in one or two copies (a wrapped ring), inflate
 //                    every zlib stream of the batch in one launch, reduce every
 //                    chunk in one launch per (layout, mask, axes) group, copy
-//                    every partial back in one copy, synchronise once, wake the
-//                    callers.
+//                    every partial back in one copy, wait on the batch's event,
+//                    wake the callers.
 // Batches grow with load (callers keep filling the ring while the previous
 // batch runs) and there are no timers.  Anything the batch cannot express —
 // vector mask tables, a chunk larger than the ring, a short read, a zlib
@@ -25,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
+#include <stdlib.h>
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -84,6 +84,7 @@ struct Req {
     int state = RESERVED;
     int rc = PYAS_OK;
     std::string err;
+    std::condition_variable cv;     // DONE (waited on with the coalescer's mutex)
 };
 
 struct Group {
@@ -135,11 +136,16 @@ struct pyas_coalescer {
     int64_t head = 0;           // next free byte
     std::deque<Req *> fifo;     // reservation order == ring order
     std::mutex mu;
-    std::condition_variable cv_disp, cv_done, cv_space;
+    std::condition_variable cv_disp, cv_space;
     std::thread disp;
     bool stop = false;
     hipStream_t st = nullptr;
     hipEvent_t done_ev = nullptr;
+    // Measured on the box (tools/bench_dropin.py): with 30 reader threads on a
+    // 16-CPU host share, the dispatcher copying the batch's prefix and
+    // sleeping on its completion event leaves the most CPU to the readers.
+    bool caller_copy = false;   // PYAS_COALESCE_COPY=caller: each caller copies its own chunk
+    bool blocking_sync = true;  // PYAS_COALESCE_SYNC=spin: the dispatcher spins on the batch
     // dispatcher-only scratch
     HostBuf<uint8_t> hmeta;
     DevBuf<uint8_t> dmeta;
@@ -321,9 +327,36 @@ void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
         }
         if (m.pool_len == 0) pool[0] = 0;
     }
-    // 1. the chunk bytes are already on their way: each caller enqueued
-    //    its own H2D copy on c->st right after its read, before it marked
-    //    the request FILLED, so the launches below are ordered after them
+    // 1. the chunk bytes: copy the prefix here, one copy per contiguous run
+    //    (two when the ring wrapped; gaps are alignment padding or skipped
+    //    reads of the same prefix) -- or, with PYAS_COALESCE_COPY=caller,
+    //    each caller already enqueued its own H2D copy on c->st right after
+    //    its read, before it marked the request FILLED, so the launches
+    //    below are ordered after them
+    if (!c->caller_copy) {
+        int64_t run_a = -1, run_b = -1;
+        for (Req *r : batch) {
+            if (r->state == SKIP) continue;
+            if (run_a >= 0 && r->ring_off >= run_b) {
+                run_b = r->ring_off + r->nbytes;
+                continue;
+            }
+            if (run_a >= 0 &&
+                (e = hipMemcpyAsync(c->dring + run_a, c->hring + run_a, (size_t)(run_b - run_a),
+                                    hipMemcpyHostToDevice, c->st)) != hipSuccess) {
+                fail_all(PYAS_EDEVICE, hipGetErrorString(e));
+                return;
+            }
+            run_a = r->ring_off;
+            run_b = r->ring_off + r->nbytes;
+        }
+        if (run_a >= 0 &&
+            (e = hipMemcpyAsync(c->dring + run_a, c->hring + run_a, (size_t)(run_b - run_a),
+                                hipMemcpyHostToDevice, c->st)) != hipSuccess) {
+            fail_all(PYAS_EDEVICE, hipGetErrorString(e));
+            return;
+        }
+    }
     // 2. meta H2D
     if ((e = hipMemcpyAsync(dm, hm, (size_t)meta_bytes, hipMemcpyHostToDevice, c->st)) != hipSuccess) {
         fail_all(PYAS_EDEVICE, hipGetErrorString(e));
@@ -441,7 +474,9 @@ void dispatcher(pyas_coalescer *c) {
         c->n_batches += 1;
         c->n_chunks += nch;
         if (nch > c->max_seen) c->max_seen = nch;
-        c->cv_done.notify_all();
+        // wake exactly this batch's callers (one condition variable each:
+        // a shared notify_all would wake every waiting caller per batch)
+        for (Req *r : batch) r->cv.notify_one();
         c->cv_space.notify_all();
     }
 }
@@ -462,7 +497,11 @@ int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch, 
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->hring, (size_t)c->ring_bytes, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc((void **)&c->dring, (size_t)c->ring_bytes);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming);
+    if (const char *v = getenv("PYAS_COALESCE_COPY")) c->caller_copy = std::strcmp(v, "caller") == 0;
+    if (const char *v = getenv("PYAS_COALESCE_SYNC")) c->blocking_sync = std::strcmp(v, "spin") != 0;
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming |
+                                                     (c->blocking_sync ? hipEventBlockingSync : 0u));
     if (e != hipSuccess) {
         if (c->hring) (void)hipHostFree(c->hring);
         if (c->dring) (void)hipFree(c->dring);
@@ -589,7 +628,7 @@ int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, i
     close(fd);
     info[0] = got;
     hipError_t ce = hipSuccess;
-    if (got == size && !read_errno && size > 0) {
+    if (c->caller_copy && got == size && !read_errno && size > 0) {
         // this chunk's H2D copy, issued by the caller so that copies overlap
         // other callers' reads; ordered before the batch's launches on c->st
         ce = hipSetDevice(c->device);
@@ -603,7 +642,7 @@ int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, i
     if (r.state == SKIP) r.rc = ce == hipSuccess ? PYAS_EIO : PYAS_EDEVICE;
     if (ce != hipSuccess) r.err = hipGetErrorString(ce);
     c->cv_disp.notify_one();
-    c->cv_done.wait(lk, [&] { return r.state == DONE; });
+    r.cv.wait(lk, [&] { return r.state == DONE; });
     c->read_ns += t_wait - t_read;
     c->wait_ns += now_ns() - t_wait;
     lk.unlock();

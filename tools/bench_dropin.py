@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--threads", type=int, default=30)
     ap.add_argument("--gpu-only", action="store_true", help="skip the per-call and oracle legs")
     ap.add_argument("--trials", type=int, default=5, help="timed passes of the GPU leg (median reported)")
+    ap.add_argument("--ceiling-read", action="store_true",
+                    help="diagnostic: also time the same pool doing only the file reads "
+                         "(open + pread of each chunk into a per-thread buffer, no GPU)")
     ap.add_argument("--ceiling-us", type=int, default=0,
                     help="diagnostic: also time the same pool driving a function that only "
                          "sleeps this long with the GIL released (the pattern's own ceiling)")
@@ -84,7 +87,10 @@ def main():
 
         from pyactivestorage_amd.device import get_context
         s0 = get_context(0).coalescer_stats() if pas.COALESCE else None
+        c0 = os.times()
         gs, gres = run(pas.reduce_chunk, a.chunks, trials=a.trials)
+        c1 = os.times()
+        cpu_us = ((c1.user - c0.user) + (c1.system - c0.system)) / (a.chunks * a.trials) * 1e6
         s1 = get_context(0).coalescer_stats() if pas.COALESCE else None
         if a.gpu_only:
             extra = {}
@@ -97,9 +103,43 @@ def main():
                     return None
                 ns, _ = run(idle, a.chunks, trials=a.trials)
                 extra = {"ceiling_us": a.ceiling_us, "ceiling_chunks_per_s": round(a.chunks / ns, 1)}
+            if a.ceiling_read:
+                import threading
+                tl = threading.local()
+
+                def read_only(p, off, size, *args):
+                    b = getattr(tl, "b", None)
+                    if b is None or len(b) < size:
+                        b = tl.b = bytearray(size)
+                    fd = os.open(p, os.O_RDONLY)
+                    try:
+                        os.preadv(fd, [memoryview(b)[:size]], off)
+                    finally:
+                        os.close(fd)
+                    return None
+                rs_, _ = run(read_only, a.chunks, trials=a.trials)
+                extra["read_only_chunks_per_s"] = round(a.chunks / rs_, 1)
             print(json.dumps({"threads": a.threads, "chunks_per_s": round(a.chunks / gs, 1),
+                              "env": {k: v for k, v in os.environ.items() if k.startswith("PYAS_")},
+                              "cpu_us_per_chunk": round(cpu_us, 1),
                               "stats": {k: s1[k] - s0[k] for k in s1}, **extra}), flush=True)
             return
+        ceiling = None
+        if a.ceiling_read:
+            import threading
+            tl2 = threading.local()
+
+            def read_only2(p, off, size, *args):
+                b = getattr(tl2, "b", None)
+                if b is None or len(b) < size:
+                    b = tl2.b = bytearray(size)
+                fd = os.open(p, os.O_RDONLY)
+                try:
+                    os.preadv(fd, [memoryview(b)[:size]], off)
+                finally:
+                    os.close(fd)
+            rs2, _ = run(read_only2, a.chunks, trials=a.trials)
+            ceiling = round(a.chunks / rs2, 1)
         pas.COALESCE = False
         ps, pres = run(pas.reduce_chunk, min(a.percall_chunks, a.chunks))
         pas.COALESCE = True
@@ -119,7 +159,9 @@ def main():
                        "largest_batch": s1["largest"] if s1 else None,
                        "dispatcher_busy_s": round(s1["busy_s"] - s0["busy_s"], 4) if s1 else None,
                        "callers_read_s": round(s1["read_s"] - s0["read_s"], 4) if s1 else None,
-                       "callers_wait_s": round(s1["wait_s"] - s0["wait_s"], 4) if s1 else None},
+                       "callers_wait_s": round(s1["wait_s"] - s0["wait_s"], 4) if s1 else None,
+                       "host_cpu_us_per_chunk": round(cpu_us, 1)},
+               "read_only_ceiling_chunks_per_s": ceiling,
                "gpu_per_call": {"chunks": npc, "s": round(ps, 4), "chunks_per_s": round(npc / ps, 1),
                                 "GBps": round(npc * cb / ps / 1e9, 3)},
                "cpu_oracle": {"chunks": a.cpu_chunks, "s": round(cs, 4),
