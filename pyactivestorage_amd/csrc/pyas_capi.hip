@@ -121,6 +121,31 @@ int ensure_counters(pyas_ctx *ctx, void *stream, int64_t n, uint32_t **out) {
     return PYAS_OK;
 }
 
+// An equality interval [lo, hi] wholly below the `< lt` threshold or wholly
+// above the `> gt` one masks nothing the threshold does not already mask, so
+// it is dropped (C3/C4: _FillValue -999 under valid_min 1000) and the kernels
+// run a mode with fewer compares (mask_mode).  A lone second interval moves
+// to slot 0.  The set of masked values is unchanged.
+void trim_mask(pyas_mask &m, int dtype) {
+    auto lt = [dtype](const pyas_scalar &x, const pyas_scalar &y) {
+        if (dtype == PYAS_F32 || dtype == PYAS_F64) return x.f < y.f;
+        if (dtype == PYAS_U8 || dtype == PYAS_U16 || dtype == PYAS_U32 || dtype == PYAS_U64) return x.u < y.u;
+        return x.i < y.i;
+    };
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t bit = k == 0 ? PYAS_MASK_EQ0 : PYAS_MASK_EQ1;
+        if (!(m.flags & bit)) continue;
+        const bool below = (m.flags & PYAS_MASK_LT) && lt(m.eq_hi[k], m.lt);
+        const bool above = (m.flags & PYAS_MASK_GT) && lt(m.gt, m.eq_lo[k]);
+        if (below || above) m.flags &= ~bit;
+    }
+    if (!(m.flags & PYAS_MASK_EQ0) && (m.flags & PYAS_MASK_EQ1)) {
+        m.eq_lo[0] = m.eq_lo[1];
+        m.eq_hi[0] = m.eq_hi[1];
+        m.flags = (m.flags & ~PYAS_MASK_EQ1) | PYAS_MASK_EQ0;
+    }
+}
+
 // Validate the batch and fill the kernel argument block.
 int prepare(const pyas_ctx *ctx, const pyas_batch *b, const pyas_mask *m, pyas::ReduceArgs &a,
             int &es, bool &shuf, bool &bsw, bool &masked) {
@@ -178,6 +203,7 @@ int prepare(const pyas_ctx *ctx, const pyas_batch *b, const pyas_mask *m, pyas::
             }
         }
         masked = m->flags != 0;
+        trim_mask(a.mask, b->dtype);
     }
     (void)ctx;
     return PYAS_OK;
@@ -484,8 +510,11 @@ int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *
 // kept dims and fit them to (RO, KO, RI, KI); pick the column layout (a
 // kept inner run of whole 16-B vectors) or the row layout (a reduced inner
 // run of whole 16-B vectors, >= 4 lanes per output).  mode 0 = not dense.
+// Shuffled chunks (vpl = es) load the row layouts in units of 16 elements
+// (one 16-B piece per byte plane = vpl vectors), so a run must hold whole
+// units.
 static void dense_geometry(pyas::AxesDense &d, const pyas_batch *b, uint32_t axes_mask, int es,
-                           bool excluded) {
+                           int vpl, bool excluded) {
     std::memset(&d, 0, sizeof(d));
     if (excluded || axes_mask == 0) return;
     int64_t ext[PYAS_MAX_DIMS];
@@ -518,6 +547,7 @@ static void dense_geometry(pyas::AxesDense &d, const pyas_batch *b, uint32_t axe
     } else {
         if ((d.RI * es) % 16) return;
         const int64_t V = d.RI / nv;
+        if (V % vpl) return;       // shuffled: whole 16-element units per run
         // Short single runs (RO == 1, <= 256 B): through LDS, 1, 2 or 4 lanes
         // per output (PYAS_ROW_LDS: 0 off, else the most lanes allowed; default 2)
         const char *e_lds = getenv("PYAS_ROW_LDS");     // per call: tests switch it
@@ -540,10 +570,11 @@ static void dense_geometry(pyas::AxesDense &d, const pyas_batch *b, uint32_t axe
             const char *e = getenv("PYAS_ROW_VECS");
             return e ? (int64_t)atoi(e) : (int64_t)2;   // measured: 2 beats 1 and 4 on (2,)
         }();
+        const int64_t Vu = V / vpl, min_units = vpl > 1 ? 1 : row_vecs;   // load units per run
         int64_t g = 1;
-        while (g < pyas::kWave && V % (g * 2) == 0 && V / (g * 2) >= row_vecs) g *= 2;
+        while (g < pyas::kWave && Vu % (g * 2) == 0 && Vu / (g * 2) >= min_units) g *= 2;
         if (g < 4) return;         // too few lanes per output to coalesce
-        const int64_t per_lane = d.RO * (V / g);
+        const int64_t per_lane = d.RO * (Vu / g);
         const int64_t uo = per_lane == 1 ? 4 : 1;
         d.mode = uo == 4 ? 3 : 2;
         d.group = (int32_t)g;
@@ -612,7 +643,7 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *ma
     x.out = out;
     x.shuf = shuf;
     x.bswap = bsw;
-    dense_geometry(x.d, batch, axes_mask, es, shuf || x.r.tab.on[0] || x.r.tab.on[1]);
+    dense_geometry(x.d, batch, axes_mask, es, shuf ? es : 1, x.r.tab.on[0] || x.r.tab.on[1]);
     // Fully selected chunks go to k_axes_dense, the rest to k_reduce_axes
     // (each kernel skips the other's chunks); sel == NULL means all full.
     if (x.d.mode) {
@@ -669,7 +700,7 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
     if (n_pos != batch->n_chunks)
         return fail(PYAS_EINVAL, "%lld chunks for a grid of %lld", (long long)batch->n_chunks, (long long)n_pos);
     fg.flags = combine_flags;
-    dense_geometry(x.d, batch, axes_mask, es, shuf || x.r.tab.on[0] || x.r.tab.on[1]);
+    dense_geometry(x.d, batch, axes_mask, es, shuf ? es : 1, x.r.tab.on[0] || x.r.tab.on[1]);
     if ((x.d.mode != 1 && x.d.mode < 4) || es < 4)
         return fail(PYAS_ENOTSUP, "the in-kernel layer fold needs the dense column or LDS row layout");
     // Each workgroup walks every layer of its column, so the grid is only

@@ -150,7 +150,7 @@ __device__ __forceinline__ T load_elem_rt(const uint8_t *base, int64_t n, int64_
 // ---------------------------------------------------------------------------
 // mask (compiled mask_missing, storage.py:126-153)
 // ---------------------------------------------------------------------------
-constexpr int kMaskAll = 1, kMaskNoEq1 = 2;
+constexpr int kMaskAll = 1, kMaskNoEq1 = 2, kMaskRange = 3;
 
 template <typename T> struct MaskT {
     T lo0, hi0, lo1, hi1, gt, lt;
@@ -172,10 +172,13 @@ template <typename T> struct MaskT {
     }
     // Kernel-level mask mode M (the MASKED template argument): 0 none,
     // kMaskAll every rule, kMaskNoEq1 without the second equality rule
-    // (the common _FillValue + valid_min/valid_max case: 4 fewer ops).
+    // (_FillValue inside the valid range: 4 fewer ops), kMaskRange the two
+    // thresholds only (no equality rule left after mask_mode's trimming,
+    // e.g. C3's _FillValue below valid_min: 2 compares per element).
     template <int M>
     __device__ __forceinline__ bool masked_m(T x) const {
-        if constexpr (M == kMaskNoEq1) return ((x >= lo0) & (x <= hi0)) | (x > gt) | (x < lt);
+        if constexpr (M == kMaskRange) return (x > gt) | (x < lt);
+        else if constexpr (M == kMaskNoEq1) return ((x >= lo0) & (x <= hi0)) | (x > gt) | (x < lt);
         else return masked(x);
     }
 };
@@ -284,15 +287,41 @@ template <typename T> struct TileAcc {
         ucount = 0;
         nan = false;
     }
-    // N values; CONV: all 64 lanes execute this call (uniform trip count).
+    // N values in groups of at most 4; CONV: all 64 lanes execute this call
+    // (uniform trip count).  Floats: the NaN flag is taken from the group
+    // sum, not per element: an unmasked NaN (NaN is never masked) makes the
+    // group sum NaN, so only when some lane's group sum is NaN (a NaN, or
+    // +inf + -inf) does the wave test that group's elements one by one.
     template <int N, int MASKED, bool CONV>
     __device__ __forceinline__ void add_n(const T *x, const MaskT<T> &mk) {
+        if (__builtin_expect(__ballot(add_lazy<N, MASKED, CONV>(x, mk)) != 0, 0))   // wave-uniform, rare
+            check_nan<N>(x);
+    }
+    // add_n without the NaN test: returns whether this lane must run
+    // check_nan on x (the caller batches one ballot over several calls)
+    template <int N, int MASKED, bool CONV>
+    __device__ __forceinline__ bool add_lazy(const T *x, const MaskT<T> &mk) {
+        constexpr int GS = N < 4 ? N : 4;
+        static_assert(N % GS == 0, "add_n: N must be a multiple of the group size");
+        bool bad = false;
+#pragma unroll
+        for (int k0 = 0; k0 < N; k0 += GS) bad |= add_group<GS, MASKED, CONV>(x + k0, mk);
+        return bad;
+    }
+    template <int N>
+    __device__ __forceinline__ void check_nan(const T *x) {
+        if constexpr (TT<T>::kind == 0) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) nan |= (x[k] != x[k]);
+        }
+    }
+    template <int N, int MASKED, bool CONV>
+    __device__ __forceinline__ bool add_group(const T *x, const MaskT<T> &mk) {
         using G = typename GroupSum<T>::type;
         G g = 0;
 #pragma unroll
         for (int k = 0; k < N; ++k) {
             const T v = x[k];
-            if constexpr (TT<T>::kind == 0) nan |= (v != v);
             if constexpr (MASKED) {
                 const bool ok = !mk.template masked_m<MASKED>(v);
                 if constexpr (TT<T>::kind == 0) {
@@ -313,6 +342,8 @@ template <typename T> struct TileAcc {
             }
         }
         sum += (S)g;
+        if constexpr (TT<T>::kind == 0) return g != g;
+        else return false;
     }
     // one element with an externally computed mask bit (generic path)
     __device__ __forceinline__ void add_one(T v, bool is_masked) {

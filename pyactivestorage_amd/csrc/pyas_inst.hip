@@ -1,5 +1,6 @@
-// pyas_inst.hip — instantiates every kernel launcher for ONE dtype, chosen
-// by -DPYAS_INST_<name> (the Makefile builds this file once per dtype).
+// pyas_inst.hip — instantiates the kernel launchers for ONE dtype, chosen by
+// -DPYAS_INST_<name>, part -DPYAS_PART=1|2|3 (the Makefile builds this file
+// once per dtype and part).
 #include "pyas_kernels.hpp"
 
 #if defined(PYAS_INST_i8)
@@ -27,5 +28,13 @@
 #endif
 
 namespace pyas {
-PYAS_INSTANTIATE_LAUNCHERS(PYAS_T)
+#if PYAS_PART == 1
+PYAS_INSTANTIATE_PART1(PYAS_T)
+#elif PYAS_PART == 2
+PYAS_INSTANTIATE_PART2(PYAS_T)
+#elif PYAS_PART == 3
+PYAS_INSTANTIATE_PART3(PYAS_T)
+#else
+#error "define PYAS_PART=1|2|3"
+#endif
 }  // namespace pyas

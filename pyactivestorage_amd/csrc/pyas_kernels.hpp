@@ -111,6 +111,27 @@ __device__ __forceinline__ void consume16(const uint4 &r, TileAcc<T> &acc, const
     acc.template add_n<N, MASKED, CONV>(x, mk);
 }
 
+// U vectors, one NaN ballot for all of them
+template <typename T, bool BSWAP, int MASKED, bool CONV, int U>
+__device__ __forceinline__ void consume16_u(const uint4 *r, TileAcc<T> &acc, const MaskT<T> &mk) {
+    constexpr int N = 16 / sizeof(T);
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        T x[N];
+        unpack16<T, BSWAP>(r[u], x);
+        bad |= acc.template add_lazy<N, MASKED, CONV>(x, mk);
+    }
+    if (__builtin_expect(__ballot(bad) != 0, 0)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            T x[N];
+            unpack16<T, BSWAP>(r[u], x);
+            acc.template check_nan<N>(x);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // contiguous runs
 // ---------------------------------------------------------------------------
@@ -156,13 +177,11 @@ __device__ void run_plain(const uint8_t *base, int64_t m0, int64_t m1, TileAcc<T
             // the next step's loads are in flight while this step is reduced
 #pragma unroll
             for (int u = 0; u < U; ++u) nxt[u] = ldg16(v + (s + 1) * STEP + tid + u * kBlock);
-#pragma unroll
-            for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED, true>(cur[u], acc, mk);
+            consume16_u<T, BSWAP, MASKED, true, U>(cur, acc, mk);
 #pragma unroll
             for (int u = 0; u < U; ++u) cur[u] = nxt[u];
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) consume16<T, BSWAP, MASKED, true>(cur[u], acc, mk);
+        consume16_u<T, BSWAP, MASKED, true, U>(cur, acc, mk);
     }
     for (int64_t k = nsteps * STEP + tid; k < nvec; k += kBlock)
         consume16<T, BSWAP, MASKED, false>(ldg16(v + k), acc, mk);
@@ -401,8 +420,16 @@ __global__ __launch_bounds__(kBlock) void k_combine(const pyas_partial *in, int6
 // Only one arrival per BLOCK of this small kernel: the hot kernel's
 // 16k workgroups never wait on each other (an arrival per reduce workgroup
 // costs ~3 us of store/atomic latency each and was measured 6 % slower).
-// Group partials cross blocks as agent-scope atomics (store/load_partial_agent:
-// sc1 accesses, no L2 write-back/invalidate fences).
+// Hand-off (HIP's scoped C++ memory model, LLVM AMDGPU memory model for
+// gfx950): each block stores its group partial, then increments the counter
+// with an agent-scope acq_rel fetch_add.  Its release half orders the
+// partial's stores before the increment; the increments form one release
+// sequence, so the block whose fetch_add returns ng-1 acquires every earlier
+// block's partial.  That block's thread 0 publishes the fact through LDS and
+// a workgroup barrier, and every thread then issues its own agent-scope
+// acquire fence before reading the partials.  (One release per finish
+// block, ng = n_chunks/256 of them, not per reduce workgroup: the L2
+// write-back a gfx950 agent release costs is paid 16 times for C3.)
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_finish(FinishArgs f) {
     const int64_t lo = (int64_t)blockIdx.x * kCombineSeg;
@@ -438,10 +465,7 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinishArgs f) {
         store_wpartial_agent(f.gtmp + blockIdx.x, acc);
         bool last = false;
         if (f.cnt) {
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            __builtin_amdgcn_s_waitcnt(0);   // the group partial's stores are complete
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            const uint32_t old = __hip_atomic_fetch_add(f.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t old = __hip_atomic_fetch_add(f.cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
             last = old == (uint32_t)ng - 1u;
             if (last) __hip_atomic_store(f.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -449,6 +473,7 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinishArgs f) {
     }
     __syncthreads();
     if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     WAcc<T> tot;   // = k_combine over the group partials (already rounded)
     tot.init();
     for (int64_t i = threadIdx.x; i < ng; i += kBlock) merge(tot, load_partial_agent(f.gtmp + i), false);
@@ -944,6 +969,123 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
     }
 }
 
+// One byte-plane piece of a shuffled vector: W bytes at q (AL: W-aligned)
+template <typename W, bool AL>
+__device__ __forceinline__ W ldp(const uint8_t *q) {
+    if constexpr (AL) {
+        return __builtin_nontemporal_load(reinterpret_cast<const W *>(q));
+    } else {
+        W r;
+        __builtin_memcpy(&r, q, sizeof(W));
+        return r;
+    }
+}
+
+// 16 bytes = N = 16/ES consecutive elements of the plain layout, addressed
+// by `p` in the plain layout of the chunk at `base` (n elements).  With SHUF
+// the chunk is HDF5-shuffled (byte b of element e at b*n + e), so those
+// elements are N consecutive bytes of each of the ES byte planes: ES loads
+// of N bytes (f32: 4 dwords, 256 contiguous bytes per plane per wave),
+// reassembled into the plain bytes with v_perm; the caller's unpack16 then
+// applies the byte order as for plain chunks.  AL: see ldv_aligned.
+template <typename T, bool SHUF, bool AL>
+__device__ __forceinline__ uint4 ldv(const uint8_t *base, const uint8_t *p, int64_t n) {
+    constexpr int ES = sizeof(T);
+    if constexpr (!SHUF || ES == 1) {
+        return ld16<AL>(p);
+    } else {
+        const uint8_t *q = base + ((uint64_t)(p - base) / ES);
+        if constexpr (ES == 4) {          // 4 planes x 4 bytes
+            uint32_t w[4], e[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) w[b] = ldp<uint32_t, AL>(q + b * n);
+            transpose4(w[0], w[1], w[2], w[3], e);
+            return make_uint4(e[0], e[1], e[2], e[3]);
+        } else if constexpr (ES == 2) {   // 2 planes x 8 bytes
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 a = ldp<u32x2, AL>(q), b = ldp<u32x2, AL>(q + n);
+            return make_uint4(perm(b.x, a.x, 0x05010400u), perm(b.x, a.x, 0x07030602u),
+                              perm(b.y, a.y, 0x05010400u), perm(b.y, a.y, 0x07030602u));
+        } else {                          // 8 planes x 2 bytes
+            uint32_t h[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) h[b] = ldp<uint16_t, AL>(q + b * n);
+            const uint32_t x01 = h[0] | (h[1] << 16), x23 = h[2] | (h[3] << 16);
+            const uint32_t x45 = h[4] | (h[5] << 16), x67 = h[6] | (h[7] << 16);
+            return make_uint4(perm(x23, x01, 0x06040200u), perm(x67, x45, 0x06040200u),
+                              perm(x23, x01, 0x07050301u), perm(x67, x45, 0x07050301u));
+        }
+    }
+}
+
+// Whether ldv<T, SHUF, true> may be used on the chunk at `base` of n elements:
+// plain: base 16-B aligned; shuffled: every plane piece W = 16/ES-aligned
+// (vector offsets are multiples of N elements in every dense layout).
+template <typename T, bool SHUF>
+__device__ __forceinline__ bool ldv_aligned(const uint8_t *base, int64_t n) {
+    constexpr int ES = sizeof(T), N = 16 / ES;
+    if constexpr (!SHUF || ES == 1) return ((uintptr_t)base & 15) == 0;
+    else return (((uintptr_t)base | (uint64_t)n) & (N - 1)) == 0;
+}
+
+// A load unit of the row layouts: VPL = (SHUF ? ES : 1) consecutive 16-B
+// vectors of the plain layout.  Shuffled, that is 16 consecutive elements =
+// one 16-B load from each of the ES byte planes (a wave reads 1 KiB of a
+// plane per instruction when its lanes' units are adjacent), transposed
+// into ES plain vectors with v_perm; the caller's unpack16 applies the byte
+// order as for plain chunks.  AL: see ldu_aligned.
+template <typename T, bool SHUF>
+struct Unit {
+    static constexpr int VPL = (SHUF && sizeof(T) > 1) ? (int)sizeof(T) : 1;
+};
+
+template <typename T, bool SHUF, bool AL>
+__device__ __forceinline__ void ldu(const uint8_t *base, const uint8_t *p, int64_t n,
+                                    uint4 v[Unit<T, SHUF>::VPL]) {
+    constexpr int ES = sizeof(T);
+    if constexpr (Unit<T, SHUF>::VPL == 1) {
+        v[0] = ld16<AL>(p);
+    } else {
+        const uint8_t *q = base + ((uint64_t)(p - base) / ES);
+        uint4 pl[ES];
+#pragma unroll
+        for (int b = 0; b < ES; ++b) pl[b] = ld16<AL>(q + b * n);
+        if constexpr (ES == 4) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t e[4];
+                transpose4(word(pl[0], j), word(pl[1], j), word(pl[2], j), word(pl[3], j), e);
+                v[j] = make_uint4(e[0], e[1], e[2], e[3]);
+            }
+        } else if constexpr (ES == 2) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t a0 = word(pl[0], 2 * j), b0 = word(pl[1], 2 * j);
+                const uint32_t a1 = word(pl[0], 2 * j + 1), b1 = word(pl[1], 2 * j + 1);
+                v[j] = make_uint4(perm(b0, a0, 0x05010400u), perm(b0, a0, 0x07030602u),
+                                  perm(b1, a1, 0x05010400u), perm(b1, a1, 0x07030602u));
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                uint32_t lo[4], hi[4];
+                transpose4(word(pl[0], w), word(pl[1], w), word(pl[2], w), word(pl[3], w), lo);
+                transpose4(word(pl[4], w), word(pl[5], w), word(pl[6], w), word(pl[7], w), hi);
+                v[2 * w] = make_uint4(lo[0], hi[0], lo[1], hi[1]);
+                v[2 * w + 1] = make_uint4(lo[2], hi[2], lo[3], hi[3]);
+            }
+        }
+    }
+}
+
+// Whether ldu<T, SHUF, true> may be used on the chunk at `base` of n
+// elements (unit offsets are multiples of 16 elements when shuffled).
+template <typename T, bool SHUF>
+__device__ __forceinline__ bool ldu_aligned(const uint8_t *base, int64_t n) {
+    if constexpr (Unit<T, SHUF>::VPL == 1) return ((uintptr_t)base & 15) == 0;
+    else return (((uintptr_t)base | (uint64_t)n) & 15) == 0;
+}
+
 template <int CTRL, typename V>
 __device__ __forceinline__ V dpp_mov(V v) {
     if constexpr (sizeof(V) <= 4) {
@@ -1024,9 +1166,9 @@ __device__ __forceinline__ void store_group(const TileAcc<T> &a, uint32_t cnt, u
 // One pass of the column layout over one chunk: lane (il, sp) folds split
 // sp of the reduced rows of vector item i (N consecutive kept outputs) into
 // acc[N], PYAS_COL_U 16-B loads in flight.
-template <typename T, bool BSWAP, int MASKED, bool AL>
-__device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base, int64_t i, int sp,
-                                         const MaskT<T> &mk, TileAcc<T> *acc) {
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL>
+__device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base, int64_t n, int64_t i,
+                                         int sp, const MaskT<T> &mk, TileAcc<T> *acc) {
     constexpr int ES = sizeof(T), N = 16 / ES;
     const int S = d.split;
     const int64_t KIV = d.KI / N, R = d.RO * d.RI;
@@ -1044,29 +1186,44 @@ __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base
         if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
     };
     constexpr int U = PYAS_COL_U;
+    static_assert(U % 4 == 0, "PYAS_COL_U: a multiple of the 4-row sum groups");
     int64_t t = 0;
     for (; t + U <= nt; t += U) {
         uint4 w[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) { w[u] = ld16<AL>(p); next(); }
+        for (int u = 0; u < U; ++u) { w[u] = ldv<T, SHUF, AL>(base, p, n); next(); }
+        // output k's U rows as groups of 4 (sums widened once per group,
+        // one mask test per element, per-lane counts)
+        T xs[N][U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             T x[N];
             unpack16<T, BSWAP>(w[u], x);
 #pragma unroll
-            for (int k = 0; k < N; ++k) acc[k].add_one(x[k], MASKED && mk.masked(x[k]));
+            for (int k = 0; k < N; ++k) xs[k][u] = x[k];
+        }
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < N; ++k) bad |= acc[k].template add_lazy<U, MASKED, false>(xs[k], mk);
+        if (__builtin_expect(__ballot(bad) != 0, 0)) {   // a NaN (or inf - inf) somewhere
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc[k].template check_nan<U>(xs[k]);
         }
     }
     for (; t < nt; ++t) {
         T x[N];
-        unpack16<T, BSWAP>(ld16<AL>(p), x);
+        unpack16<T, BSWAP>(ldv<T, SHUF, AL>(base, p, n), x);
         next();
 #pragma unroll
-        for (int k = 0; k < N; ++k) acc[k].add_one(x[k], MASKED && mk.masked(x[k]));
+        for (int k = 0; k < N; ++k) acc[k].template add_n<1, MASKED, false>(x + k, mk);
+    }
+    if constexpr (!MASKED) {   // add_n counts only in masked mode
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k].count += (uint32_t)nt;
     }
 }
 
-template <typename T, bool BSWAP, int MASKED, bool AL>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL>
 __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                           const MaskT<T> &mk, uint4 *stage) {
     constexpr int ES = sizeof(T), N = 16 / ES;
@@ -1081,7 +1238,7 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
 #pragma unroll
         for (int k = 0; k < N; ++k) acc[k].init();
         if (i < items && sp < S && sp < d.RO * d.RI)
-            col_rows<T, BSWAP, MASKED, AL>(d, base, i, sp, mk, acc);
+            col_rows<T, SHUF, BSWAP, MASKED, AL>(d, base, a.r.chunk_elems, i, sp, mk, acc);
         if constexpr (N <= 4) {
             // Stage the pass's IT*N partials (<= 32 KiB) in LDS, then write
             // them as consecutive 16-B stores (a lane's own N partials are
@@ -1118,18 +1275,19 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     }
 }
 
-template <typename T, bool BSWAP, int MASKED, bool AL, int UO>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int UO>
 __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                           const MaskT<T> &mk) {
-    constexpr int ES = sizeof(T), N = 16 / ES;
+    const int64_t n = a.r.chunk_elems;
+    constexpr int ES = sizeof(T), N = 16 / ES, VPL = Unit<T, SHUF>::VPL;
     const AxesDense &d = a.d;
     const int G = d.group, P = kWave / G;
     const int lane = threadIdx.x & (kWave - 1), gl = lane & (G - 1), pg = lane / G;
-    const int64_t VG = d.RI / N / G;                 // vectors per lane per run
-    const int64_t Q = d.RO * VG;                     // vectors per lane per output
+    const int64_t VG = d.RI / N / VPL / G;           // load units per lane per run
+    const int64_t Q = d.RO * VG;                     // load units per lane per output
     const int64_t wave = j * (kBlock / kWave) + threadIdx.x / kWave;
     const int64_t nwaves = d.bpc * (kBlock / kWave);
-    const int64_t vstep = (int64_t)G * N * ES;                   // bytes
+    const int64_t vstep = (int64_t)G * N * VPL * ES;             // bytes (plain layout)
     const int64_t wrap = (d.KO - 1) * d.RI * ES;                 // next run of the output
     pyas_partial *out = a.out + a.out_offsets[c];
     for (int64_t o0 = wave * P * UO; o0 < d.KO; o0 += nwaves * P * UO) {   // wave-uniform
@@ -1137,52 +1295,46 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
 #pragma unroll
         for (int u = 0; u < UO; ++u) acc[u].init();
         if constexpr (UO > 1) {
-            // one vector per lane per output (RO == 1, RI == G*N): UO outputs in flight
-            uint4 w[UO];
+            // one unit per lane per output (RO == 1, RI == G*N*VPL): UO outputs in flight
+            uint4 w[UO][VPL];
 #pragma unroll
             for (int u = 0; u < UO; ++u) {
                 const int64_t o = o0 + u * P + pg;
-                if (o < d.KO) w[u] = ld16<AL>(base + (o * d.RI + gl * N) * ES);
+                if (o < d.KO) ldu<T, SHUF, AL>(base, base + (o * d.RI + gl * N * VPL) * ES, n, w[u]);
             }
 #pragma unroll
             for (int u = 0; u < UO; ++u) {
                 const int64_t o = o0 + u * P + pg;
                 if (o < d.KO) {
-                    T x[N];
-                    unpack16<T, BSWAP>(w[u], x);
-                    acc[u].template add_n<N, MASKED, false>(x, mk);
-                    if constexpr (!MASKED) acc[u].count += N;
+                    consume16_u<T, BSWAP, MASKED, false, VPL>(w[u], acc[u], mk);
+                    if constexpr (!MASKED) acc[u].count += N * VPL;
                 }
             }
         } else {
             const int64_t o = o0 + pg;
             if (o < d.KO) {
-                const uint8_t *p = base + (o * d.RI + gl * N) * ES;
+                const uint8_t *p = base + (o * d.RI + gl * N * VPL) * ES;
                 int64_t vc = 0;
                 auto next = [&]() {
                     p += vstep;
                     if (++vc == VG) { vc = 0; p += wrap; }
                 };
-                constexpr int U = 4;
+                // units in flight: 4 plain vectors, or 2 (f32) / 1 (f64) shuffled units
+                constexpr int U = VPL == 1 ? 4 : (VPL >= 8 ? 1 : 8 / VPL);
                 int64_t t = 0;
                 for (; t + U <= Q; t += U) {
-                    uint4 w[U];
+                    uint4 w[U * VPL];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) { w[u] = ld16<AL>(p); next(); }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        T x[N];
-                        unpack16<T, BSWAP>(w[u], x);
-                        acc[0].template add_n<N, MASKED, false>(x, mk);
-                    }
+                    for (int u = 0; u < U; ++u) { ldu<T, SHUF, AL>(base, p, n, w + u * VPL); next(); }
+                    consume16_u<T, BSWAP, MASKED, false, U * VPL>(w, acc[0], mk);
                 }
                 for (; t < Q; ++t) {
-                    T x[N];
-                    unpack16<T, BSWAP>(ld16<AL>(p), x);
+                    uint4 w[VPL];
+                    ldu<T, SHUF, AL>(base, p, n, w);
                     next();
-                    acc[0].template add_n<N, MASKED, false>(x, mk);
+                    consume16_u<T, BSWAP, MASKED, false, VPL>(w, acc[0], mk);
                 }
-                if constexpr (!MASKED) acc[0].count += (uint32_t)(Q * N);
+                if constexpr (!MASKED) acc[0].count += (uint32_t)(Q * N * VPL);
             }
         }
 #pragma unroll
@@ -1210,33 +1362,37 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <typename T, bool BSWAP, int MASKED, bool AL, int H>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int H>
 __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                               const MaskT<T> &mk, uint4 *tile) {
-    constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, UL = 16 / H;
+    const int64_t n = a.r.chunk_elems;
+    constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
+    // load units per lane per tile (64 * UL * VPL >= the tile's RPW * 16 vectors)
+    constexpr int UL = 16 / H / VPL > 0 ? 16 / H / VPL : 1;
     const AxesDense &d = a.d;
-    const int V = (int)(d.RI / N);                  // vectors per run, V % H == 0
+    const int V = (int)(d.RI / N);                  // vectors per run, V % H == 0, V % VPL == 0
     const int VH = V / H;                           // vectors per lane
     const int lane = threadIdx.x & (kWave - 1), r = lane / H, h = lane - r * H;
     uint4 *t = tile + (threadIdx.x / kWave) * RPW * kRowLdsStride;
     const int64_t wave = j * (kBlock / kWave) + threadIdx.x / kWave;
     const int64_t nwaves = d.bpc * (kBlock / kWave);
     pyas_partial *out = a.out + a.out_offsets[c];
-    // tile vector q = u * kWave + lane lands in run q / V, column q % V
+    // tile unit q = u * kWave + lane: vectors q*VPL .. +VPL-1, in run q*VPL / V
     int lrow[UL], lcol[UL];
 #pragma unroll
     for (int u = 0; u < UL; ++u) {
-        const int q = u * kWave + lane;
+        const int q = (u * kWave + lane) * VPL;
         lrow[u] = q / V;
         lcol[u] = q - lrow[u] * V;
     }
-    uint4 w[UL];
+    uint4 w[UL][VPL];
     auto load = [&](int64_t o0) {
         const int64_t nvec = (d.KO - o0 < RPW ? d.KO - o0 : RPW) * V;
         const uint8_t *src = base + o0 * d.RI * ES;
 #pragma unroll
         for (int u = 0; u < UL; ++u)
-            if (u * kWave + lane < nvec) w[u] = ld16<AL>(src + (int64_t)(u * kWave + lane) * 16);
+            if ((u * kWave + lane) * VPL < nvec)
+                ldu<T, SHUF, AL>(base, src + (int64_t)(u * kWave + lane) * VPL * 16, n, w[u]);
     };
     int64_t o0 = wave * RPW;
     if (o0 < d.KO) load(o0);
@@ -1244,7 +1400,10 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
         const int64_t nvec = (d.KO - o0 < RPW ? d.KO - o0 : RPW) * V;
 #pragma unroll
         for (int u = 0; u < UL; ++u)
-            if (u * kWave + lane < nvec) t[lrow[u] * kRowLdsStride + lcol[u]] = w[u];
+            if ((u * kWave + lane) * VPL < nvec) {
+#pragma unroll
+                for (int i = 0; i < VPL; ++i) t[lrow[u] * kRowLdsStride + lcol[u] + i] = w[u][i];
+            }
         wave_sync_lds();
         if (o0 + nwaves * RPW < d.KO) load(o0 + nwaves * RPW);
         TileAcc<T> acc;
@@ -1268,7 +1427,7 @@ __device__ __forceinline__ bool dense_owns(const AxesArgs &a, const Sel &s) {
     return a.d.mode != 0 && chunk_is_full(s, a.r.shape, a.r.ndim);
 }
 
-template <typename T, bool BSWAP, int MASKED, int MODE>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
 __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs a) {
     const int64_t c = blockIdx.x / a.d.bpc;
     const int64_t j = blockIdx.x - c * a.d.bpc;
@@ -1279,23 +1438,23 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs 
     const uint8_t *base = r.data + r.offsets[c];
     MaskT<T> mk;
     mk.init(r.mask);
-    const bool al = ((uintptr_t)base & 15) == 0;
+    const bool al = MODE == 1 ? ldv_aligned<T, SHUF>(base, r.chunk_elems) : ldu_aligned<T, SHUF>(base, r.chunk_elems);
     if constexpr (MODE == 1) {
         // staging for coalesced partial stores (dense_col, N <= 4): 32 KiB
         __shared__ uint4 stage[sizeof(T) >= 4 ? kBlock * 4 * 2 : 1];
-        if (al) dense_col<T, BSWAP, MASKED, true>(a, c, j, base, mk, stage);
-        else dense_col<T, BSWAP, MASKED, false>(a, c, j, base, mk, stage);
+        if (al) dense_col<T, SHUF, BSWAP, MASKED, true>(a, c, j, base, mk, stage);
+        else dense_col<T, SHUF, BSWAP, MASKED, false>(a, c, j, base, mk, stage);
     } else if constexpr (MODE >= 4) {
         constexpr int H = MODE == 4 ? 1 : MODE == 5 ? 2 : 4;
         __shared__ uint4 tile[(kBlock / kWave) * (kWave / H) * kRowLdsStride];
-        if (al) dense_row_lds<T, BSWAP, MASKED, true, H>(a, c, j, base, mk, tile);
-        else dense_row_lds<T, BSWAP, MASKED, false, H>(a, c, j, base, mk, tile);
+        if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H>(a, c, j, base, mk, tile);
+        else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H>(a, c, j, base, mk, tile);
     } else if constexpr (MODE == 2) {
-        if (al) dense_row<T, BSWAP, MASKED, true, 1>(a, c, j, base, mk);
-        else dense_row<T, BSWAP, MASKED, false, 1>(a, c, j, base, mk);
+        if (al) dense_row<T, SHUF, BSWAP, MASKED, true, 1>(a, c, j, base, mk);
+        else dense_row<T, SHUF, BSWAP, MASKED, false, 1>(a, c, j, base, mk);
     } else {
-        if (al) dense_row<T, BSWAP, MASKED, true, 4>(a, c, j, base, mk);
-        else dense_row<T, BSWAP, MASKED, false, 4>(a, c, j, base, mk);
+        if (al) dense_row<T, SHUF, BSWAP, MASKED, true, 4>(a, c, j, base, mk);
+        else dense_row<T, SHUF, BSWAP, MASKED, false, 4>(a, c, j, base, mk);
     }
 }
 
@@ -1307,7 +1466,7 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs 
 // the same rounding) into a running WAcc per output.  The arithmetic is
 // k_axes_dense + k_combine_grid's, operation for operation, so the result is
 // bit-identical; the per-chunk partial arrays are never written.
-template <typename T, bool BSWAP, int MASKED>
+template <typename T, bool SHUF, bool BSWAP, int MASKED>
 __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold(AxesArgs a, FoldGrid g) {
     constexpr int N = 16 / sizeof(T);
     const AxesDense &d = a.d;
@@ -1357,8 +1516,10 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold(AxesArgs a
 #pragma unroll
             for (int k = 0; k < N; ++k) acc[k].init();
             if (i < items && sp < S && sp < d.RO * d.RI) {
-                if (((uintptr_t)base & 15) == 0) col_rows<T, BSWAP, MASKED, true>(d, base, i, sp, mk, acc);
-                else col_rows<T, BSWAP, MASKED, false>(d, base, i, sp, mk, acc);
+                if (ldv_aligned<T, SHUF>(base, r.chunk_elems))
+                    col_rows<T, SHUF, BSWAP, MASKED, true>(d, base, r.chunk_elems, i, sp, mk, acc);
+                else
+                    col_rows<T, SHUF, BSWAP, MASKED, false>(d, base, r.chunk_elems, i, sp, mk, acc);
             }
 #pragma unroll
             for (int k = 0; k < N; ++k) {
@@ -1396,9 +1557,10 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold(AxesArgs a
 // does, then merges the partial store_group would write into a running WAcc
 // (k_combine_grid's merge, same rounding).  Bit-identical to k_axes_dense +
 // k_combine_grid; the next layer's tile is loaded while this one is folded.
-template <typename T, bool BSWAP, int MASKED, int H>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int H>
 __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold_row(AxesArgs a, FoldGrid g) {
-    constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, UL = 16 / H;
+    constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
+    constexpr int UL = 16 / H / VPL > 0 ? 16 / H / VPL : 1;   // load units per lane per tile
     __shared__ uint4 tile[(kBlock / kWave) * RPW * kRowLdsStride];
     const AxesDense &d = a.d;
     const ReduceArgs &r = a.r;
@@ -1444,21 +1606,23 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold_row(AxesAr
     int lrow[UL], lcol[UL];
 #pragma unroll
     for (int u = 0; u < UL; ++u) {
-        const int q = u * kWave + lane;
+        const int q = (u * kWave + lane) * VPL;
         lrow[u] = q / V;
         lcol[u] = q - lrow[u] * V;
     }
-    uint4 w[UL];
+    uint4 w[UL][VPL];
     auto load = [&](const uint8_t *base, int64_t o0, int64_t nvec) {
         const uint8_t *src = base + o0 * d.RI * ES;
-        if (((uintptr_t)src & 15) == 0) {
+        if (ldu_aligned<T, SHUF>(SHUF ? base : src, r.chunk_elems)) {
 #pragma unroll
             for (int u = 0; u < UL; ++u)
-                if (u * kWave + lane < nvec) w[u] = ld16<true>(src + (int64_t)(u * kWave + lane) * 16);
+                if ((u * kWave + lane) * VPL < nvec)
+                    ldu<T, SHUF, true>(base, src + (int64_t)(u * kWave + lane) * VPL * 16, r.chunk_elems, w[u]);
         } else {
 #pragma unroll
             for (int u = 0; u < UL; ++u)
-                if (u * kWave + lane < nvec) w[u] = ld16<false>(src + (int64_t)(u * kWave + lane) * 16);
+                if ((u * kWave + lane) * VPL < nvec)
+                    ldu<T, SHUF, false>(base, src + (int64_t)(u * kWave + lane) * VPL * 16, r.chunk_elems, w[u]);
         }
     };
     for (int64_t o0 = wave * RPW; o0 < d.KO; o0 += nwaves * RPW) {   // wave-uniform
@@ -1469,7 +1633,10 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold_row(AxesAr
         for (int64_t l = 0; l < g.n_layers; ++l) {
 #pragma unroll
             for (int u = 0; u < UL; ++u)
-                if (u * kWave + lane < nvec) t[lrow[u] * kRowLdsStride + lcol[u]] = w[u];
+                if ((u * kWave + lane) * VPL < nvec) {
+#pragma unroll
+                    for (int i = 0; i < VPL; ++i) t[lrow[u] * kRowLdsStride + lcol[u] + i] = w[u][i];
+                }
             wave_sync_lds();
             if (l + 1 < g.n_layers) load(layer_base(l + 1), o0, nvec);
             TileAcc<T> acc;
@@ -1577,6 +1744,18 @@ __global__ __launch_bounds__(kBlock) void k_select(SelectArgs a) {
 // ---------------------------------------------------------------------------
 // per-dtype launchers (declared in pyas_internal.hpp)
 // ---------------------------------------------------------------------------
+// Kernel mask mode for the scalar rules left in m (prepare() has dropped
+// equality rules a threshold already covers): 0 unmasked, kMaskRange
+// thresholds only, kMaskNoEq1 one equality interval + thresholds, kMaskAll.
+inline int mask_mode(const pyas_mask &m, bool masked) {
+    if (!masked) return 0;
+    const uint32_t f = m.flags;
+    if (f & (PYAS_MASK_TAB0 | PYAS_MASK_TAB1)) return kMaskAll;
+    if (!(f & (PYAS_MASK_EQ0 | PYAS_MASK_EQ1))) return kMaskRange;
+    if (!(f & PYAS_MASK_EQ1)) return kMaskNoEq1;
+    return kMaskAll;
+}
+
 template <typename T, bool SEL>
 static void launch_reduce_ts(const ReduceArgs &a, bool shuf, bool bsw, bool masked, dim3 g,
                              hipStream_t st) {
@@ -1587,23 +1766,24 @@ static void launch_reduce_ts(const ReduceArgs &a, bool shuf, bool bsw, bool mask
             hipLaunchKernelGGL((k_reduce_u<T, S, B, M, SEL>), g, blk, 0, st, a);       \
         else hipLaunchKernelGGL((k_reduce<T, S, B, M>), g, blk, 0, st, a);             \
     } while (0)
-    // the lean kernel also has a variant without the second equality rule
-    const bool no_eq1 = !SEL && sizeof(T) >= 4 && !(a.mask.flags & PYAS_MASK_EQ1);
+    // the lean kernel also has variants with fewer rules (mask_mode)
+    const int mm = mask_mode(a.mask, masked);
     if constexpr (sizeof(T) == 1) {
         if (masked) PYAS_L(false, false, kMaskAll);
         else PYAS_L(false, false, 0);
     } else if constexpr (!SEL && sizeof(T) >= 4) {
 #define PYAS_LM(S, B)                                                 \
         do {                                                          \
-            if (!masked) PYAS_L(S, B, 0);                             \
-            else if (no_eq1) PYAS_L(S, B, kMaskNoEq1);                \
+            if (!mm) PYAS_L(S, B, 0);                                 \
+            else if (mm == kMaskRange) PYAS_L(S, B, kMaskRange);      \
+            else if (mm == kMaskNoEq1) PYAS_L(S, B, kMaskNoEq1);      \
             else PYAS_L(S, B, kMaskAll);                              \
         } while (0)
         if (shuf) { if (bsw) PYAS_LM(true, true); else PYAS_LM(true, false); }
         else { if (bsw) PYAS_LM(false, true); else PYAS_LM(false, false); }
 #undef PYAS_LM
     } else {
-        (void)no_eq1;
+        (void)mm;
         if (shuf) {
             if (bsw) { if (masked) PYAS_L(true, true, kMaskAll); else PYAS_L(true, true, 0); }
             else { if (masked) PYAS_L(true, false, kMaskAll); else PYAS_L(true, false, 0); }
@@ -1659,16 +1839,31 @@ hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int
     return hipGetLastError();
 }
 
+// Mask modes: all four for little-endian >= 4-byte data, {0, kMaskAll}
+// for byte-swapped or narrow data (fewer instantiations; same results).
+template <typename T, bool SHUF, int MODE>
+static void launch_dense_ms(const AxesArgs &a, bool masked, dim3 g, hipStream_t st) {
+    const dim3 blk(kBlock);
+    const int mm = mask_mode(a.r.mask, masked);
+    if (a.bswap && sizeof(T) > 1) {
+        if (mm) hipLaunchKernelGGL((k_axes_dense<T, SHUF, true, kMaskAll, MODE>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_dense<T, SHUF, true, 0, MODE>), g, blk, 0, st, a);
+        return;
+    }
+    if constexpr (sizeof(T) >= 4) {
+        if (mm == kMaskRange) { hipLaunchKernelGGL((k_axes_dense<T, SHUF, false, kMaskRange, MODE>), g, blk, 0, st, a); return; }
+        if (mm == kMaskNoEq1) { hipLaunchKernelGGL((k_axes_dense<T, SHUF, false, kMaskNoEq1, MODE>), g, blk, 0, st, a); return; }
+    }
+    if (mm) hipLaunchKernelGGL((k_axes_dense<T, SHUF, false, kMaskAll, MODE>), g, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_axes_dense<T, SHUF, false, 0, MODE>), g, blk, 0, st, a);
+}
+
 template <typename T, int MODE>
 static void launch_dense_m(const AxesArgs &a, bool masked, dim3 g, hipStream_t st) {
-    const dim3 blk(kBlock);
-    if (a.bswap && sizeof(T) > 1) {
-        if (masked) hipLaunchKernelGGL((k_axes_dense<T, true, true, MODE>), g, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_axes_dense<T, true, false, MODE>), g, blk, 0, st, a);
-    } else {
-        if (masked) hipLaunchKernelGGL((k_axes_dense<T, false, true, MODE>), g, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_axes_dense<T, false, false, MODE>), g, blk, 0, st, a);
+    if constexpr (sizeof(T) > 1) {
+        if (a.shuf) { launch_dense_ms<T, true, MODE>(a, masked, g, st); return; }
     }
+    launch_dense_ms<T, false, MODE>(a, masked, g, st);
 }
 
 template <typename T>
@@ -1683,22 +1878,50 @@ hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hip
     return hipGetLastError();
 }
 
+template <typename T, bool SHUF, int H>
+static void launch_fold_row_s(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
+    const dim3 blk(kBlock);
+    const int mm = mask_mode(a.r.mask, masked);
+    if (a.bswap) {
+        if (mm) hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, true, kMaskAll, H>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, true, 0, H>), gr, blk, 0, st, a, g);
+    } else if (mm == kMaskRange) {
+        hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, kMaskRange, H>), gr, blk, 0, st, a, g);
+    } else if (mm == kMaskNoEq1) {
+        hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, kMaskNoEq1, H>), gr, blk, 0, st, a, g);
+    } else {
+        if (mm) hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, kMaskAll, H>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, 0, H>), gr, blk, 0, st, a, g);
+    }
+}
+
 template <typename T, int H>
 static void launch_fold_row(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
+    if (a.shuf) launch_fold_row_s<T, true, H>(a, g, masked, gr, st);
+    else launch_fold_row_s<T, false, H>(a, g, masked, gr, st);
+}
+
+template <typename T, bool SHUF>
+static void launch_fold_col(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
     const dim3 blk(kBlock);
+    const int mm = mask_mode(a.r.mask, masked);
     if (a.bswap) {
-        if (masked) hipLaunchKernelGGL((k_axes_fold_row<T, true, 1, H>), gr, blk, 0, st, a, g);
-        else hipLaunchKernelGGL((k_axes_fold_row<T, true, 0, H>), gr, blk, 0, st, a, g);
+        if (mm) hipLaunchKernelGGL((k_axes_fold<T, SHUF, true, kMaskAll>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold<T, SHUF, true, 0>), gr, blk, 0, st, a, g);
+    } else if (mm == kMaskRange) {
+        hipLaunchKernelGGL((k_axes_fold<T, SHUF, false, kMaskRange>), gr, blk, 0, st, a, g);
+    } else if (mm == kMaskNoEq1) {
+        hipLaunchKernelGGL((k_axes_fold<T, SHUF, false, kMaskNoEq1>), gr, blk, 0, st, a, g);
     } else {
-        if (masked) hipLaunchKernelGGL((k_axes_fold_row<T, false, 1, H>), gr, blk, 0, st, a, g);
-        else hipLaunchKernelGGL((k_axes_fold_row<T, false, 0, H>), gr, blk, 0, st, a, g);
+        if (mm) hipLaunchKernelGGL((k_axes_fold<T, SHUF, false, kMaskAll>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold<T, SHUF, false, 0>), gr, blk, 0, st, a, g);
     }
 }
 
 template <typename T>
 hipError_t launch_axes_fold_t(const AxesArgs &a, const FoldGrid &g, bool masked, int64_t grid,
                               hipStream_t st) {
-    const dim3 gr((unsigned)grid), blk(kBlock);
+    const dim3 gr((unsigned)grid);
     if constexpr (sizeof(T) < 4) {
         return hipErrorInvalidValue;     // dense_geometry: >= 4-byte elements only
     } else if (a.d.mode >= 4) {
@@ -1706,13 +1929,8 @@ hipError_t launch_axes_fold_t(const AxesArgs &a, const FoldGrid &g, bool masked,
         else if (a.d.mode == 5) launch_fold_row<T, 2>(a, g, masked, gr, st);
         else launch_fold_row<T, 4>(a, g, masked, gr, st);
     } else {
-        if (a.bswap) {
-            if (masked) hipLaunchKernelGGL((k_axes_fold<T, true, 1>), gr, blk, 0, st, a, g);
-            else hipLaunchKernelGGL((k_axes_fold<T, true, 0>), gr, blk, 0, st, a, g);
-        } else {
-            if (masked) hipLaunchKernelGGL((k_axes_fold<T, false, 1>), gr, blk, 0, st, a, g);
-            else hipLaunchKernelGGL((k_axes_fold<T, false, 0>), gr, blk, 0, st, a, g);
-        }
+        if (a.shuf) launch_fold_col<T, true>(a, g, masked, gr, st);
+        else launch_fold_col<T, false>(a, g, masked, gr, st);
     }
     return hipGetLastError();
 }
@@ -1807,8 +2025,11 @@ hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, vo
     return hipGetLastError();
 }
 
-// Explicit instantiation of every launcher for one dtype (pyas_inst.hip).
-#define PYAS_INSTANTIATE_LAUNCHERS(T)                                                          \
+// Explicit instantiation of every launcher for one dtype (pyas_inst.hip), in
+// three parts compiled as separate objects (the build runs them in parallel):
+// 1 the streaming reduce, combines, select, format and the generic axes
+// kernel; 2 the dense partial-axis kernels; 3 the in-kernel layer folds.
+#define PYAS_INSTANTIATE_PART1(T)                                                              \
     template hipError_t launch_reduce_t<T>(const ReduceArgs &, bool, bool, bool, int64_t,     \
                                            hipStream_t);                                      \
     template hipError_t launch_finish_t<T>(const FinishArgs &, hipStream_t);                  \
@@ -1821,11 +2042,13 @@ hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, vo
     template hipError_t launch_combine_grid_t<T>(const pyas_partial *, const pyas_grid &,     \
                                                  int64_t, int64_t, uint32_t, pyas_partial *,  \
                                                  hipStream_t);                               \
-    template hipError_t launch_axes_dense_t<T>(const AxesArgs &, bool, int64_t, hipStream_t); \
-    template hipError_t launch_axes_fold_t<T>(const AxesArgs &, const FoldGrid &, bool, int64_t, \
-                                              hipStream_t);                                   \
     template hipError_t launch_select_t<T>(const SelectArgs &, int64_t, hipStream_t);         \
     template hipError_t launch_format_t<T>(const pyas_partial *, int64_t, int32_t, void *,    \
                                            uint8_t *, int64_t *, hipStream_t);
+#define PYAS_INSTANTIATE_PART2(T)                                                              \
+    template hipError_t launch_axes_dense_t<T>(const AxesArgs &, bool, int64_t, hipStream_t);
+#define PYAS_INSTANTIATE_PART3(T)                                                              \
+    template hipError_t launch_axes_fold_t<T>(const AxesArgs &, const FoldGrid &, bool, int64_t, \
+                                              hipStream_t);
 
 }  // namespace pyas

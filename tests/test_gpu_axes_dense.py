@@ -1,7 +1,8 @@
 """GPU parity of the dense partial-axis kernels (``k_axes_dense``) against
 the oracle.
 
-The dense kernels take fully selected, unshuffled chunks whose merged dims
+The dense kernels take fully selected chunks (plain or HDF5-shuffled: the
+shuffled form loads each 16-B vector as one piece per byte plane) whose merged dims
 fit (RO, KO, RI, KI) with 16-byte inner runs (column layout: kept inner run;
 row layout: reduced inner run, including the 4-outputs-per-lane variant).
 The reference semantics are ``storage.py:95-100`` (``chunk[sel]``, mask,
@@ -19,7 +20,7 @@ import pytest
 from oracle import storage_ref as ref
 from pyactivestorage_amd import _lib, engine
 from pyactivestorage_amd import storage as pas
-from tests._compare import assert_counts, assert_same
+from tests._compare import assert_counts, assert_same, shuffle_bytes
 
 pytestmark = pytest.mark.gpu
 
@@ -68,20 +69,24 @@ def _cases():
 CASES = _cases()
 
 
+@pytest.mark.parametrize("shuf", [False, True])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_dense_chunk_matches_oracle(gpu, case):
+def test_dense_chunk_matches_oracle(gpu, case, shuf):
     dt, shape, mi = CASES[case]
     miss = _missings(dt)[mi]
     rng = np.random.default_rng(case)
     arr = _data(dt, shape, rng, nan=(case % 4 == 0))
-    raw = arr.tobytes()
+    es = np.dtype(dt).itemsize
+    raw = shuffle_bytes(arr, es) if shuf else arr.tobytes()
+    rf = [ref.Shuffle(es)] if shuf else None
+    gf = [pas.Shuffle(es)] if shuf else None
     sel = tuple(slice(0, n, 1) for n in shape)
     for axis in _axes(len(shape)):
         for method in METHODS:
-            what = f"{dt} {shape} miss={miss} axis={axis} {method.__name__}"
-            want, wn = ref.reduce_chunk_bytes(raw, None, None, miss, dt, shape, "C", sel, axis, method)
-            got, gn = pas.reduce_chunk_bytes(raw, None, None, miss, dt, shape, "C", sel, axis, method)
-            masked_sel, _ = ref.reduce_chunk_bytes(raw, None, None, miss, dt, shape, "C", sel, axis, None)
+            what = f"{dt} {shape} shuf={shuf} miss={miss} axis={axis} {method.__name__}"
+            want, wn = ref.reduce_chunk_bytes(raw, None, rf, miss, dt, shape, "C", sel, axis, method)
+            got, gn = pas.reduce_chunk_bytes(raw, None, gf, miss, dt, shape, "C", sel, axis, method)
+            masked_sel, _ = ref.reduce_chunk_bytes(raw, None, rf, miss, dt, shape, "C", sel, axis, None)
             with np.errstate(all="ignore"):
                 abs_sum = np.ma.sum(np.abs(np.ma.asarray(masked_sel).astype(np.float64)),
                                     axis=axis, keepdims=True)
@@ -100,11 +105,14 @@ def _oracle_partials(arr, sel, axis, miss, dt):
     return v, m, cnt
 
 
+@pytest.mark.parametrize("shuf", [False, True])
 @pytest.mark.parametrize("dt", ["<f4", ">f8", "<i2", "<u8"])
 @pytest.mark.parametrize("axes", [(0,), (2,), (1, 2), (0, 2)])
-def test_dense_batch_mixed_and_misaligned(gpu, dt, axes):
+def test_dense_batch_mixed_and_misaligned(gpu, dt, axes, shuf):
     """One pyas_reduce_axes call over 6 chunks: full and hyperslab selections
-    interleaved, chunk offsets at element (not 16-byte) alignment."""
+    interleaved, chunk offsets at element (not 16-byte) alignment; shuffled:
+    <i2 chunks are not 8-byte aligned, so their plane pieces take the
+    unaligned loads."""
     from pyactivestorage_amd.batch import ReductionPlan
     from pyactivestorage_amd.device import DeviceBuffer, get_context
     dt = np.dtype(dt)
@@ -121,7 +129,8 @@ def test_dense_batch_mixed_and_misaligned(gpu, dt, axes):
     offsets = np.array([k * (cbytes + es) + es for k in range(6)], dtype=np.int64)
     blob = np.zeros(int(offsets[-1]) + cbytes + 16, dtype=np.uint8)
     for k, a in enumerate(chunks):
-        blob[offsets[k]:offsets[k] + cbytes] = np.frombuffer(a.tobytes(), np.uint8)
+        raw = shuffle_bytes(a, es) if shuf else a.tobytes()
+        blob[offsets[k]:offsets[k] + cbytes] = np.frombuffer(raw, np.uint8)
     dbuf = DeviceBuffer(ctx, blob.nbytes)
     ctx.h2d(dbuf.ptr, blob, st)
     miss = (42, None, 0, 90)
@@ -129,7 +138,7 @@ def test_dense_batch_mixed_and_misaligned(gpu, dt, axes):
     csels = [selection.normalize(s, shape) for s in sels]
     plan = ReductionPlan(ctx, dt, shape, dbuf.ptr, offsets,
                          selections=[selection.ChunkSel(c.dims, c.shape, c.kept) for c in csels],
-                         missing=miss, stream=st)
+                         missing=miss, stream=st, shuffle=es if shuf else 0)
     n_outs = [int(np.prod([1 if d in axes else c.shape[d] for d in range(3)])) for c in csels]
     out_offs = np.concatenate([[0], np.cumsum(n_outs)[:-1]]).astype(np.int64)
     offs_t = DeviceBuffer(ctx, out_offs.nbytes)

@@ -1,6 +1,9 @@
 """Partial-axis reduction throughput (row f1) on the C3 workload:
 1024^3 f32 in 64^3 chunks, _FillValue + valid_min/valid_max, device-resident.
-Reports GB/s of pyas_reduce_axes for several axis sets (per chunk, keepdims)."""
+Reports GB/s of pyas_reduce_axes for several axis sets (per chunk, keepdims),
+or with --fold of pyas_reduce_axes_grid (the whole-variable box query with
+the chunk layers folded in the kernel, what Active runs on resident data).
+--shuffle stores the chunks HDF5-byte-shuffled."""
 import json
 import os
 import sys
@@ -31,6 +34,34 @@ def main():
                          shuffle=4 if shuffled else 0)
     nbytes = data.numel()
     res = {}
+    if "--fold" in sys.argv:
+        grid_n = [s // c for s, c in zip(shape, chunks)]
+        for axes in ((0,), (1,), (2,), (0, 1), (1, 2), (0, 2)):
+            g = _lib.Grid()
+            g.ndim = 3
+            g.axes_mask = sum(1 << a for a in axes)
+            for d in range(3):
+                g.n_coords[d] = grid_n[d]
+                g.out_extent[d] = 1 if d in axes else shape[d]
+            n_final = int(np.prod([1 if d in axes else shape[d] for d in range(3)]))
+            fin = DeviceBuffer(ctx, n_final * _lib.PARTIAL_NBYTES)
+            try:
+                engine.reduce_axes_grid(ctx, plan.batch, plan.mask_up.struct, g, fin.ptr, True, st)
+            except NotImplementedError as exc:
+                res[str(axes)] = {"refused": str(exc)}
+                continue
+            torch.cuda.synchronize()
+            reps = 5
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                engine.reduce_axes_grid(ctx, plan.batch, plan.mask_up.struct, g, fin.ptr, True, st)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / reps
+            res[str(axes)] = {"ms": round(dt * 1e3, 3), "GBps": round(nbytes / dt / 1e9, 1), "outputs": n_final}
+            del fin
+        print(json.dumps({"workload": "c3 box query, chunk layers folded in-kernel (pyas_reduce_axes_grid)"
+                          + (", byte-shuffled chunks" if shuffled else ""), "results": res}))
+        return
     for axes in ((0,), (1,), (2,), (0, 1), (1, 2), (0, 2)):
         n_out = int(np.prod([1 if d in axes else chunks[d] for d in range(3)]))
         out = DeviceBuffer(ctx, len(offsets) * n_out * _lib.PARTIAL_NBYTES)
