@@ -403,8 +403,10 @@ typedef struct pyas_coalescer pyas_coalescer;
 int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch,
                           pyas_coalescer **out);
 int pyas_coalescer_destroy(pyas_coalescer *c);
-/* stats (int64[6]): batches dispatched, chunks reduced, largest batch,
- * dispatcher busy ns, callers' file-read ns, callers' wait-for-batch ns */
+/* stats (int64[7]): batches dispatched, chunks reduced, largest batch,
+ * dispatcher busy ns (launching), callers' file-read ns, callers'
+ * wait-for-batch ns, device-queue ns (per batch: from its launch, or the
+ * previous batch's completion if later, to its completion) */
 int pyas_coalescer_stats(pyas_coalescer *c, int64_t *stats);
 /* Reduce file `path` bytes [offset, offset + size) as one chunk described by
  * desc/mask (mask without vector tables), selection `sel` (host

@@ -10,14 +10,24 @@
 // Here concurrent calls are coalesced without changing the calling pattern:
 //   caller thread  : open + pread(2) of its chunk straight into a pinned host
 //                    ring (ctypes released the GIL), then sleep;
-//   dispatcher     : take the longest prefix of the ring whose reads are done,
-//                    copy it H2D in one or two copies (a wrapped ring), inflate
-//                    every zlib stream of the batch in one launch, reduce every
-//                    chunk in one launch per (layout, mask, axes) group, copy
-//                    every partial back in one copy, wait on the batch's event,
-//                    wake the callers.
-// Batches grow with load (callers keep filling the ring while the previous
-// batch runs) and there are no timers.  Anything the batch cannot express —
+//   dispatcher     : take the longest prefix of the ring's unsubmitted
+//                    requests whose reads are done, copy it H2D in one or two
+//                    copies (a wrapped ring), inflate every zlib stream of the
+//                    batch in one launch, reduce every chunk in one launch per
+//                    (layout, mask, axes) group, copy every partial back in one
+//                    copy, record the batch's event -- and go on to the next
+//                    batch without waiting (up to `depth` batches in flight,
+//                    each with its own scratch slot);
+//   completer      : wait on the oldest batch's event, hand each caller its
+//                    partials, wake exactly those callers, free their ring
+//                    space.
+// Batches grow with load (callers keep filling the ring while earlier
+// batches run) and there are no timers.  Only the launches are serial: the
+// device round trip of one batch overlaps the next batch's launch, and the
+// batches in flight run side by side (one stream per slot; a zlib batch's
+// inflate is one wave per chunk, latency-bound).  The chunk bytes go H2D on
+// a copy stream; the batch meta and the partials stay in coherent host
+// memory that the kernels read and write directly.  Anything the batch cannot express —
 // vector mask tables, a chunk larger than the ring, a short read, a zlib
 // failure — is handed back to the caller (PYAS_ENOTSUP / PYAS_EIO / info[])
 // so that the per-call path raises the reference's exact exception.
@@ -92,6 +102,8 @@ struct Group {
     std::vector<Req *> reqs;
 };
 
+struct GMeta { int64_t off, sel_off, pool_off, n, pool_len, out_base, dec_base, inf_base; bool any_sel; };
+
 template <typename T>
 struct DevBuf {
     T *p = nullptr;
@@ -108,22 +120,49 @@ struct DevBuf {
     }
 };
 
+// Pinned host memory; `coherent` = uncached fine-grained memory the kernels
+// read and write directly over PCIe (the zero-copy batch meta and partials).
 template <typename T>
 struct HostBuf {
     T *p = nullptr;
     int64_t n = 0;
+    bool coherent = false;
     hipError_t ensure(int64_t want) {
         if (want <= n) return hipSuccess;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         n = 0;
         int64_t m = want < 1024 ? 1024 : want + want / 2;
-        hipError_t e = hipHostMalloc((void **)&p, (size_t)m * sizeof(T), hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void **)&p, (size_t)m * sizeof(T),
+                                     coherent ? hipHostMallocCoherent : hipHostMallocDefault);
         if (e == hipSuccess) n = m;
         return e;
     }
 };
 
+}  // namespace
+
+namespace {
+// Scratch of one in-flight batch (the dispatcher fills it, the completer
+// drains it); reused once the batch has completed.
+struct Slot {
+    HostBuf<uint8_t> hmeta;
+    DevBuf<uint8_t> dmeta;
+    DevBuf<uint8_t> ddecode;
+    DevBuf<pyas_partial> dout;
+    HostBuf<pyas_partial> hout;
+    HostBuf<int64_t> hinf;      // inflate out_sizes + status, copied back
+    hipStream_t st = nullptr;   // this slot's kernels: batches in flight run side by side
+    hipEvent_t ev = nullptr;
+    hipEvent_t ev_copy = nullptr;   // the batch's H2D copies are done (copy stream)
+    bool ev_ok = false;         // the event was recorded behind the batch
+    std::vector<Req *> batch;
+    std::vector<Group> groups;
+    std::vector<GMeta> gm;
+    int64_t n_inf = 0;
+    int64_t inf_off = 0;        // inflate out_sizes + status: offset in the meta block
+    int64_t t_launched = 0;     // launch_batch returned
+};
 }  // namespace
 
 struct pyas_coalescer {
@@ -137,24 +176,26 @@ struct pyas_coalescer {
     std::deque<Req *> fifo;     // reservation order == ring order
     std::mutex mu;
     std::condition_variable cv_disp, cv_space;
-    std::thread disp;
+    std::thread disp, comp;
     bool stop = false;
-    hipStream_t st = nullptr;
-    hipEvent_t done_ev = nullptr;
+    bool disp_done = false;
+    hipStream_t cst = nullptr;   // H2D chunk copies (callers' in caller-copy mode; the
+                                 // dispatcher's unless PYAS_COALESCE_COPYSTREAM=0)
+    bool copy_stream = true;
+    bool zero_copy = true;       // meta read / partials written in coherent host memory (PYAS_COALESCE_ZEROCOPY)
+    int32_t depth = 4;           // batches in flight (PYAS_COALESCE_DEPTH)
+    std::vector<Slot *> slots;
+    std::deque<Slot *> free_slots, inflight;
+    int64_t n_sub = 0;           // fifo[0, n_sub) are submitted, in flight
+    std::condition_variable cv_comp, cv_slot;
     // Measured on the box (tools/bench_dropin.py): with 30 reader threads on a
     // 16-CPU host share, the dispatcher copying the batch's prefix and
     // sleeping on its completion event leaves the most CPU to the readers.
     bool caller_copy = false;   // PYAS_COALESCE_COPY=caller: each caller copies its own chunk
     bool blocking_sync = true;  // PYAS_COALESCE_SYNC=spin: the dispatcher spins on the batch
-    // dispatcher-only scratch
-    HostBuf<uint8_t> hmeta;
-    DevBuf<uint8_t> dmeta;
-    DevBuf<uint8_t> ddecode;
-    DevBuf<pyas_partial> dout;
-    HostBuf<pyas_partial> hout;
-    HostBuf<int64_t> hinf;      // inflate out_sizes + status, copied back
     int64_t n_batches = 0, n_chunks = 0, max_seen = 0;
-    int64_t busy_ns = 0, read_ns = 0, wait_ns = 0;   // dispatcher busy; callers reading; callers waiting
+    int64_t busy_ns = 0, read_ns = 0, wait_ns = 0;   // dispatcher launching; callers reading; callers waiting
+    int64_t gpu_ns = 0, t_last_done = 0;   // completion-to-completion time of back-to-back batches
 };
 
 namespace {
@@ -217,10 +258,15 @@ bool sel_ok(const pyas_chunk_desc &d, const int32_t *sel, const int32_t *pool, i
     return true;
 }
 
-// Run one batch (no lock held).  Fills each request's rc/out/info.
-void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
+// Enqueue one batch on its slot's stream (no lock held) and record its event; requests
+// that cannot run get their rc here.  The completer finishes the batch.
+void launch_batch(pyas_coalescer *c, Slot *sl) {
+    std::vector<Req *> &batch = sl->batch;
+    std::vector<Group> &groups = sl->groups;
+    groups.clear();
+    sl->ev_ok = false;
+    sl->n_inf = 0;
     // groups of identical keys, in first-seen order
-    std::vector<Group> groups;
     for (Req *r : batch) {
         if (r->state == SKIP) continue;
         Group *g = nullptr;
@@ -243,8 +289,8 @@ void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
     // host meta block: per group [offsets n][out_offsets n][src_off n][src_size n]
     // [dst_off n][dst_cap n] (int64) [sel n*24][pool] (int32); partial bases
     int64_t meta_bytes = 0, total_out = 0, decode_bytes = 0, n_inf = 0;
-    struct GMeta { int64_t off, sel_off, pool_off, n, pool_len, out_base, dec_base, inf_base; bool any_sel; };
-    std::vector<GMeta> gm(groups.size());
+    std::vector<GMeta> &gm = sl->gm;
+    gm.assign(groups.size(), GMeta{});
     for (size_t gi = 0; gi < groups.size(); ++gi) {
         Group &g = groups[gi];
         GMeta &m = gm[gi];
@@ -267,22 +313,29 @@ void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
             n_inf += m.n;
         }
     }
-    if ((e = c->hmeta.ensure(meta_bytes)) != hipSuccess || (e = c->dmeta.ensure(meta_bytes)) != hipSuccess ||
-        (e = c->dout.ensure(total_out > 0 ? total_out : 1)) != hipSuccess ||
-        (e = c->hout.ensure(total_out > 0 ? total_out : 1)) != hipSuccess ||
-        (e = c->hinf.ensure(2 * (n_inf > 0 ? n_inf : 1))) != hipSuccess ||
-        (decode_bytes > 0 && (e = c->ddecode.ensure(decode_bytes)) != hipSuccess)) {
+    sl->n_inf = n_inf;
+    if ((e = sl->hmeta.ensure(meta_bytes)) != hipSuccess || (e = sl->dmeta.ensure(meta_bytes)) != hipSuccess ||
+        (e = sl->dout.ensure(total_out > 0 ? total_out : 1)) != hipSuccess ||
+        (e = sl->hout.ensure(total_out > 0 ? total_out : 1)) != hipSuccess ||
+        (e = sl->hinf.ensure(2 * (n_inf > 0 ? n_inf : 1))) != hipSuccess ||
+        (decode_bytes > 0 && (e = sl->ddecode.ensure(decode_bytes)) != hipSuccess)) {
         fail_all(e == hipErrorOutOfMemory ? PYAS_ENOMEM : PYAS_EDEVICE, hipGetErrorString(e));
         return;
     }
     // inflate out_sizes + status: a device-only region after the meta block
     const int64_t inf_dev_off = align_up(meta_bytes, 16);
-    if (n_inf > 0 && (e = c->dmeta.ensure(inf_dev_off + 2 * n_inf * 8)) != hipSuccess) {
+    sl->inf_off = inf_dev_off;
+    if (n_inf > 0 && (e = sl->dmeta.ensure(inf_dev_off + 2 * n_inf * 8)) != hipSuccess) {
         fail_all(PYAS_EDEVICE, hipGetErrorString(e));
         return;
     }
-    uint8_t *hm = c->hmeta.p;
-    uint8_t *dm = c->dmeta.p;
+    if (n_inf > 0 && c->zero_copy && (e = sl->hmeta.ensure(inf_dev_off + 2 * n_inf * 8)) != hipSuccess) {
+        fail_all(PYAS_EDEVICE, hipGetErrorString(e));
+        return;
+    }
+    uint8_t *hm = sl->hmeta.p;
+    uint8_t *dm = c->zero_copy ? sl->hmeta.p : sl->dmeta.p;   // the kernels read the meta from here
+    pyas_partial *dout = c->zero_copy ? sl->hout.p : sl->dout.p;
     int64_t dec_cursor = 0;
     for (size_t gi = 0; gi < groups.size(); ++gi) {
         Group &g = groups[gi];
@@ -330,9 +383,10 @@ void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
     // 1. the chunk bytes: copy the prefix here, one copy per contiguous run
     //    (two when the ring wrapped; gaps are alignment padding or skipped
     //    reads of the same prefix) -- or, with PYAS_COALESCE_COPY=caller,
-    //    each caller already enqueued its own H2D copy on c->st right after
+    //    each caller already enqueued its own H2D copy on sl->st right after
     //    its read, before it marked the request FILLED, so the launches
     //    below are ordered after them
+    hipStream_t cs = c->copy_stream ? c->cst : sl->st;   // where the chunk bytes are copied
     if (!c->caller_copy) {
         int64_t run_a = -1, run_b = -1;
         for (Req *r : batch) {
@@ -343,7 +397,7 @@ void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
             }
             if (run_a >= 0 &&
                 (e = hipMemcpyAsync(c->dring + run_a, c->hring + run_a, (size_t)(run_b - run_a),
-                                    hipMemcpyHostToDevice, c->st)) != hipSuccess) {
+                                    hipMemcpyHostToDevice, cs)) != hipSuccess) {
                 fail_all(PYAS_EDEVICE, hipGetErrorString(e));
                 return;
             }
@@ -352,13 +406,22 @@ void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
         }
         if (run_a >= 0 &&
             (e = hipMemcpyAsync(c->dring + run_a, c->hring + run_a, (size_t)(run_b - run_a),
-                                hipMemcpyHostToDevice, c->st)) != hipSuccess) {
+                                hipMemcpyHostToDevice, cs)) != hipSuccess) {
             fail_all(PYAS_EDEVICE, hipGetErrorString(e));
             return;
         }
     }
-    // 2. meta H2D
-    if ((e = hipMemcpyAsync(dm, hm, (size_t)meta_bytes, hipMemcpyHostToDevice, c->st)) != hipSuccess) {
+    // the kernels wait for the copy stream's copies (the callers' too, in
+    // caller-copy mode: they were enqueued before the requests were FILLED)
+    if ((c->copy_stream || c->caller_copy) &&
+        ((e = hipEventRecord(sl->ev_copy, c->cst)) != hipSuccess ||
+         (e = hipStreamWaitEvent(sl->st, sl->ev_copy, 0)) != hipSuccess)) {
+        fail_all(PYAS_EDEVICE, hipGetErrorString(e));
+        return;
+    }
+    // 2. meta H2D (zero-copy: the kernels read it from coherent host memory)
+    if (!c->zero_copy &&
+        (e = hipMemcpyAsync(dm, hm, (size_t)meta_bytes, hipMemcpyHostToDevice, sl->st)) != hipSuccess) {
         fail_all(PYAS_EDEVICE, hipGetErrorString(e));
         return;
     }
@@ -373,8 +436,8 @@ void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
                       *d_dcap = d_doff + m.n;
         int rc = PYAS_OK;
         if (g.key.desc.zlib) {
-            rc = pyas_inflate(c->ctx, c->dring, d_soff, d_ssz, m.n, c->ddecode.p, d_doff, d_dcap,
-                              dinf + m.inf_base, (int32_t *)(dinf + n_inf) + m.inf_base, c->st);
+            rc = pyas_inflate(c->ctx, c->dring, d_soff, d_ssz, m.n, sl->ddecode.p, d_doff, d_dcap,
+                              dinf + m.inf_base, (int32_t *)(dinf + n_inf) + m.inf_base, sl->st);
         }
         pyas_batch b;
         std::memset(&b, 0, sizeof(b));
@@ -384,50 +447,72 @@ void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
         b.ndim = g.key.desc.ndim;
         for (int k = 0; k < PYAS_MAX_DIMS; ++k) b.chunk_shape[k] = g.key.desc.chunk_shape[k];
         b.n_chunks = m.n;
-        b.data = g.key.desc.zlib ? (const void *)c->ddecode.p : (const void *)c->dring;
+        b.data = g.key.desc.zlib ? (const void *)sl->ddecode.p : (const void *)c->dring;
         b.offsets = d_offs;
         b.sel = m.any_sel ? (const int32_t *)(dm + m.sel_off) : nullptr;
         b.index_pool = (const int32_t *)(dm + m.pool_off);
         const uint32_t full = (g.key.desc.ndim >= 32) ? 0xffffffffu : ((1u << g.key.desc.ndim) - 1u);
         if (rc == PYAS_OK) {
             if ((g.key.desc.axes_mask & full) == full)
-                rc = pyas_reduce_chunks(c->ctx, &b, &g.key.mask, c->dout.p + m.out_base, nullptr, 0u, c->st);
+                rc = pyas_reduce_chunks(c->ctx, &b, &g.key.mask, dout + m.out_base, nullptr, 0u, sl->st);
             else
-                rc = pyas_reduce_axes(c->ctx, &b, &g.key.mask, g.key.desc.axes_mask, d_oofs, c->dout.p, c->st);
+                rc = pyas_reduce_axes(c->ctx, &b, &g.key.mask, g.key.desc.axes_mask, d_oofs, dout, sl->st);
         }
         if (rc != PYAS_OK) {
             const std::string msg = pyas_last_error();
             for (Req *r : g.reqs) { r->rc = rc; r->err = msg; }
         }
     }
-    // 4. partials (and inflate results) back, one sync
-    if (total_out > 0 &&
-        (e = hipMemcpyAsync(c->hout.p, c->dout.p, (size_t)total_out * sizeof(pyas_partial),
-                            hipMemcpyDeviceToHost, c->st)) != hipSuccess) {
+    // 4. partials (and inflate results) back; the completer waits on the event
+    if (!c->zero_copy && total_out > 0 &&
+        (e = hipMemcpyAsync(sl->hout.p, sl->dout.p, (size_t)total_out * sizeof(pyas_partial),
+                            hipMemcpyDeviceToHost, sl->st)) != hipSuccess) {
         fail_all(PYAS_EDEVICE, hipGetErrorString(e));
         return;
     }
-    if (n_inf > 0 &&
-        (e = hipMemcpyAsync(c->hinf.p, dinf, (size_t)(2 * n_inf) * 8, hipMemcpyDeviceToHost, c->st)) !=
+    if (!c->zero_copy && n_inf > 0 &&
+        (e = hipMemcpyAsync(sl->hinf.p, dinf, (size_t)(2 * n_inf) * 8, hipMemcpyDeviceToHost, sl->st)) !=
             hipSuccess) {
         fail_all(PYAS_EDEVICE, hipGetErrorString(e));
         return;
     }
-    // wait for this batch only (callers keep enqueueing copies behind it)
-    if ((e = hipEventRecord(c->done_ev, c->st)) != hipSuccess ||
-        (e = hipEventSynchronize(c->done_ev)) != hipSuccess) {
+    if ((e = hipEventRecord(sl->ev, sl->st)) != hipSuccess) {
         fail_all(PYAS_EDEVICE, hipGetErrorString(e));
         return;
     }
-    for (size_t gi = 0; gi < groups.size(); ++gi) {
-        Group &g = groups[gi];
-        GMeta &m = gm[gi];
+    sl->ev_ok = true;
+}
+
+// After the batch's event (no lock held): the partials and inflate results
+// to each caller's memory.
+void finish_batch(pyas_coalescer *c, Slot *sl) {
+    std::vector<Req *> &batch = sl->batch;
+    if (sl->ev_ok) {
+        const hipError_t e = hipEventSynchronize(sl->ev);
+        if (e != hipSuccess) {
+            for (Req *r : batch)
+                if (r->state != SKIP) { r->rc = PYAS_EDEVICE; r->err = hipGetErrorString(e); }
+            return;
+        }
+    } else {
+        // launch_batch failed part-way (every live request carries its rc):
+        // drain what it did enqueue before the slot is reused
+        (void)hipStreamSynchronize(sl->st);
+        return;
+    }
+    const int64_t n_inf = sl->n_inf;
+    // inflate out_sizes + status: copied back, or written in place (zero-copy)
+    const int64_t *inf = sl->hinf.p;
+    if (c->zero_copy && n_inf > 0) inf = (const int64_t *)(sl->hmeta.p + sl->inf_off);
+    for (size_t gi = 0; gi < sl->groups.size(); ++gi) {
+        Group &g = sl->groups[gi];
+        GMeta &m = sl->gm[gi];
         int64_t ob = m.out_base;
         for (int64_t i = 0; i < m.n; ++i) {
             Req *r = g.reqs[i];
             if (g.key.desc.zlib) {
-                const int64_t osz = c->hinf.p[m.inf_base + i];
-                const int32_t stt = ((int32_t *)(c->hinf.p + n_inf))[m.inf_base + i];
+                const int64_t osz = inf[m.inf_base + i];
+                const int32_t stt = ((const int32_t *)(inf + n_inf))[m.inf_base + i];
                 r->info[1] = stt;
                 r->info[2] = osz;
                 if (r->rc == PYAS_OK && (stt != PYAS_INFLATE_OK || osz != r->chunk_bytes)) {
@@ -436,7 +521,7 @@ void run_batch(pyas_coalescer *c, std::vector<Req *> &batch) {
                 }
             }
             if (r->rc == PYAS_OK)
-                std::memcpy(r->out, c->hout.p + ob, (size_t)r->n_out * sizeof(pyas_partial));
+                std::memcpy(r->out, sl->hout.p + ob, (size_t)r->n_out * sizeof(pyas_partial));   // both modes
             ob += r->n_out;
         }
     }
@@ -446,37 +531,71 @@ void dispatcher(pyas_coalescer *c) {
     (void)hipSetDevice(c->device);
     std::unique_lock<std::mutex> lk(c->mu);
     for (;;) {
-        c->cv_disp.wait(lk, [&] {
-            return (c->stop && c->fifo.empty()) ||
-                   (!c->fifo.empty() && c->fifo.front()->state != RESERVED);
-        });
-        if (c->fifo.empty()) break;   // stopping, nothing queued
-        std::vector<Req *> batch;
-        for (Req *r : c->fifo) {
-            if ((int32_t)batch.size() >= c->max_batch) break;
+        auto ready = [&] {
+            return (int64_t)c->fifo.size() > c->n_sub && c->fifo[c->n_sub]->state != RESERVED;
+        };
+        c->cv_disp.wait(lk, [&] { return ready() || (c->stop && (int64_t)c->fifo.size() == c->n_sub); });
+        if (!ready()) break;   // stopping, nothing unsubmitted
+        c->cv_slot.wait(lk, [&] { return !c->free_slots.empty(); });
+        Slot *sl = c->free_slots.front();
+        c->free_slots.pop_front();
+        sl->batch.clear();
+        for (int64_t i = c->n_sub; i < (int64_t)c->fifo.size(); ++i) {
+            Req *r = c->fifo[i];
+            if ((int32_t)sl->batch.size() >= c->max_batch) break;
             if (r->state != FILLED && r->state != SKIP) break;
-            batch.push_back(r);
+            sl->batch.push_back(r);
         }
-        for (Req *r : batch)
+        for (Req *r : sl->batch)
             if (r->state == FILLED) r->state = SUBMITTED;
+        c->n_sub += (int64_t)sl->batch.size();
         lk.unlock();
         const int64_t t0 = now_ns();
-        run_batch(c, batch);
+        launch_batch(c, sl);
         const int64_t t1 = now_ns();
+        sl->t_launched = t1;
         lk.lock();
         c->busy_ns += t1 - t0;
+        c->inflight.push_back(sl);
+        c->cv_comp.notify_one();
+    }
+    c->disp_done = true;
+    c->cv_comp.notify_one();
+}
+
+void completer(pyas_coalescer *c) {
+    (void)hipSetDevice(c->device);
+    std::unique_lock<std::mutex> lk(c->mu);
+    for (;;) {
+        c->cv_comp.wait(lk, [&] { return !c->inflight.empty() || c->disp_done; });
+        if (c->inflight.empty()) break;   // the dispatcher has stopped and everything completed
+        Slot *sl = c->inflight.front();
+        c->inflight.pop_front();
+        lk.unlock();
+        finish_batch(c, sl);
+        const int64_t t_done = now_ns();
+        lk.lock();
+        // time this batch held the device queue: from its launch (or the
+        // previous batch's completion, if later) to its completion
+        c->gpu_ns += t_done - (sl->t_launched > c->t_last_done ? sl->t_launched : c->t_last_done);
+        c->t_last_done = t_done;
         int64_t nch = 0;
-        for (Req *r : batch) {
+        for (Req *r : sl->batch) {
             if (r->state == SUBMITTED) ++nch;
             r->state = DONE;
         }
-        for (size_t i = 0; i < batch.size(); ++i) c->fifo.pop_front();
+        // batches complete in submission order == the fifo's order
+        for (size_t i = 0; i < sl->batch.size(); ++i) c->fifo.pop_front();
+        c->n_sub -= (int64_t)sl->batch.size();
         c->n_batches += 1;
         c->n_chunks += nch;
         if (nch > c->max_seen) c->max_seen = nch;
         // wake exactly this batch's callers (one condition variable each:
         // a shared notify_all would wake every waiting caller per batch)
-        for (Req *r : batch) r->cv.notify_one();
+        for (Req *r : sl->batch) r->cv.notify_one();
+        sl->batch.clear();
+        c->free_slots.push_back(sl);
+        c->cv_slot.notify_one();
         c->cv_space.notify_all();
     }
 }
@@ -496,19 +615,37 @@ int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch, 
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->hring, (size_t)c->ring_bytes, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc((void **)&c->dring, (size_t)c->ring_bytes);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->cst, hipStreamNonBlocking);
     if (const char *v = getenv("PYAS_COALESCE_COPY")) c->caller_copy = std::strcmp(v, "caller") == 0;
     if (const char *v = getenv("PYAS_COALESCE_SYNC")) c->blocking_sync = std::strcmp(v, "spin") != 0;
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming |
-                                                     (c->blocking_sync ? hipEventBlockingSync : 0u));
+    if (const char *v = getenv("PYAS_COALESCE_DEPTH")) c->depth = atoi(v) > 0 ? atoi(v) : 1;
+    if (const char *v = getenv("PYAS_COALESCE_ZEROCOPY")) c->zero_copy = std::strcmp(v, "0") != 0;
+    if (const char *v = getenv("PYAS_COALESCE_COPYSTREAM")) c->copy_stream = std::strcmp(v, "0") != 0;
+    for (int i = 0; e == hipSuccess && i < c->depth; ++i) {
+        Slot *sl = new Slot();
+        sl->hmeta.coherent = sl->hout.coherent = c->zero_copy;
+        e = hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming |
+                                                 (c->blocking_sync ? hipEventBlockingSync : 0u));
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&sl->ev_copy, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking);
+        c->slots.push_back(sl);
+        c->free_slots.push_back(sl);
+    }
     if (e != hipSuccess) {
+        for (Slot *sl : c->slots) {
+            if (sl->ev) (void)hipEventDestroy(sl->ev);
+            if (sl->ev_copy) (void)hipEventDestroy(sl->ev_copy);
+            if (sl->st) (void)hipStreamDestroy(sl->st);
+            delete sl;
+        }
+        if (c->cst) (void)hipStreamDestroy(c->cst);
         if (c->hring) (void)hipHostFree(c->hring);
         if (c->dring) (void)hipFree(c->dring);
         delete c;
         return pyas::set_error(e == hipErrorOutOfMemory ? PYAS_ENOMEM : PYAS_EDEVICE, hipGetErrorString(e));
     }
     c->disp = std::thread(dispatcher, c);
+    c->comp = std::thread(completer, c);
     *out = c;
     return PYAS_OK;
 }
@@ -522,18 +659,25 @@ int pyas_coalescer_destroy(pyas_coalescer *c) {
     c->cv_disp.notify_all();
     c->cv_space.notify_all();
     if (c->disp.joinable()) c->disp.join();
+    if (c->comp.joinable()) c->comp.join();
     (void)hipSetDevice(c->device);
-    if (c->st) (void)hipStreamSynchronize(c->st);
-    if (c->st) (void)hipStreamDestroy(c->st);
-    if (c->done_ev) (void)hipEventDestroy(c->done_ev);
+    if (c->cst) (void)hipStreamSynchronize(c->cst);
+    if (c->cst) (void)hipStreamDestroy(c->cst);
+    for (Slot *sl : c->slots) {
+        if (sl->st) (void)hipStreamSynchronize(sl->st);
+        if (sl->st) (void)hipStreamDestroy(sl->st);
+        if (sl->ev) (void)hipEventDestroy(sl->ev);
+        if (sl->ev_copy) (void)hipEventDestroy(sl->ev_copy);
+        if (sl->hmeta.p) (void)hipHostFree(sl->hmeta.p);
+        if (sl->hout.p) (void)hipHostFree(sl->hout.p);
+        if (sl->hinf.p) (void)hipHostFree(sl->hinf.p);
+        if (sl->dmeta.p) (void)hipFree(sl->dmeta.p);
+        if (sl->ddecode.p) (void)hipFree(sl->ddecode.p);
+        if (sl->dout.p) (void)hipFree(sl->dout.p);
+        delete sl;
+    }
     (void)hipHostFree(c->hring);
     (void)hipFree(c->dring);
-    if (c->hmeta.p) (void)hipHostFree(c->hmeta.p);
-    if (c->hout.p) (void)hipHostFree(c->hout.p);
-    if (c->hinf.p) (void)hipHostFree(c->hinf.p);
-    if (c->dmeta.p) (void)hipFree(c->dmeta.p);
-    if (c->ddecode.p) (void)hipFree(c->ddecode.p);
-    if (c->dout.p) (void)hipFree(c->dout.p);
     delete c;
     return PYAS_OK;
 }
@@ -547,6 +691,7 @@ int pyas_coalescer_stats(pyas_coalescer *c, int64_t *stats) {
     stats[3] = c->busy_ns;
     stats[4] = c->read_ns;
     stats[5] = c->wait_ns;
+    stats[6] = c->gpu_ns;
     return PYAS_OK;
 }
 
@@ -630,10 +775,10 @@ int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, i
     hipError_t ce = hipSuccess;
     if (c->caller_copy && got == size && !read_errno && size > 0) {
         // this chunk's H2D copy, issued by the caller so that copies overlap
-        // other callers' reads; ordered before the batch's launches on c->st
+        // other callers' reads; ordered before the batch's launches by its ev_copy
         ce = hipSetDevice(c->device);
         if (ce == hipSuccess)
-            ce = hipMemcpyAsync(c->dring + off, c->hring + off, (size_t)size, hipMemcpyHostToDevice, c->st);
+            ce = hipMemcpyAsync(c->dring + off, c->hring + off, (size_t)size, hipMemcpyHostToDevice, c->cst);
     }
 
     const int64_t t_wait = now_ns();

@@ -38,9 +38,13 @@ PyObject *g_str_mask = nullptr, *g_str_shared = nullptr;
 
 constexpr int kMaxEntries = 4096;
 
-// key of one call shape (everything but rfile/offset/size)
+// key of one call shape (everything but rfile/offset/size); the chunk shape
+// by value when it is a tuple/list of ints (callers may build it per call),
+// otherwise by identity like the other objects
 struct Key {
     PyObject *missing, *compression, *filters, *shape, *method;
+    int nshape;                              // -1: shape keyed by identity
+    long shapev[PYAS_MAX_DIMS];
     uint64_t dtype;                          // np.dtype by value, anything else by identity
     int order;                               // 'C' / 'F'
     int nsel;                                // slices in the selection
@@ -86,6 +90,23 @@ size_t g_n = 0;
 uint64_t mix(uint64_t h, uint64_t v) {
     h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
     return h;
+}
+
+// shape -> k.shapev by value when it is a short tuple/list of exact ints
+void parse_shape(PyObject *shape, Key &k) {
+    k.shape = shape;
+    k.nshape = -1;
+    if (!PyTuple_Check(shape) && !PyList_Check(shape)) return;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(shape);
+    if (n < 1 || n > PYAS_MAX_DIMS) return;
+    PyObject *const *items = PySequence_Fast_ITEMS(shape);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        if (!PyLong_CheckExact(items[i])) return;
+        k.shapev[i] = PyLong_AsLong(items[i]);
+        if (k.shapev[i] == -1 && PyErr_Occurred()) { PyErr_Clear(); return; }
+    }
+    k.shape = nullptr;
+    k.nshape = (int)n;
 }
 
 // Parse the non-identity parts of the key.  Returns false (no exception set)
@@ -150,6 +171,8 @@ uint64_t hash_key(const Key &k) {
     h = mix(h, (uint64_t)(uintptr_t)k.compression);
     h = mix(h, (uint64_t)(uintptr_t)k.filters);
     h = mix(h, (uint64_t)(uintptr_t)k.shape);
+    h = mix(h, (uint64_t)(int64_t)k.nshape);
+    for (int i = 0; i < k.nshape; ++i) h = mix(h, (uint64_t)k.shapev[i]);
     h = mix(h, (uint64_t)(uintptr_t)k.method);
     h = mix(h, (uint64_t)k.order);
     h = mix(h, (uint64_t)k.nsel);
@@ -162,8 +185,10 @@ uint64_t hash_key(const Key &k) {
 bool same_key(const Key &a, const Key &b) {
     if (a.missing != b.missing || a.dtype != b.dtype || a.compression != b.compression ||
         a.filters != b.filters || a.shape != b.shape || a.method != b.method || a.order != b.order ||
-        a.nsel != b.nsel || a.axis_kind != b.axis_kind || a.naxis != b.naxis)
+        a.nsel != b.nsel || a.axis_kind != b.axis_kind || a.naxis != b.naxis || a.nshape != b.nshape)
         return false;
+    for (int i = 0; i < a.nshape; ++i)
+        if (a.shapev[i] != b.shapev[i]) return false;
     for (int i = 0; i < 3 * a.nsel; ++i)
         if (a.sel[i] != b.sel[i]) return false;
     for (int i = 0; i < a.naxis; ++i)
@@ -263,7 +288,7 @@ PyObject *py_reduce(PyObject *, PyObject *const *a, Py_ssize_t n) {
     k.filters = a[4];
     k.missing = a[5];
     k.dtype = dtype_key(a[6]);
-    k.shape = a[7];
+    parse_shape(a[7], k);
     k.method = a[11];
     if (!parse_key(a[8], a[9], a[10], k)) Py_RETURN_NONE;
     auto it = g_cache.find(hash_key(k));
@@ -334,7 +359,7 @@ PyObject *py_register(PyObject *, PyObject *args) {
     e->key.dtype = dtype_key(dtype);
     e->key.compression = compression;
     e->key.filters = filters;
-    e->key.shape = shape;
+    parse_shape(shape, e->key);
     e->key.method = method;
     e->dtype_ref = nullptr;
     if (!parse_key(order, sel, axis, e->key)) {
@@ -353,7 +378,7 @@ PyObject *py_register(PyObject *, PyObject *args) {
     e->dtype_ref = dtype;
     Py_INCREF(compression);
     Py_INCREF(filters);
-    Py_INCREF(shape);
+    Py_XINCREF(e->key.shape);   // NULL when keyed by value
     Py_INCREF(method);
     auto &bucket = g_cache[hash_key(e->key)];
     for (size_t i = 0; i < bucket.size(); ++i) {

@@ -115,10 +115,15 @@ def test_misses_return_none():
     NEXT["p"] = p
     args = ["/tmp/x", 0, 256, None, None, missing, dt, shape, "C", sel, (0, 1, 2), np.ma.sum]
     assert _fastpath.reduce(*args) is not None
-    # equal-valued dtype objects share the plan (np.dtype keyed by value)
+    # equal-valued dtype objects share the plan (np.dtype keyed by value), and
+    # so do equal chunk shapes built per call (a tuple or list of ints)
     assert _fastpath.reduce(*(args[:6] + [np.dtype("float32")] + args[7:])) is not None
+    assert _fastpath.reduce(*(args[:7] + [tuple([4, 4, 4])] + args[8:])) is not None
+    assert _fastpath.reduce(*(args[:7] + [[4, 4, 4]] + args[8:])) is not None
     for i, other in ((5, (np.float32(1), None, None, None)),     # another missing object
-                     (7, tuple([4, 4, 4])),                      # another shape object
+                     (7, (4, 4, 8)),                             # another chunk shape
+                     (7, (4, 4)),
+                     (7, (np.int64(4), 4, 4)),                   # not plain ints: by identity
                      (9, (slice(0, 4), slice(0, 4), slice(0, 3))),
                      (9, (0, slice(0, 4), slice(0, 4))),         # integer index: not cached
                      (10, [0, 1, 2]),                            # list axis: not cached
