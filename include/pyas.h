@@ -403,10 +403,11 @@ typedef struct pyas_coalescer pyas_coalescer;
 int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch,
                           pyas_coalescer **out);
 int pyas_coalescer_destroy(pyas_coalescer *c);
-/* stats (int64[7]): batches dispatched, chunks reduced, largest batch,
+/* stats (int64[8]): batches dispatched, chunks reduced, largest batch,
  * dispatcher busy ns (launching), callers' file-read ns, callers'
  * wait-for-batch ns, device-queue ns (per batch: from its launch, or the
- * previous batch's completion if later, to its completion) */
+ * previous batch's completion if later, to its completion), requests
+ * handed back to the per-call path */
 int pyas_coalescer_stats(pyas_coalescer *c, int64_t *stats);
 /* Reduce file `path` bytes [offset, offset + size) as one chunk described by
  * desc/mask (mask without vector tables), selection `sel` (host

@@ -183,7 +183,12 @@ struct pyas_coalescer {
                                  // dispatcher's unless PYAS_COALESCE_COPYSTREAM=0)
     bool copy_stream = true;
     bool zero_copy = true;       // meta read / partials written in coherent host memory (PYAS_COALESCE_ZEROCOPY)
-    int32_t depth = 4;           // batches in flight (PYAS_COALESCE_DEPTH)
+    // batches in flight (PYAS_COALESCE_DEPTH).  Measured on the box
+    // (profiles/r02/dropin_*knobs.jsonl): uncompressed 21.5k chunks/s at 1
+    // and 2, 21.4k at 4; zlib 1,063 chunks/s at 1, 760 at 4, 604 at 8 (more
+    // batches in flight are smaller, and each zlib batch is bounded by one
+    // stream's inflate latency), so one batch runs while the next gathers.
+    int32_t depth = 1;
     std::vector<Slot *> slots;
     std::deque<Slot *> free_slots, inflight;
     int64_t n_sub = 0;           // fifo[0, n_sub) are submitted, in flight
@@ -196,6 +201,7 @@ struct pyas_coalescer {
     int64_t n_batches = 0, n_chunks = 0, max_seen = 0;
     int64_t busy_ns = 0, read_ns = 0, wait_ns = 0;   // dispatcher launching; callers reading; callers waiting
     int64_t gpu_ns = 0, t_last_done = 0;   // completion-to-completion time of back-to-back batches
+    int64_t n_back = 0;          // requests handed back to the per-call path (rc != OK)
 };
 
 namespace {
@@ -582,6 +588,7 @@ void completer(pyas_coalescer *c) {
         int64_t nch = 0;
         for (Req *r : sl->batch) {
             if (r->state == SUBMITTED) ++nch;
+            if (r->rc != PYAS_OK) ++c->n_back;
             r->state = DONE;
         }
         // batches complete in submission order == the fifo's order
@@ -692,6 +699,7 @@ int pyas_coalescer_stats(pyas_coalescer *c, int64_t *stats) {
     stats[4] = c->read_ns;
     stats[5] = c->wait_ns;
     stats[6] = c->gpu_ns;
+    stats[7] = c->n_back;
     return PYAS_OK;
 }
 

@@ -202,11 +202,12 @@ class Context:
         return c
 
     def coalescer_stats(self) -> dict:
-        s = (ctypes.c_int64 * 7)()
+        s = (ctypes.c_int64 * 8)()
         if self._coalescer is not None:
             _lib.check(self.lib.pyas_coalescer_stats(self._coalescer, s), "pyas_coalescer_stats")
         return {"batches": s[0], "chunks": s[1], "largest": s[2], "busy_s": s[3] * 1e-9,
-                "read_s": s[4] * 1e-9, "wait_s": s[5] * 1e-9, "gpu_s": s[6] * 1e-9}
+                "read_s": s[4] * 1e-9, "wait_s": s[5] * 1e-9, "gpu_s": s[6] * 1e-9,
+                "handed_back": s[7]}
 
     def set_tile_bytes(self, nbytes: int) -> None:
         _lib.check(self.lib.pyas_ctx_set_tile_bytes(self.handle, int(nbytes)), "set_tile_bytes")
