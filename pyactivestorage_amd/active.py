@@ -55,6 +55,77 @@ _EMPTY, _LOADING, _LOADED = 0, 1, 2
 _AXES_FOLD = os.environ.get("PYAS_AXES_FOLD", "1") != "0"
 
 
+# Resident repeat queries: per-store cache of device plans, keyed by the
+# query (index of slices/Ellipsis, reduced axes, missing-data values)
+_PLAN_CACHE_CAP = 64
+_MISS = object()
+
+
+def _index_key(index):
+    """Hashable form of an index made only of slices and Ellipsis (the box
+    queries a plan can be replayed for); None otherwise."""
+    if not isinstance(index, tuple):
+        index = (index,)
+    out = []
+    for x in index:
+        if x is Ellipsis:
+            out.append(("e",))
+        elif isinstance(x, slice):
+            part = ["s"]
+            for v in (x.start, x.stop, x.step):
+                if v is None:
+                    part.append(None)
+                elif isinstance(v, (int, np.integer)) and not isinstance(v, (bool, np.bool_)):
+                    part.append(int(v))
+                else:
+                    return None
+            out.append(tuple(part))
+        else:
+            return None
+    return tuple(out)
+
+
+def _missing_key(missing):
+    key = []
+    for m in missing:
+        if m is None:
+            key.append(None)
+        else:
+            a = np.asarray(m)
+            key.append((a.dtype.str, a.shape, a.tobytes()))
+    return tuple(key)
+
+
+class _CachedQuery:
+    """A resident query's device plan, replayed by later identical queries:
+    no indexer, no chunk table, no uploads or allocations, only the
+    launches, the result copy and the formatting (``active.py:591-630``)."""
+
+    def __init__(self, plan, final_shape, grid=None):
+        self.plan = plan
+        self.final_shape = final_shape
+        self.grid = grid            # None: full reduction; else _grid_partials' record
+        self.fmt = {}               # format buffers by result dtype / components
+
+    def run(self, act):
+        ctx = self.plan.ctx
+        st = ctx.thread_stream()
+        shape = self.final_shape
+        if self.grid is None:
+            self.plan.launch(st, chunk_partials=False)
+            final = self.plan.read_total(st)
+            return act._format(final.reshape(shape), shape)
+        g = self.grid
+        if g["folded"]:
+            engine.reduce_axes_grid(ctx, self.plan.batch, self.plan.mask_up.struct, g["g"], g["fin"].ptr,
+                                    True, st)
+        else:
+            engine.reduce_axes(ctx, self.plan.batch, self.plan.mask_up.struct, g["axes_mask"], g["obuf"].ptr,
+                               g["parts"].ptr, st)
+            engine.combine_grid(ctx, act.ds.dtype, g["parts"].ptr, g["g"], g["fin"].ptr, True, st)
+        return act._format_device(ctx, st, g["fin"], g["n_final"], shape, bufs=self.fmt)
+
+
 def release_resident(variable) -> None:
     """Free the HBM copy that resident-mode ``Active`` queries keep for
     ``variable`` (e.g. after the file changed).  Queries already using the
@@ -209,6 +280,14 @@ class Active:
             self._axis = tuple(range(ds.ndim))
         elif isinstance(self._axis, int):
             self._axis = (self._axis,)
+        cache_key = None
+        if self.resident and self.group is None and self._method is not None:
+            ikey = _index_key(index)
+            if ikey is not None:
+                cache_key = (ikey, self._norm_axes(), _missing_key(self.missing))
+                hit = self._cached_query(cache_key)
+                if hit is not _MISS:
+                    return hit
         compressor, filters = (None, None) if not ds.filter_pipeline else \
             decode_filters(ds.filter_pipeline, ds.dtype.itemsize, ds.name)
         indexer = OrthogonalIndexer(index, ds.shape, ds.chunks)
@@ -220,14 +299,43 @@ class Active:
             if d.kind == "int":
                 raise IndexError("Can't do an active reduction when the index for "
                                  f"axis {i!r} drops the axis.")
+        return self._reduce(indexer, compressor, filters, self._norm_axes(), cache_key)
+
+    def _norm_axes(self):
+        """The reduced axes, sorted and non-negative (active.py:505-510)."""
+        ndim = self.ds.ndim
         axes = []
-        for i in self._axis:                                # active.py:505-510
-            if not -ds.ndim <= i < ds.ndim:
+        for i in self._axis:
+            if not -ndim <= i < ndim:
                 raise ValueError(f"Can't do an active reduction for an out-of-range axis: {i!r}")
-            axes.append(i % ds.ndim)
+            axes.append(i % ndim)
         if len(set(axes)) != len(axes):
             raise ValueError("duplicate value in 'axis'")
-        return self._reduce(indexer, compressor, filters, tuple(sorted(axes)))
+        return tuple(sorted(axes))
+
+    def _cached_query(self, key):
+        """Replay a cached plan of this resident variable (every chunk of the
+        query is still in its slot), or _MISS."""
+        store = getattr(self.ds, "_pyas_resident", None)
+        if store is None or store["device"] != self.device:
+            return _MISS
+        with _RESIDENT_LOCK:
+            entry = store.get("plans", {}).get(key)
+            if entry is None or store["released"]:
+                return _MISS
+            store["users"] += 1
+        self._held.stores.append(store)
+        return entry.run(self)
+
+    def _remember(self, key, entry):
+        store = getattr(self.ds, "_pyas_resident", None)
+        if key is None or store is None or entry.plan.batch.data != store["buf"].ptr:
+            return
+        with _RESIDENT_LOCK:
+            plans = store.setdefault("plans", {})
+            if len(plans) >= _PLAN_CACHE_CAP:
+                plans.pop(next(iter(plans)))
+            plans[key] = entry
 
     # -- host ingest -------------------------------------------------------
     def _ingest(self, coords, compressor, filters):
@@ -491,7 +599,7 @@ class Active:
         pool = np.concatenate(pool_parts) if pool_parts else np.zeros(1, dtype=np.int32)
         return dims, coords, table, pool
 
-    def _reduce(self, indexer, compressor, filters, axes):
+    def _reduce(self, indexer, compressor, filters, axes, cache_key=None):
         box = self._box_plan(indexer)
         if box is None:
             if self.group is not None:
@@ -518,14 +626,21 @@ class Active:
             plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused,
                                  sel_table=None if full else sub, index_pool=None if full else pool,
                                  missing=self.missing, round_to_var=True, stream=st)
+            cacheable = cache_key is not None and self.resident and self.group is None
             if len(axes) == ds.ndim:
                 plan.launch(st, chunk_partials=False)
                 final = plan.read_total(st)
+                if cacheable:
+                    self._remember(cache_key, _CachedQuery(plan, final_shape))
             else:
                 grid = self._grid_from_dims(dims, axes, final_shape)
                 if self.group is None:   # one process: format on the device
-                    return self._grid_partials(ctx, st, plan, grid, axes, final_shape, lo, hi,
-                                               formatted=True)
+                    rec = {} if cacheable else None
+                    out = self._grid_partials(ctx, st, plan, grid, axes, final_shape, lo, hi,
+                                              formatted=True, rec=rec)
+                    if cacheable:
+                        self._remember(cache_key, _CachedQuery(plan, final_shape, rec))
+                    return out
                 final = self._grid_partials(ctx, st, plan, grid, axes, final_shape, lo, hi)
         else:
             final = np.zeros(n_final, dtype=pdt)   # count 0: neutral in every combine
@@ -572,12 +687,13 @@ class Active:
         return self._grid_partials(ctx, st, plan, grid, axes, final_shape, 0, plan.n_chunks,
                                    formatted=True)
 
-    def _grid_partials(self, ctx, st, plan, grid, axes, final_shape, lo, hi, formatted=False):
+    def _grid_partials(self, ctx, st, plan, grid, axes, final_shape, lo, hi, formatted=False, rec=None):
         """Per-chunk partial arrays of chunks [lo, hi) of the box query
         (pyas_reduce_axes over ``plan``), then pyas_combine_grid into the
         final grid; chunks outside [lo, hi) read a zeroed (count 0, neutral)
         partial region.  ``formatted``: return the formatted result
-        (``_format_device``) instead of the host partials."""
+        (``_format_device``) instead of the host partials.  ``rec``: filled
+        with what a replay of this query needs (_CachedQuery)."""
         ds = self.ds
         dt = ds.dtype
         n_final = int(np.prod(final_shape))
@@ -621,6 +737,7 @@ class Active:
                 folded = True
             except NotImplementedError:
                 pass   # geometry without the dense column or LDS row layout: two steps
+        parts = None
         if not folded:
             n_parts = top - base
             parts = DeviceBuffer(ctx, max(n_parts + neutral, 1) * _lib.PARTIAL_NBYTES)
@@ -629,6 +746,9 @@ class Active:
                 ctx.h2d(parts.ptr + n_parts * _lib.PARTIAL_NBYTES, zeros, st)
             engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st)
             engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st)
+        if rec is not None:
+            rec.update(folded=folded, g=g, fin=fin, obuf=obuf, abuf=abuf, tbuf=tbuf, parts=parts,
+                       axes_mask=axes_mask, n_final=n_final)
         if formatted:
             return self._format_device(ctx, st, fin, n_final, final_shape)
         final = np.zeros(n_final, dtype=engine.partial_dtype(dt))
@@ -653,15 +773,20 @@ class Active:
                 return False
         return True
 
-    def _format_device(self, ctx, st, fin, n, shape):
+    def _format_device(self, ctx, st, fin, n, shape, bufs=None):
         """``_format`` on the device (pyas_format_partials): only the
-        result's values, mask (and counts in components mode) come back."""
+        result's values, mask (and counts in components mode) come back.
+        ``bufs``: a dict that keeps the device result buffers for reuse."""
         dt = self.ds.dtype
         method = "sum" if (self._components and self._method == "mean") else self._method
         vdt = engine.format_dtype(dt, method)
-        vbuf = DeviceBuffer(ctx, max(n, 1) * vdt.itemsize)
-        mbuf = DeviceBuffer(ctx, max(n, 1))
-        cbuf = DeviceBuffer(ctx, max(n, 1) * 8) if self._components else None
+        have = bufs.get((vdt.str, self._components)) if bufs is not None else None
+        if have is None:
+            have = (DeviceBuffer(ctx, max(n, 1) * vdt.itemsize), DeviceBuffer(ctx, max(n, 1)),
+                    DeviceBuffer(ctx, max(n, 1) * 8) if self._components else None)
+            if bufs is not None:
+                bufs[(vdt.str, self._components)] = have
+        vbuf, mbuf, cbuf = have
         engine.format_partials(ctx, dt, fin.ptr, n, method, vbuf.ptr, mbuf.ptr,
                                cbuf.ptr if cbuf is not None else None, st)
         vals = np.empty(n, dtype=vdt)

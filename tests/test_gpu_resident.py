@@ -108,3 +108,59 @@ def test_release_while_queries_run(gpu):
         _same(g, want, f"racing query {k}")
     release_resident(var)
     assert getattr(var, "_pyas_resident", None) is None
+
+
+def _q(act, method, axis):
+    """Set up a query as the reference's users do (active.method, axis)."""
+    act.method = method
+    act._axis = axis
+    return act
+
+
+def test_resident_plan_replay(gpu, monkeypatch):
+    """Repeat box queries replay the cached device plan (_CachedQuery): the
+    same results as a fresh query for every method, components mode and
+    axis set, a new plan when the missing-data attributes change, and no
+    plans left after release_resident."""
+    from pyactivestorage_amd import active as A
+    var = D.make_variable()
+    nd = len(var.shape)
+    built = []
+    real = A._CachedQuery.__init__
+
+    def spy(self, *a, **k):
+        built.append(1)
+        real(self, *a, **k)
+    monkeypatch.setattr(A._CachedQuery, "__init__", spy)
+    index = (slice(1, None),) + (slice(None),) * (nd - 1)
+    try:
+        for axis in (None, (0,), (nd - 1,), (0, nd - 1)):
+            for method in ("mean", "sum", "min", "max"):
+                want = _q(Active(var), method, axis)[index]
+                act = _q(Active(var, resident=True), method, axis)
+                first = act[index]
+                n_built = len(built)
+                for _ in range(2):
+                    again = _q(act, method, axis)[index]
+                    _same(again, want, f"{method} {axis} replay", "exact")
+                _same(first, want, f"{method} {axis}", "exact")
+                assert len(built) == n_built            # replays built nothing
+                act.components = True
+                comp = _q(act, method, axis)[index]
+                ref_act = Active(var)
+                ref_act.components = True
+                ref = _q(ref_act, method, axis)[index]
+                assert comp.keys() == ref.keys()
+                for k in ref:
+                    _same(comp[k], ref[k], f"{method} {axis} components {k}", "exact")
+        store = var._pyas_resident
+        n_plans = len(store["plans"])
+        assert n_plans == 4                              # one per axis set (method-independent)
+        var.attrs = dict(var.attrs, valid_max=np.array([50.0], dtype=var.dtype))
+        want, _ = _query(var, "mean", None, index, False)
+        got, _ = _query(var, "mean", None, index, True)
+        _same(got, want, "changed valid_max", "exact")
+        assert len(store["plans"]) == n_plans + 1
+    finally:
+        release_resident(var)
+    assert getattr(var, "_pyas_resident", None) is None

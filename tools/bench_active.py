@@ -91,7 +91,8 @@ def main():
                 r = act[...]
                 times.append(time.perf_counter() - t0)
             t = float(np.median(times))
-            res[str(axis)] = {"s": round(t, 4), "GBps_file_to_result": round(nbytes / t / 1e9, 2),
+            rate = "GBps_hbm_resident_query" if a.resident else "GBps_file_to_result"
+            res[str(axis)] = {"s": round(t, 4), "ms": round(t * 1e3, 3), rate: round(nbytes / t / 1e9, 2),
                               "result_shape": list(np.shape(r))}
             print(json.dumps({str(axis): res[str(axis)]}), flush=True)
             if a.profile:
@@ -103,7 +104,7 @@ def main():
                     act.mean(axis=axis)
                     act[...]
                 pr.disable()
-                pstats.Stats(pr).sort_stats("tottime").print_stats(14)
+                pstats.Stats(pr).sort_stats("tottime").print_stats(22)
     finally:
         if os.path.exists(path):
             os.unlink(path)
