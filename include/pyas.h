@@ -170,6 +170,40 @@ int pyas_ctx_set_chained_combine(pyas_ctx *ctx, int32_t on);
  * (PYAS_ENOTSUP, two-step path) below n / 4.  0 restores the default 2048. */
 int pyas_ctx_set_fold_min_blocks(pyas_ctx *ctx, int64_t n);
 
+/* ---- NumPy's sign of a zero min/max -------------------------------------
+ * storage.py:99-100 returns np.ma.min/max of a chunk's selected, masked
+ * elements, and active.py:598 reduces the per-chunk results the same way.
+ * When that extreme is zero and +0.0 and -0.0 both occur, the zero NumPy
+ * returns is decided by its reduction loop: one accumulator per SIMD lane
+ * seeded with the running result (a later element wins a tie in its lane),
+ * a fixed lane tree, a scalar remainder (later wins), over the flattened
+ * C-ordered data in pieces of np.getbufsize() elements after the seeding
+ * first element.  The lane count and tree depend on the SIMD target NumPy
+ * dispatches on the host, so the host derives them from NumPy
+ * (pyactivestorage_amd/zerosign.py) and sets them per float dtype:
+ *   lanes 1..64, piece >= 1, rank[lane] = priority (0 = wins every tie). */
+typedef struct {
+    int32_t lanes;
+    int32_t piece;
+    uint8_t rank[64];
+} pyas_tie_rule;
+/* dtype PYAS_F32 or PYAS_F64; rule NULL clears it (no sign rewriting). */
+int pyas_ctx_set_tie_rule(pyas_ctx *ctx, int32_t dtype, const pyas_tie_rule *rule);
+/* For every chunk c of `batch` (float dtypes; others: no-op) whose
+ * partials[c] (device) has count > 0 and a zero min (which bit 0) / max
+ * (bit 1): rewrite that zero's sign as NumPy's over the chunk's selected
+ * elements in C order (masked elements never tie).  No-op without a rule.
+ * PYAS_ENOTSUP when a chunk's selection exceeds the kernel's table (more
+ * than ~60 KiB of (pieces x (lanes + 1)) slots). */
+int pyas_zero_sign_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, uint32_t which,
+                          pyas_partial *partials, void *stream);
+/* The same over a sequence: `total` (device) is the combine of partials[0,
+ * n) (device, in the reference's `out` C order; count == 0 = masked); when
+ * its min / max is zero, rewrite the sign as np.ma.min/max over the
+ * per-chunk values would leave it (active.py:598). */
+int pyas_zero_sign_seq(pyas_ctx *ctx, int32_t dtype, const pyas_partial *partials, int64_t n,
+                       uint32_t which, pyas_partial *total, void *stream);
+
 /* ---- memory helpers (so a non-torch host can drive the ABI) ------------- */
 int pyas_malloc(pyas_ctx *ctx, size_t nbytes, void **dptr);
 int pyas_free(pyas_ctx *ctx, void *dptr);

@@ -102,6 +102,15 @@ class ChunkDesc(ctypes.Structure):
     ]
 
 
+class TieRule(ctypes.Structure):
+    """pyas_tie_rule: NumPy's zero-sign tie rule (zerosign.py)."""
+    _fields_ = [
+        ("lanes", ctypes.c_int32),
+        ("piece", ctypes.c_int32),
+        ("rank", ctypes.c_uint8 * 64),
+    ]
+
+
 PARTIAL_NBYTES = ctypes.sizeof(Partial)
 assert PARTIAL_NBYTES == 32
 
@@ -122,6 +131,9 @@ SIGNATURES = {
     "pyas_ctx_set_inflate_window_bits": [_vp, _i32],
     "pyas_ctx_set_chained_combine": [_vp, _i32],
     "pyas_ctx_set_fold_min_blocks": [_vp, _i64],
+    "pyas_ctx_set_tie_rule": [_vp, _i32, ctypes.POINTER(TieRule)],
+    "pyas_zero_sign_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _u32, _vp, _vp],
+    "pyas_zero_sign_seq": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
     "pyas_malloc": [_vp, _sz, ctypes.POINTER(_vp)],
     "pyas_free": [_vp, _vp],
     "pyas_host_alloc": [_vp, _sz, ctypes.POINTER(_vp)],

@@ -112,8 +112,7 @@ class _CachedQuery:
         st = ctx.thread_stream()
         shape = self.final_shape
         if self.grid is None:
-            self.plan.launch(st, chunk_partials=False)
-            final = self.plan.read_total(st)
+            final = act._total(self.plan, st)
             return act._format(final.reshape(shape), shape)
         g = self.grid
         if g["folded"]:
@@ -628,8 +627,7 @@ class Active:
                                  missing=self.missing, round_to_var=True, stream=st)
             cacheable = cache_key is not None and self.resident and self.group is None
             if len(axes) == ds.ndim:
-                plan.launch(st, chunk_partials=False)
-                final = plan.read_total(st)
+                final = self._total(plan, st)
                 if cacheable:
                     self._remember(cache_key, _CachedQuery(plan, final_shape))
             else:
@@ -647,6 +645,24 @@ class Active:
         if self.group is not None:
             final = self._exchange(final)
         return self._format(final.reshape(final_shape), final_shape)
+
+    def _total(self, plan, st):
+        """Full reduction of the plan's chunks: the combined partial.  For
+        min/max of a float variable the chunk partials are kept so that a
+        zero extreme gets NumPy's sign: per chunk over its elements
+        (storage.py:99-100), then over the per-chunk values in the `out`
+        array's C order (active.py:598) -- pyas_zero_sign_chunks / _seq.
+        (Across a torch.distributed group the rank combine keeps the sign the
+        ranks' totals carry.)"""
+        zs = self._method in ("min", "max") and self.ds.dtype.kind == "f" and self.group is None
+        plan.launch(st, chunk_partials=zs)
+        if zs:
+            which = 1 if self._method == "min" else 2
+            if engine.zero_sign_chunks(plan.ctx, plan.batch, plan.mask_up.struct, which,
+                                       plan.chunk_partials.ptr, st):
+                engine.zero_sign_seq(plan.ctx, self.ds.dtype, plan.chunk_partials.ptr, plan.n_chunks, which,
+                                     plan.total.ptr, st)
+        return plan.read_total(st)
 
     def _exchange(self, final):
         """All-gather the per-rank partial grids (RCCL for an nccl group,
@@ -820,8 +836,7 @@ class Active:
         plan = ReductionPlan(ctx, dt, ds.chunks, buf.ptr, offsets, shuffle=fused, selections=sels,
                              missing=self.missing, round_to_var=True, stream=st)
         if len(axes) == ds.ndim:
-            plan.launch(st, chunk_partials=False)
-            final = plan.read_total(st)
+            final = self._total(plan, st)
             return self._format(final.reshape(final_shape), final_shape)
         axes_mask = 0
         for a in axes:

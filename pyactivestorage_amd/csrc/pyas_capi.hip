@@ -71,6 +71,7 @@ struct pyas_ctx {
     int32_t inflate_wbits = 13;   // LDS history ring of pyas_inflate: 2^13 B per stream
     bool chained = true;          // k_finish folds the total itself (arrival counter)
     int64_t fold_min_blocks = 2048;   // pyas_reduce_axes_grid: fewest workgroups worth folding
+    pyas::TieRule tie[2];             // NumPy's zero-sign rule for f32, f64 (lanes 0: unset)
     pyas::Ingest *ingest = nullptr;   // pinned staging ring of pyas_read_ranges (lazy)
     std::mutex mu;
     std::unordered_map<void *, Scratch> scratch;  // keyed by stream
@@ -327,6 +328,71 @@ int pyas_read_ranges(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offse
     const int rc = pyas::ingest_read(ingest_of(ctx), fd, n, file_offsets, sizes, (uint8_t *)dst,
                                      dst_offsets, threads, (hipStream_t)stream, msg);
     return rc ? fail(rc, "%s", msg.c_str()) : PYAS_OK;
+}
+
+int pyas_ctx_set_tie_rule(pyas_ctx *ctx, int32_t dtype, const pyas_tie_rule *rule) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (dtype != PYAS_F32 && dtype != PYAS_F64) return fail(PYAS_EINVAL, "tie rules are for f32/f64");
+    pyas::TieRule &t = ctx->tie[dtype == PYAS_F64 ? 1 : 0];
+    std::memset(&t, 0, sizeof(t));
+    if (!rule) return PYAS_OK;
+    if (rule->lanes < 1 || rule->lanes > 64 || rule->piece < 1)
+        return fail(PYAS_EINVAL, "tie rule: lanes %d, piece %d", rule->lanes, rule->piece);
+    bool seen[64] = {false};
+    for (int l = 0; l < rule->lanes; ++l) {
+        if (rule->rank[l] >= rule->lanes || seen[rule->rank[l]])
+            return fail(PYAS_EINVAL, "tie rule: rank is not a permutation of 0..%d", rule->lanes - 1);
+        seen[rule->rank[l]] = true;
+    }
+    t.lanes = rule->lanes;
+    t.piece = rule->piece;
+    std::memcpy(t.rank, rule->rank, sizeof(t.rank));
+    return PYAS_OK;
+}
+
+namespace {
+// LDS table of the zero-sign kernels: (pieces) x (lanes + 1) 8-byte slots
+constexpr int64_t kTieLdsMax = 60 * 1024;
+int64_t tie_lds(const pyas::TieRule &t, int64_t elems) {
+    const int64_t npieces = elems > 1 ? (elems - 1) / t.piece + 1 : 1;
+    return npieces * (t.lanes + 1) * 8;
+}
+}  // namespace
+
+int pyas_zero_sign_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, uint32_t which,
+                          pyas_partial *partials, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    pyas::ReduceArgs a;
+    int es;
+    bool shuf, bsw, masked;
+    int rc = prepare(ctx, batch, mask, a, es, shuf, bsw, masked);
+    if (rc) return rc;
+    if (batch->dtype != PYAS_F32 && batch->dtype != PYAS_F64) return PYAS_OK;
+    const pyas::TieRule &t = ctx->tie[batch->dtype == PYAS_F64 ? 1 : 0];
+    if (t.lanes == 0 || batch->n_chunks == 0 || (which & 3u) == 0) return PYAS_OK;
+    if (!partials) return fail(PYAS_EINVAL, "partials is NULL");
+    const int64_t lds = tie_lds(t, a.chunk_elems);   // a selection never exceeds its chunk
+    if (lds > kTieLdsMax) return fail(PYAS_ENOTSUP, "zero-sign table for %lld elements exceeds LDS",
+                                      (long long)a.chunk_elems);
+    if (batch->n_chunks >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(pyas::launch_zero_sign_chunks(batch->dtype, a, shuf, bsw, t, which, partials, batch->n_chunks, lds,
+                                           (hipStream_t)stream));
+    return PYAS_OK;
+}
+
+int pyas_zero_sign_seq(pyas_ctx *ctx, int32_t dtype, const pyas_partial *partials, int64_t n,
+                       uint32_t which, pyas_partial *total, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (dtype != PYAS_F32 && dtype != PYAS_F64) return PYAS_OK;
+    const pyas::TieRule &t = ctx->tie[dtype == PYAS_F64 ? 1 : 0];
+    if (t.lanes == 0 || n <= 0 || (which & 3u) == 0) return PYAS_OK;
+    if (!partials || !total) return fail(PYAS_EINVAL, "NULL argument");
+    const int64_t lds = tie_lds(t, n);
+    if (lds > kTieLdsMax) return fail(PYAS_ENOTSUP, "zero-sign table for %lld partials exceeds LDS", (long long)n);
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(pyas::launch_zero_sign_seq(dtype, partials, n, t, which, total, lds, (hipStream_t)stream));
+    return PYAS_OK;
 }
 
 int pyas_ctx_set_fold_min_blocks(pyas_ctx *ctx, int64_t n) {

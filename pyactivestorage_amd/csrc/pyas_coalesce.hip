@@ -459,9 +459,13 @@ void launch_batch(pyas_coalescer *c, Slot *sl) {
         b.index_pool = (const int32_t *)(dm + m.pool_off);
         const uint32_t full = (g.key.desc.ndim >= 32) ? 0xffffffffu : ((1u << g.key.desc.ndim) - 1u);
         if (rc == PYAS_OK) {
-            if ((g.key.desc.axes_mask & full) == full)
+            if ((g.key.desc.axes_mask & full) == full) {
                 rc = pyas_reduce_chunks(c->ctx, &b, &g.key.mask, dout + m.out_base, nullptr, 0u, sl->st);
-            else
+                // NumPy's sign of a zero min/max (the method is not known here: both)
+                if (rc == PYAS_OK)
+                    rc = pyas_zero_sign_chunks(c->ctx, &b, &g.key.mask, 3u, dout + m.out_base, sl->st);
+                if (rc == PYAS_ENOTSUP) rc = PYAS_OK;   // a chunk too large for the table: sign as reduced
+            } else
                 rc = pyas_reduce_axes(c->ctx, &b, &g.key.mask, g.key.desc.axes_mask, d_oofs, dout, sl->st);
         }
         if (rc != PYAS_OK) {

@@ -129,6 +129,17 @@ hipError_t launch_axes_fold_t(const AxesArgs &a, const FoldGrid &g, bool masked,
                               hipStream_t st);
 template <typename T>
 hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st);
+// NumPy's zero sign (pyas_zero_sign_chunks / _seq); float types only
+struct TieRule {
+    int32_t lanes, piece;
+    uint8_t rank[64];
+};
+template <typename T>
+hipError_t launch_zero_sign_chunks_t(const ReduceArgs &r, bool shuf, bool bswap, const TieRule &t,
+                                     uint32_t which, pyas_partial *parts, int64_t n_chunks, int64_t lds_bytes, hipStream_t st);
+template <typename T>
+hipError_t launch_zero_sign_seq_t(const pyas_partial *parts, int64_t n, const TieRule &t, uint32_t which,
+                                  pyas_partial *total, int64_t lds_bytes, hipStream_t st);
 template <typename T>
 hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, void *values,
                            uint8_t *mask, int64_t *counts, hipStream_t st);
@@ -151,6 +162,10 @@ hipError_t launch_axes_fold(int dtype, const AxesArgs &a, const FoldGrid &g, boo
                             hipStream_t st);
 hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
+hipError_t launch_zero_sign_chunks(int dtype, const ReduceArgs &r, bool shuf, bool bswap, const TieRule &t,
+                                   uint32_t which, pyas_partial *parts, int64_t n_chunks, int64_t lds_bytes, hipStream_t st);
+hipError_t launch_zero_sign_seq(int dtype, const pyas_partial *parts, int64_t n, const TieRule &t,
+                                uint32_t which, pyas_partial *total, int64_t lds_bytes, hipStream_t st);
 hipError_t launch_format(int dtype, const pyas_partial *in, int64_t n, int32_t method, void *values,
                          uint8_t *mask, int64_t *counts, hipStream_t st);
 // host ingest (pyas_ingest.hip): pread ring -> pinned slots -> H2D

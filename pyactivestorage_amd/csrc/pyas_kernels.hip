@@ -134,6 +134,18 @@ hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_zero_sign_chunks(int dtype, const ReduceArgs &r, bool shuf, bool bswap, const TieRule &t,
+                                   uint32_t which, pyas_partial *parts, int64_t n_chunks, int64_t lds_bytes, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_zero_sign_chunks_t<T>(r, shuf, bswap, t, which, parts, n_chunks, lds_bytes, st));
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_zero_sign_seq(int dtype, const pyas_partial *parts, int64_t n, const TieRule &t,
+                                uint32_t which, pyas_partial *total, int64_t lds_bytes, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_zero_sign_seq_t<T>(parts, n, t, which, total, lds_bytes, st));
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_format(int dtype, const pyas_partial *in, int64_t n, int32_t method, void *values,
                          uint8_t *mask, int64_t *counts, hipStream_t st) {
     PYAS_DISPATCH_T(dtype, return launch_format_t<T>(in, n, method, values, mask, counts, st));

@@ -765,6 +765,46 @@ __device__ __forceinline__ void axes_walk_lds(const uint8_t *base, int64_t chunk
 
 // Fold the S split partials of each of OT outputs through LDS in split order
 // (deterministic); thread (ol, sp=0) ends with the folded value.
+// fold_splits for the N accumulators of a lane at once: one barrier pair
+// per pass instead of one per output.  `lds`: fold_lds_bytes<T, N>() bytes.
+template <typename T, int N>
+constexpr int fold_lds_bytes() {
+    return N * kBlock * (int)(sizeof(typename TT<T>::Acc) + sizeof(uint32_t) + 2 * sizeof(T) + 1);
+}
+template <typename T, int N>
+__device__ __forceinline__ void fold_splits_n(TileAcc<T> *acc, int S, int OT, int ol, int sp, void *lds) {
+    using A = typename TT<T>::Acc;
+    A *l_sum = reinterpret_cast<A *>(lds);
+    uint32_t *l_cnt = reinterpret_cast<uint32_t *>(l_sum + N * kBlock);
+    T *l_mn = reinterpret_cast<T *>(l_cnt + N * kBlock);
+    T *l_mx = l_mn + N * kBlock;
+    uint8_t *l_nan = reinterpret_cast<uint8_t *>(l_mx + N * kBlock);
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        l_sum[k * kBlock + t] = acc[k].sum;
+        l_cnt[k * kBlock + t] = acc[k].count;
+        l_mn[k * kBlock + t] = acc[k].mn;
+        l_mx[k * kBlock + t] = acc[k].mx;
+        l_nan[k * kBlock + t] = acc[k].nan ? 1 : 0;
+    }
+    __syncthreads();
+    if (sp == 0) {
+        for (int q = 1; q < S; ++q) {
+            const int u = q * OT + ol;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                acc[k].sum += l_sum[k * kBlock + u];
+                acc[k].count += l_cnt[k * kBlock + u];
+                acc[k].mn = tmin(acc[k].mn, l_mn[k * kBlock + u]);
+                acc[k].mx = tmax(acc[k].mx, l_mx[k * kBlock + u]);
+                acc[k].nan = acc[k].nan || l_nan[k * kBlock + u];
+            }
+        }
+    }
+    __syncthreads();
+}
+
 template <typename T>
 __device__ __forceinline__ void fold_splits(TileAcc<T> &acc, int S, int OT, int ol, int sp) {
     __shared__ typename TT<T>::Acc l_sum[kBlock];
@@ -1152,16 +1192,62 @@ __device__ __forceinline__ void store_group(const TileAcc<T> &a, uint32_t cnt, u
 }
 
 #ifndef PYAS_COL_U
-#define PYAS_COL_U 8      // 16-B loads in flight per lane (column layout)
+#define PYAS_COL_U 4      // 16-B loads per step per lane (column layout; measured 4 >= 8)
 #endif
-#ifndef PYAS_DENSE_WAVES
-#define PYAS_DENSE_WAVES 0
+// Occupancy floors (waves per SIMD; 0 = none) of the partial-axis kernels,
+// per layout: column / row / LDS-row per-chunk kernels, column / LDS-row
+// in-kernel folds.  A floor caps VGPRs at 512 / waves (minus granularity).
+#ifndef PYAS_COL_WAVES
+#define PYAS_COL_WAVES 0
 #endif
-#if PYAS_DENSE_WAVES
-#define PYAS_DENSE_ATTR __attribute__((amdgpu_waves_per_eu(PYAS_DENSE_WAVES, 8)))
-#else
-#define PYAS_DENSE_ATTR
+#ifndef PYAS_ROW_WAVES
+#define PYAS_ROW_WAVES 0
 #endif
+#ifndef PYAS_LDS_WAVES
+#define PYAS_LDS_WAVES 0
+#endif
+#ifndef PYAS_FOLD_COL_WAVES
+#define PYAS_FOLD_COL_WAVES 0
+#endif
+#ifndef PYAS_FOLD_ROW_WAVES
+#define PYAS_FOLD_ROW_WAVES 0
+#endif
+#define PYAS_WAVES_FLOOR_(W) __attribute__((amdgpu_waves_per_eu(W, 8)))
+#define PYAS_WAVES_FLOOR(W) PYAS_WAVES_FLOOR_##W
+#define PYAS_WAVES_FLOOR_0
+#define PYAS_WAVES_FLOOR_1 PYAS_WAVES_FLOOR_(1)
+#define PYAS_WAVES_FLOOR_2 PYAS_WAVES_FLOOR_(2)
+#define PYAS_WAVES_FLOOR_3 PYAS_WAVES_FLOOR_(3)
+#define PYAS_WAVES_FLOOR_4 PYAS_WAVES_FLOOR_(4)
+#define PYAS_WAVES_FLOOR_5 PYAS_WAVES_FLOOR_(5)
+#define PYAS_WAVES_FLOOR_6 PYAS_WAVES_FLOOR_(6)
+#define PYAS_WAVES_FLOOR_7 PYAS_WAVES_FLOOR_(7)
+#define PYAS_WAVES_FLOOR_8 PYAS_WAVES_FLOOR_(8)
+#define PYAS_XATTR(W) PYAS_WAVES_FLOOR(W)
+
+// U rows of N outputs (16-B vectors w[u]) into acc[N]: output k's U rows as
+// groups of 4 (sums widened once per group, one mask test per element,
+// per-lane counts), one NaN ballot for all of them.
+template <typename T, bool BSWAP, int MASKED, int U>
+__device__ __forceinline__ void col_consume(const uint4 *w, TileAcc<T> *acc, const MaskT<T> &mk) {
+    constexpr int N = 16 / sizeof(T);
+    static_assert(U % 4 == 0, "PYAS_COL_U: a multiple of the 4-row sum groups");
+    T xs[N][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        T x[N];
+        unpack16<T, BSWAP>(w[u], x);
+#pragma unroll
+        for (int k = 0; k < N; ++k) xs[k][u] = x[k];
+    }
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < N; ++k) bad |= acc[k].template add_lazy<U, MASKED, false>(xs[k], mk);
+    if (__builtin_expect(__ballot(bad) != 0, 0)) {   // a NaN (or inf - inf) somewhere
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k].template check_nan<U>(xs[k]);
+    }
+}
 
 // One pass of the column layout over one chunk: lane (il, sp) folds split
 // sp of the reduced rows of vector item i (N consecutive kept outputs) into
@@ -1186,29 +1272,12 @@ __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base
         if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
     };
     constexpr int U = PYAS_COL_U;
-    static_assert(U % 4 == 0, "PYAS_COL_U: a multiple of the 4-row sum groups");
     int64_t t = 0;
     for (; t + U <= nt; t += U) {
         uint4 w[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) { w[u] = ldv<T, SHUF, AL>(base, p, n); next(); }
-        // output k's U rows as groups of 4 (sums widened once per group,
-        // one mask test per element, per-lane counts)
-        T xs[N][U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            T x[N];
-            unpack16<T, BSWAP>(w[u], x);
-#pragma unroll
-            for (int k = 0; k < N; ++k) xs[k][u] = x[k];
-        }
-        bool bad = false;
-#pragma unroll
-        for (int k = 0; k < N; ++k) bad |= acc[k].template add_lazy<U, MASKED, false>(xs[k], mk);
-        if (__builtin_expect(__ballot(bad) != 0, 0)) {   // a NaN (or inf - inf) somewhere
-#pragma unroll
-            for (int k = 0; k < N; ++k) acc[k].template check_nan<U>(xs[k]);
-        }
+        col_consume<T, BSWAP, MASKED, U>(w, acc, mk);
     }
     for (; t < nt; ++t) {
         T x[N];
@@ -1242,10 +1311,12 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
         if constexpr (N <= 4) {
             // Stage the pass's IT*N partials (<= 32 KiB) in LDS, then write
             // them as consecutive 16-B stores (a lane's own N partials are
-            // 32*N bytes apart from its neighbours').
+            // 32*N bytes apart from its neighbours').  The split fold uses
+            // the same LDS first (fold_lds_bytes <= 32 KiB for N <= 4).
+            static_assert(fold_lds_bytes<T, N>() <= kBlock * 4 * 2 * 16, "fold scratch exceeds the stage");
+            if (S > 1) fold_splits_n<T, N>(acc, S, IT, il, sp, stage);
 #pragma unroll
             for (int k = 0; k < N; ++k) {
-                if (S > 1) fold_splits(acc[k], S, IT, il, sp);
                 if (sp == 0) {
                     pyas_partial pp;
                     tile_store_lane(acc[k], &pp);
@@ -1428,7 +1499,7 @@ __device__ __forceinline__ bool dense_owns(const AxesArgs &a, const Sel &s) {
 }
 
 template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
-__global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs a) {
+__device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
     const int64_t c = blockIdx.x / a.d.bpc;
     const int64_t j = blockIdx.x - c * a.d.bpc;
     const ReduceArgs &r = a.r;
@@ -1458,6 +1529,20 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs 
     }
 }
 
+// One kernel per layout family, so each carries its own occupancy floor.
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_COL_WAVES) void k_axes_dense_col(AxesArgs a) {
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE>(a);
+}
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_ROW_WAVES) void k_axes_dense_row(AxesArgs a) {
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE>(a);
+}
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LDS_WAVES) void k_axes_dense_lds(AxesArgs a) {
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE>(a);
+}
+
 // Whole-chunk box query, column layout, chunk layers folded in the kernel
 // (pyas_reduce_axes_grid).  Block (col, j) owns the kept-dims chunk column
 // `col` and items j, j + bpc, ... of it; for each layer (the column's chunks
@@ -1467,7 +1552,7 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_dense(AxesArgs 
 // k_axes_dense + k_combine_grid's, operation for operation, so the result is
 // bit-identical; the per-chunk partial arrays are never written.
 template <typename T, bool SHUF, bool BSWAP, int MASKED>
-__global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold(AxesArgs a, FoldGrid g) {
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes_fold(AxesArgs a, FoldGrid g) {
     constexpr int N = 16 / sizeof(T);
     const AxesDense &d = a.d;
     const ReduceArgs &r = a.r;
@@ -1496,38 +1581,109 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold(AxesArgs a
     const int il = threadIdx.x & (IT - 1), sp = threadIdx.x / IT;
     const int64_t items = d.KO * (d.KI / N);
     const bool round = (g.flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
+    __shared__ __attribute__((aligned(16))) uint8_t fold_lds[fold_lds_bytes<T, N>()];
+    auto layer_base = [&](int64_t l) {
+        int64_t n = nk, rr = l;
+#pragma unroll
+        for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+            if (dd < r.ndim && ((red >> dd) & 1u)) {
+                const int64_t q = rr / g.n_coords[dd];
+                n += (rr - q * g.n_coords[dd]) * gstride[dd];
+                rr = q;
+            }
+        }
+        return r.data + r.offsets[n];
+    };
+    // Pipelined walk (block-uniform choice): every lane has the same rows per
+    // layer, a multiple of U, and every layer is aligned, so the walk is
+    // one stream of U-row steps whose next step's loads -- across a layer
+    // boundary too -- are in flight while the current step is consumed.
+    constexpr int U = PYAS_COL_U, ES = sizeof(T);
+    const int64_t R = d.RO * d.RI;
+    bool pipe = R % S == 0 && (R / S) % U == 0;
+    for (int64_t l = 0; pipe && l < g.n_layers; ++l) pipe = ldv_aligned<T, SHUF>(layer_base(l), r.chunk_elems);
+    const int64_t KIV = d.KI / N, sRO = d.KO * d.RI * d.KI;
+    const int64_t dq = S / d.RI, dr = S - dq * d.RI;
+    const int64_t step_off = (dq * sRO + dr * d.KI) * ES, wrap_off = (sRO - d.RI * d.KI) * ES;
     for (int64_t i0 = j * IT; i0 < items; i0 += d.bpc * IT) {   // block-uniform
         const int64_t i = i0 + il;
         WAcc<T> w[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) w[k].init();
-        for (int64_t l = 0; l < g.n_layers; ++l) {
-            int64_t n = nk, rr = l;
+        const bool act = i < items && sp < S && sp < R;
+        if (pipe) {
+            const int64_t ntu = R / S;
+            const int64_t ko = i / KIV, v = i - ko * KIV, ro0 = sp / d.RI, ri0 = sp - ro0 * d.RI;
+            const int64_t off0 = ((ro0 * d.KO + ko) * d.RI * d.KI + ri0 * d.KI + v * N) * ES;
+            int64_t off = off0, ri = ri0;
+            const uint8_t *b = layer_base(0);
+            uint4 nx[U];
+            auto fetch = [&]() {
 #pragma unroll
-            for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
-                if (dd < r.ndim && ((red >> dd) & 1u)) {
-                    const int64_t q = rr / g.n_coords[dd];
-                    n += (rr - q * g.n_coords[dd]) * gstride[dd];
-                    rr = q;
+                for (int u = 0; u < U; ++u) {
+                    nx[u] = ldv<T, SHUF, true>(b, b + off, r.chunk_elems);
+                    off += step_off;
+                    ri += dr;
+                    if (ri >= d.RI) { ri -= d.RI; off += wrap_off; }
+                }
+            };
+            if (act) fetch();
+            for (int64_t l = 0; l < g.n_layers; ++l) {
+                TileAcc<T> acc[N];
+#pragma unroll
+                for (int k = 0; k < N; ++k) acc[k].init();
+                for (int64_t t = 0; t < ntu; t += U) {
+                    uint4 cur[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) cur[u] = nx[u];
+                    if (act) {
+                        if (t + U < ntu) {
+                            fetch();
+                        } else if (l + 1 < g.n_layers) {   // the next layer's first step
+                            b = layer_base(l + 1);
+                            off = off0;
+                            ri = ri0;
+                            fetch();
+                        }
+                        col_consume<T, BSWAP, MASKED, U>(cur, acc, mk);
+                    }
+                }
+                if constexpr (!MASKED) {
+                    if (act) {
+#pragma unroll
+                        for (int k = 0; k < N; ++k) acc[k].count += (uint32_t)ntu;
+                    }
+                }
+                if (S > 1) fold_splits_n<T, N>(acc, S, IT, il, sp, fold_lds);
+                if (sp == 0) {
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        pyas_partial pp;
+                        tile_store_lane(acc[k], &pp);
+                        merge(w[k], pp, round);
+                    }
                 }
             }
-            const uint8_t *base = r.data + r.offsets[n];
-            TileAcc<T> acc[N];
+        } else {
+            for (int64_t l = 0; l < g.n_layers; ++l) {
+                const uint8_t *base = layer_base(l);
+                TileAcc<T> acc[N];
 #pragma unroll
-            for (int k = 0; k < N; ++k) acc[k].init();
-            if (i < items && sp < S && sp < d.RO * d.RI) {
-                if (ldv_aligned<T, SHUF>(base, r.chunk_elems))
-                    col_rows<T, SHUF, BSWAP, MASKED, true>(d, base, r.chunk_elems, i, sp, mk, acc);
-                else
-                    col_rows<T, SHUF, BSWAP, MASKED, false>(d, base, r.chunk_elems, i, sp, mk, acc);
-            }
-#pragma unroll
-            for (int k = 0; k < N; ++k) {
-                if (S > 1) fold_splits(acc[k], S, IT, il, sp);
+                for (int k = 0; k < N; ++k) acc[k].init();
+                if (act) {
+                    if (ldv_aligned<T, SHUF>(base, r.chunk_elems))
+                        col_rows<T, SHUF, BSWAP, MASKED, true>(d, base, r.chunk_elems, i, sp, mk, acc);
+                    else
+                        col_rows<T, SHUF, BSWAP, MASKED, false>(d, base, r.chunk_elems, i, sp, mk, acc);
+                }
+                if (S > 1) fold_splits_n<T, N>(acc, S, IT, il, sp, fold_lds);
                 if (sp == 0) {
-                    pyas_partial pp;
-                    tile_store_lane(acc[k], &pp);
-                    merge(w[k], pp, round);
+#pragma unroll
+                    for (int k = 0; k < N; ++k) {
+                        pyas_partial pp;
+                        tile_store_lane(acc[k], &pp);
+                        merge(w[k], pp, round);
+                    }
                 }
             }
         }
@@ -1558,7 +1714,7 @@ __global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold(AxesArgs a
 // (k_combine_grid's merge, same rounding).  Bit-identical to k_axes_dense +
 // k_combine_grid; the next layer's tile is loaded while this one is folded.
 template <typename T, bool SHUF, bool BSWAP, int MASKED, int H>
-__global__ __launch_bounds__(kBlock) PYAS_DENSE_ATTR void k_axes_fold_row(AxesArgs a, FoldGrid g) {
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes_fold_row(AxesArgs a, FoldGrid g) {
     constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
     constexpr int UL = 16 / H / VPL > 0 ? 16 / H / VPL : 1;   // load units per lane per tile
     __shared__ uint4 tile[(kBlock / kWave) * RPW * kRowLdsStride];
@@ -1742,6 +1898,159 @@ __global__ __launch_bounds__(kBlock) void k_select(SelectArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// NumPy's sign of a zero min/max (pyas.h pyas_tie_rule; zerosign.py)
+// ---------------------------------------------------------------------------
+// Flattened element e >= 1 of S (e == 0 seeds the result) falls in piece k
+// (piece 0 = [1, P), piece k = [kP, (k+1)P)), in lane (e - start) % L of the
+// piece's vector part or in its scalar remainder (slot L).
+__device__ __forceinline__ void tie_slot(int64_t e, int64_t S, const TieRule &t, int64_t &k, int &slot) {
+    const int64_t P = t.piece;
+    k = e / P;
+    const int64_t s0 = k == 0 ? 1 : k * P;
+    const int64_t e1 = (k + 1) * P < S ? (k + 1) * P : S;
+    const int64_t m = e1 - s0, nv = m - m % t.lanes, o = e - s0;
+    slot = o < nv ? (int)(o % t.lanes) : t.lanes;
+}
+
+// Thread 0, after the scan: tab[k * (L + 1) + slot] holds ((e + 1) << 1 |
+// signbit) of the last zero there (0: none).  Replays the loop's ties piece
+// by piece: with a zero already in hand every lane ties, so the rank-0 lane
+// decides (its own last zero, else the carried result); otherwise the best
+// ranked lane holding a zero; then the remainder's last zero.
+__device__ bool tie_fold(const uint64_t *tab, int64_t npieces, const TieRule &t, bool have, bool &sign) {
+    const int L = t.lanes;
+    int top = 0;
+    for (int l = 0; l < L; ++l)
+        if (t.rank[l] == 0) top = l;
+    for (int64_t k = 0; k < npieces; ++k) {
+        const uint64_t *row = tab + k * (L + 1);
+        if (have) {
+            if (row[top]) sign = row[top] & 1u;
+        } else {
+            int best = -1, br = 1 << 30;
+            for (int l = 0; l < L; ++l)
+                if (row[l] && t.rank[l] < br) { br = t.rank[l]; best = l; }
+            if (best >= 0) { sign = row[best] & 1u; have = true; }
+        }
+        if (row[L]) { sign = row[L] & 1u; have = true; }
+    }
+    return have;
+}
+
+template <typename T>
+__device__ __forceinline__ void tie_record(uint64_t *tab, int64_t e, int64_t S, const TieRule &t, T x,
+                                           uint32_t *seed) {
+    const uint64_t sg = __builtin_signbit(x) ? 1u : 0u;
+    if (e == 0) {
+        *seed = 1u | (uint32_t)(sg << 1);
+        return;
+    }
+    int64_t k;
+    int slot;
+    tie_slot(e, S, t, k, slot);
+    atomicMax(reinterpret_cast<unsigned long long *>(tab + k * (t.lanes + 1) + slot),
+              (unsigned long long)((((uint64_t)e + 1) << 1) | sg));
+}
+
+// One workgroup per chunk; chunks whose min/max is not a zero return at once.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_zero_sign_chunks(ReduceArgs r, bool shuf, bool bswap, TieRule t,
+                                                             uint32_t which, pyas_partial *parts) {
+    extern __shared__ uint64_t tab[];
+    __shared__ uint32_t seed;
+    const int64_t c = blockIdx.x;
+    pyas_partial p = parts[c];
+    if (p.count <= 0) return;
+    const bool fmin = (which & 1u) && TT<T>::from(p.min) == (T)0;
+    const bool fmax = (which & 2u) && TT<T>::from(p.max) == (T)0;
+    if (!fmin && !fmax) return;   // block-uniform
+    Sel s;
+    load_sel(s, r.sel, c, r.ndim, r.shape);
+    int64_t S = 1;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) S *= s.cnt[d];
+    const int64_t npieces = S > 1 ? (S - 1) / t.piece + 1 : 0;
+    for (int64_t q = threadIdx.x; q < npieces * (t.lanes + 1); q += kBlock) tab[q] = 0;
+    if (threadIdx.x == 0) seed = 0;
+    __syncthreads();
+    const uint8_t *base = r.data + r.offsets[c];
+    MaskT<T> mk;
+    mk.init(r.mask);
+    const uint32_t all = (1u << r.ndim) - 1u;
+    for (int64_t e = threadIdx.x; e < S; e += kBlock) {
+        Decomp o{0, {0, 0}};
+        decompose(s, r.pool, r.cstride, r.tab, r.ndim, all, e, o);
+        const T x = load_elem_rt<T>(base, r.chunk_elems, o.mem, shuf, bswap);
+        if (x == (T)0 && !all_masked(mk, r.tab, o, x)) tie_record(tab, e, S, t, x, &seed);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        bool sign = (seed >> 1) & 1u;
+        if (tie_fold(tab, npieces, t, (seed & 1u) != 0, sign)) {
+            const T z = sign ? -(T)0 : (T)0;
+            if (fmin) TT<T>::put(parts[c].min, z);
+            if (fmax) TT<T>::put(parts[c].max, z);
+        }
+    }
+}
+
+// One workgroup over the sequence of per-chunk values (min or max).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_zero_sign_seq(const pyas_partial *parts, int64_t n, TieRule t,
+                                                          bool use_max, pyas_partial *total) {
+    extern __shared__ uint64_t tab[];
+    __shared__ uint32_t seed;
+    const pyas_partial tp = *total;
+    if (tp.count <= 0 || TT<T>::from(use_max ? tp.max : tp.min) != (T)0) return;
+    const int64_t npieces = n > 1 ? (n - 1) / t.piece + 1 : 0;
+    for (int64_t q = threadIdx.x; q < npieces * (t.lanes + 1); q += kBlock) tab[q] = 0;
+    if (threadIdx.x == 0) seed = 0;
+    __syncthreads();
+    for (int64_t e = threadIdx.x; e < n; e += kBlock) {
+        const pyas_partial p = parts[e];
+        const T x = TT<T>::from(use_max ? p.max : p.min);
+        if (p.count > 0 && x == (T)0) tie_record(tab, e, n, t, x, &seed);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        bool sign = (seed >> 1) & 1u;
+        if (tie_fold(tab, npieces, t, (seed & 1u) != 0, sign)) {
+            const T z = sign ? -(T)0 : (T)0;
+            if (use_max) TT<T>::put(total->max, z);
+            else TT<T>::put(total->min, z);
+        }
+    }
+}
+
+template <typename T>
+hipError_t launch_zero_sign_chunks_t(const ReduceArgs &r, bool shuf, bool bswap, const TieRule &t,
+                                     uint32_t which, pyas_partial *parts, int64_t n_chunks, int64_t lds_bytes, hipStream_t st) {
+    if constexpr (TT<T>::kind != 0) {
+        return hipSuccess;
+    } else {
+        hipLaunchKernelGGL((k_zero_sign_chunks<T>), dim3((unsigned)n_chunks), dim3(kBlock), (size_t)lds_bytes,
+                           st, r, shuf, bswap, t, which, parts);
+        return hipGetLastError();
+    }
+}
+
+template <typename T>
+hipError_t launch_zero_sign_seq_t(const pyas_partial *parts, int64_t n, const TieRule &t, uint32_t which,
+                                  pyas_partial *total, int64_t lds_bytes, hipStream_t st) {
+    if constexpr (TT<T>::kind != 0) {
+        return hipSuccess;
+    } else {
+        if (which & 1u)
+            hipLaunchKernelGGL((k_zero_sign_seq<T>), dim3(1), dim3(kBlock), (size_t)lds_bytes, st, parts, n, t,
+                               false, total);
+        if (which & 2u)
+            hipLaunchKernelGGL((k_zero_sign_seq<T>), dim3(1), dim3(kBlock), (size_t)lds_bytes, st, parts, n, t,
+                               true, total);
+        return hipGetLastError();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // per-dtype launchers (declared in pyas_internal.hpp)
 // ---------------------------------------------------------------------------
 // Kernel mask mode for the scalar rules left in m (prepare() has dropped
@@ -1841,21 +2150,28 @@ hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int
 
 // Mask modes: all four for little-endian >= 4-byte data, {0, kMaskAll}
 // for byte-swapped or narrow data (fewer instantiations; same results).
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+static void launch_dense_k(const AxesArgs &a, dim3 g, hipStream_t st) {
+    const dim3 blk(kBlock);
+    if constexpr (MODE == 1) hipLaunchKernelGGL((k_axes_dense_col<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
+    else if constexpr (MODE >= 4) hipLaunchKernelGGL((k_axes_dense_lds<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_axes_dense_row<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
+}
+
 template <typename T, bool SHUF, int MODE>
 static void launch_dense_ms(const AxesArgs &a, bool masked, dim3 g, hipStream_t st) {
-    const dim3 blk(kBlock);
     const int mm = mask_mode(a.r.mask, masked);
     if (a.bswap && sizeof(T) > 1) {
-        if (mm) hipLaunchKernelGGL((k_axes_dense<T, SHUF, true, kMaskAll, MODE>), g, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_axes_dense<T, SHUF, true, 0, MODE>), g, blk, 0, st, a);
+        if (mm) launch_dense_k<T, SHUF, true, kMaskAll, MODE>(a, g, st);
+        else launch_dense_k<T, SHUF, true, 0, MODE>(a, g, st);
         return;
     }
     if constexpr (sizeof(T) >= 4) {
-        if (mm == kMaskRange) { hipLaunchKernelGGL((k_axes_dense<T, SHUF, false, kMaskRange, MODE>), g, blk, 0, st, a); return; }
-        if (mm == kMaskNoEq1) { hipLaunchKernelGGL((k_axes_dense<T, SHUF, false, kMaskNoEq1, MODE>), g, blk, 0, st, a); return; }
+        if (mm == kMaskRange) { launch_dense_k<T, SHUF, false, kMaskRange, MODE>(a, g, st); return; }
+        if (mm == kMaskNoEq1) { launch_dense_k<T, SHUF, false, kMaskNoEq1, MODE>(a, g, st); return; }
     }
-    if (mm) hipLaunchKernelGGL((k_axes_dense<T, SHUF, false, kMaskAll, MODE>), g, blk, 0, st, a);
-    else hipLaunchKernelGGL((k_axes_dense<T, SHUF, false, 0, MODE>), g, blk, 0, st, a);
+    if (mm) launch_dense_k<T, SHUF, false, kMaskAll, MODE>(a, g, st);
+    else launch_dense_k<T, SHUF, false, 0, MODE>(a, g, st);
 }
 
 template <typename T, int MODE>
@@ -2044,7 +2360,11 @@ hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, vo
                                                  hipStream_t);                               \
     template hipError_t launch_select_t<T>(const SelectArgs &, int64_t, hipStream_t);         \
     template hipError_t launch_format_t<T>(const pyas_partial *, int64_t, int32_t, void *,    \
-                                           uint8_t *, int64_t *, hipStream_t);
+                                           uint8_t *, int64_t *, hipStream_t);                \
+    template hipError_t launch_zero_sign_chunks_t<T>(const ReduceArgs &, bool, bool, const TieRule &, \
+                                                     uint32_t, pyas_partial *, int64_t, int64_t, hipStream_t); \
+    template hipError_t launch_zero_sign_seq_t<T>(const pyas_partial *, int64_t, const TieRule &,   \
+                                                  uint32_t, pyas_partial *, int64_t, hipStream_t);
 #define PYAS_INSTANTIATE_PART2(T)                                                              \
     template hipError_t launch_axes_dense_t<T>(const AxesArgs &, bool, int64_t, hipStream_t);
 #define PYAS_INSTANTIATE_PART3(T)                                                              \

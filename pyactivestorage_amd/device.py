@@ -92,11 +92,26 @@ class Context:
         h = ctypes.c_void_p()
         _lib.check(self.lib.pyas_ctx_create(self.device, ctypes.byref(h)), "pyas_ctx_create")
         self.handle = h.value
+        self._set_tie_rules()
         self._tls = threading.local()
         self._stats_lock = threading.Lock()
         self.live_streams = 0        # per-thread streams currently alive
         self.pinned_bytes = 0        # per-thread pinned staging currently alive
         self._coalescer = None
+
+    def _set_tie_rules(self):
+        """NumPy's zero-sign tie rule of this host for f32/f64 (zerosign.py),
+        so the device returns the same +0.0/-0.0 as storage.py:99-100."""
+        from .zerosign import tie_rule
+        for code, dt in ((_lib.F32, "f4"), (_lib.F64, "f8")):
+            rule = tie_rule(dt)
+            if rule is None:
+                continue
+            r = _lib.TieRule()
+            r.lanes, r.piece = rule.lanes, rule.piece
+            for lane, rank in enumerate(rule.rank):
+                r.rank[lane] = rank
+            _lib.check(self.lib.pyas_ctx_set_tie_rule(self.handle, code, ctypes.byref(r)), "set_tie_rule")
 
     def _count(self, streams=0, pinned=0):
         with self._stats_lock:

@@ -86,6 +86,30 @@ def reduce_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, chunk_out_pt
                "pyas_reduce_chunks")
 
 
+def zero_sign_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, which: int, partials_ptr,
+                     stream) -> bool:
+    """NumPy's sign of each chunk's zero min (which & 1) / max (which & 2)
+    (pyas_zero_sign_chunks); False when a chunk is too large for the table
+    (the sign is then the reduction's own)."""
+    rc = ctx.lib.pyas_zero_sign_chunks(ctx.handle, ctypes.byref(batch), ctypes.byref(mask), int(which),
+                                       partials_ptr, stream)
+    if rc == _lib.ENOTSUP:
+        return False
+    _lib.check(rc, "pyas_zero_sign_chunks")
+    return True
+
+
+def zero_sign_seq(ctx: Context, dt, partials_ptr, n, which: int, total_ptr, stream) -> bool:
+    """NumPy's sign of the combined zero min/max over per-chunk partials in
+    the reference's `out` order (pyas_zero_sign_seq)."""
+    rc = ctx.lib.pyas_zero_sign_seq(ctx.handle, dtype_code(dt), partials_ptr, int(n), int(which), total_ptr,
+                                    stream)
+    if rc == _lib.ENOTSUP:
+        return False
+    _lib.check(rc, "pyas_zero_sign_seq")
+    return True
+
+
 def reduce_axes(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, axes_mask: int, out_offsets_ptr,
                 out_ptr, stream) -> None:
     _lib.check(ctx.lib.pyas_reduce_axes(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),

@@ -498,6 +498,8 @@ def reduce_chunk_bytes(raw, compression, filters, missing, dtype, shape, order,
     if len(axes) == len(cs.shape):
         out = ctx.thread_buffer("out", _lib.PARTIAL_NBYTES)
         engine.reduce_chunks(ctx, batch, mup.struct, out.ptr, None, False, st)
+        if kind in ("min", "max"):   # NumPy's +0.0/-0.0 when the extreme is zero
+            engine.zero_sign_chunks(ctx, batch, mup.struct, 1 if kind == "min" else 2, out.ptr, st)
         host = np.zeros(1, dtype=pdt)
         ctx.d2h(host, out.ptr, st)
         ctx.synchronize(st)

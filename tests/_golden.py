@@ -49,6 +49,21 @@ def cases():
 
 
 @functools.lru_cache(maxsize=1)
+def signs_comparable() -> bool:
+    """Whether this host's NumPy breaks zero ties as the NumPy that made
+    the golden vectors (zerosign.py): then a zero min/max must match its
+    sign bit too (the device follows the host's rule)."""
+    from pyactivestorage_amd.zerosign import tie_rule
+    with open(os.path.join(HERE, "reference_cases.json")) as f:
+        rec = json.load(f).get("tie_rule", {})
+    for dt in ("f4", "f8"):
+        r = tie_rule(dt)
+        if r is None or dt not in rec or rec[dt] != {"lanes": r.lanes, "order": r.order, "piece": r.piece}:
+            return False
+    return True
+
+
+@functools.lru_cache(maxsize=1)
 def arrays():
     return dict(np.load(os.path.join(HERE, "reference_outputs.npz")))
 
@@ -106,6 +121,9 @@ def check(i, tmp, n, rel=1e-6):
         assert ok.all(), (i, gd, wd)
     else:
         assert np.array_equal(gd, wd, equal_nan=wd.dtype.kind == "f"), (i, gd, wd)
+        if wd.dtype.kind == "f" and signs_comparable():   # +0.0 vs -0.0 (storage.py:99-100)
+            z = wd == 0
+            assert np.array_equal(np.signbit(gd[z]), np.signbit(wd[z])), (i, "zero sign", gd[z], wd[z])
     if count is None:
         assert n is None, i
     else:
@@ -115,8 +133,9 @@ def check(i, tmp, n, rel=1e-6):
 def check_gpu(i, tmp, n, a, reduce_bytes):
     """:func:`check` at 1e-6 relative; float sums/means that cancel may
     instead sit within 4e-7 * sum|x| of the reference (NumPy's pairwise f32
-    error bound, tests/_compare.py).  Returns True when case i needed that
-    fallback (the caller reports how many did)."""
+    error bound, tests/_compare.py) -- only where the sum really cancels
+    (|sum| < sum|x| / 2): a non-cancelling sum is held to 1e-6.  Returns
+    True when case i needed that fallback (the caller reports how many did)."""
     try:
         check(i, tmp, n, rel=1e-6)
         return False
@@ -133,7 +152,8 @@ def check_gpu(i, tmp, n, a, reduce_bytes):
     w = data.astype(np.float64)[~mask]
     s = np.broadcast_to(np.ma.filled(scale, 0), mask.shape)[~mask]
     with np.errstate(invalid="ignore"):
-        ok = (np.isnan(g) & np.isnan(w)) | (np.abs(g - w) <= np.maximum(1e-6 * np.abs(w), 4e-7 * s))
+        strict = (np.isnan(g) & np.isnan(w)) | (np.abs(g - w) <= 1e-6 * np.abs(w))
+        ok = strict | ((np.abs(g - w) <= 4e-7 * s) & (np.abs(w) < 0.5 * s))
     assert ok.all(), (i, g, w)
     assert np.array_equal(np.ma.getmaskarray(tmp), mask) and np.array_equal(n, count), i
     return True

@@ -18,6 +18,7 @@ import io
 import json
 import os
 import sys
+import tempfile
 import types
 
 import numpy as np
@@ -125,18 +126,21 @@ def codecs(spec):
 
 
 def run_case(ref, raw, case):
+    """The reference's own ``reduce_chunk`` (storage.py:8-104) on `raw`
+    written to a temporary file, called as active.py:765-776 calls it."""
     comp, filters = codecs(case["codecs"])
     missing = tuple(dec_value(v) for v in case["missing"])
-    with contextlib.redirect_stdout(io.StringIO()):  # storage.py:44 prints per chunk
-        chunk = ref.filter_pipeline(raw, comp, filters)
-        chunk = np.frombuffer(memoryview(chunk), "u1") if not isinstance(chunk, np.ndarray) else chunk
-        chunk = chunk.view(case["dtype"]).reshape(-1, order="A").reshape(case["shape"], order=case["order"])
-        tmp = ref.mask_missing(chunk[dec_sel(case["sel"])], missing)
-        method = METHODS[case["method"]]
-        axis = tuple(case["axis"]) if case["axis"] is not None else None
-        if method is None:
-            return tmp, None
-        return method(tmp, axis=axis, keepdims=True), np.ma.count(tmp, axis=axis, keepdims=True)
+    axis = tuple(case["axis"]) if case["axis"] is not None else None
+    fd, path = tempfile.mkstemp(suffix=".chunk")
+    try:
+        with os.fdopen(fd, "wb") as f:
+            f.write(raw)
+        with contextlib.redirect_stdout(io.StringIO()):  # storage.py:44 prints per chunk
+            return ref.reduce_chunk(path, 0, len(raw), comp, filters, missing, np.dtype(case["dtype"]),
+                                    tuple(case["shape"]), case["order"], dec_sel(case["sel"]), axis,
+                                    method=METHODS[case["method"]])
+    finally:
+        os.unlink(path)
 
 
 def describe(out):
@@ -252,9 +256,49 @@ def main():
                             axis=axis, method=meth, missing=miss,
                             codecs={"shuffle": es} if shuffle and es > 1 else {})
 
+    # 4. zero extremes with both signed zeros (storage.py:99-100 np.ma.min/max
+    #    and np.min/max): NumPy's sign of a zero min/max follows its reduction
+    #    loop (pyactivestorage_amd/zerosign.py).  Data >= 0 (min is a zero),
+    #    <= 0 (max is a zero), and all zeros; > np.getbufsize() elements so
+    #    the iterator's piece boundary is crossed; masked (the filled copy
+    #    NumPy reduces is contiguous) and unmasked whole-chunk selections.
+    zshape = (6, 10, 160)
+    for dt in ("<f4", ">f4", "<f8", ">f8"):
+        ndt = np.dtype(dt)
+        for pattern in ("min0", "max0", "zeros"):
+            n = int(np.prod(zshape))
+            if pattern == "zeros":
+                arr = np.zeros(n, dtype=ndt)
+            else:
+                arr = rng.uniform(0.5, 400.0, n).astype(ndt) * (1 if pattern == "min0" else -1)
+            pos = rng.choice(n, 40, replace=False)
+            arr[pos] = np.where(rng.random(40) < 0.5, -0.0, 0.0)
+            arr[rng.choice(n, 30, replace=False)] = -999.0
+            arr[0] = -0.0 if pattern != "max0" else 0.0
+            arr = arr.reshape(zshape)
+            for shuffle in ((False, True) if dt == "<f4" else (False,)):
+                es = ndt.itemsize
+                raw = arr.tobytes()
+                if shuffle:
+                    raw = np.frombuffer(raw, dtype=np.uint8).reshape(-1, es).T.reshape(-1).tobytes()
+                for miss in ([None, None, None, None], [-999.0, None, None, None], [None, -999.0, -1.0, 1e6],
+                             [-999.0, None, -500.0, 500.0]):
+                    sels = [(slice(None),) * 3]
+                    if miss[0] is not None or miss[1] is not None:
+                        sels.append((slice(1, 6), slice(2, 9), slice(3, 150, 2)))   # masked: filled copy
+                    for sel in sels:
+                        for meth in ("ma.min", "ma.max", "min", "max"):
+                            add(raw, source="zero-sign", dtype=dt, shape=list(zshape), order="C", sel=sel,
+                                axis=[0, 1, 2], method=meth, missing=miss,
+                                codecs={"shuffle": es} if shuffle else {})
+
+    sys.path.insert(0, ROOT)
+    from pyactivestorage_amd.zerosign import tie_rule
+    rules = {dt: {"lanes": r.lanes, "order": r.order, "piece": r.piece}
+             for dt, r in (("f4", tie_rule("f4")), ("f8", tie_rule("f8"))) if r is not None}
     with open(os.path.join(HERE, "reference_cases.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "reference": REF_STORAGE,
-                   "numpy": np.__version__, "cases": cases}, f)
+                   "numpy": np.__version__, "tie_rule": rules, "cases": cases}, f)
     np.savez_compressed(os.path.join(HERE, "reference_outputs.npz"), **arrays)
     print(f"wrote {len(cases)} cases")
 

@@ -6,7 +6,8 @@ reference's ``activestorage/storage.py`` on the reference's own test inputs
 every chunk of test1.nc with zlib+shuffle, cesm2 chunks) and on a synthetic
 sweep — is replayed through the HIP drop-in ``reduce_chunk_bytes``.  Same
 container type, dtype, shape, nomask-ness, mask and count; values bit-exact
-except float sums/means (<= 1e-6 relative).  Cases where the reference
+(a zero min/max down to its sign bit) except float sums/means (<= 1e-6
+relative; cancelling sums within 4e-7 * sum|x|, counted and reported).  Cases where the reference
 raises must raise the same exception type.
 """
 import numpy as np
@@ -18,7 +19,10 @@ from tests import _golden as G
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("block", range(0, 3205, 400))
+FALLBACKS = []
+
+
+@pytest.mark.parametrize("block", range(0, len(G.cases()), 400))
 def test_gpu_reproduces_reference_outputs(gpu, block):
     cases = G.cases()
     for i in range(block, min(block + 400, len(cases))):
@@ -33,4 +37,15 @@ def test_gpu_reproduces_reference_outputs(gpu, block):
             assert type(ei.value).__name__ == exp[0], (i, G.cases()[i], ei.value)
             continue
         tmp, n = call()
-        G.check_gpu(i, tmp, n, a, pas.reduce_chunk_bytes)
+        if G.check_gpu(i, tmp, n, a, pas.reduce_chunk_bytes):
+            FALLBACKS.append(i)
+
+
+def test_report_cancelling_sum_fallbacks(gpu):
+    """How many float sum/mean cases sat outside 1e-6 relative but within
+    4e-7 * sum|x| (cancelling sums only; see tests/_golden.py check_gpu)."""
+    n_float_sums = sum(1 for c in G.cases() if "raises" not in c and c["dtype"].lstrip("<>=|")[0] == "f"
+                       and c["method"] in ("ma.sum", "sum", "ma.mean", "mean"))
+    print(f"\ngolden float sum/mean cases: {n_float_sums}; needing the cancelling-sum bound: "
+          f"{len(FALLBACKS)} {FALLBACKS}; zero min/max sign bits compared: {G.signs_comparable()}")
+    assert len(FALLBACKS) <= n_float_sums

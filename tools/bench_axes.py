@@ -24,7 +24,10 @@ def main():
     ctx = get_context(0)
     st = torch.cuda.current_stream().cuda_stream
     shape, chunks = (1024, 1024, 1024), (64, 64, 64)
-    shuffled = "--shuffle" in sys.argv   # chunks stored HDF5-byte-shuffled (the generic kernel's path)
+    shuffled = "--shuffle" in sys.argv   # chunks stored HDF5-byte-shuffled
+    for k, arg in enumerate(sys.argv):     # --fold-blocks N: workgroup floor of the in-kernel fold
+        if arg == "--fold-blocks":
+            ctx.set_fold_min_blocks(int(sys.argv[k + 1]))
     data, offsets, _ = chunk_major_device(torch, shape, chunks, np.float32, dev, fill=-999.0, fill_frac=0.01,
                                           shuffle=shuffled)
     missing = (np.float32(-999.0), None, np.float32(1000.0), np.float32(5e8))
@@ -34,6 +37,21 @@ def main():
                          shuffle=4 if shuffled else 0)
     nbytes = data.numel()
     res = {}
+    reps = 20
+
+    def timed(fn):
+        """Median and min of `reps` launches, each timed with HIP events on
+        the launch stream (torch's current stream)."""
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            ts.append((e0, e1))
+        torch.cuda.synchronize()
+        ms = sorted(a.elapsed_time(b) for a, b in ts)
+        return ms[len(ms) // 2] * 1e-3, ms[0] * 1e-3
     if "--fold" in sys.argv:
         grid_n = [s // c for s, c in zip(shape, chunks)]
         for axes in ((0,), (1,), (2,), (0, 1), (1, 2), (0, 2)):
@@ -50,14 +68,10 @@ def main():
             except NotImplementedError as exc:
                 res[str(axes)] = {"refused": str(exc)}
                 continue
-            torch.cuda.synchronize()
-            reps = 5
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                engine.reduce_axes_grid(ctx, plan.batch, plan.mask_up.struct, g, fin.ptr, True, st)
-            torch.cuda.synchronize()
-            dt = (time.perf_counter() - t0) / reps
-            res[str(axes)] = {"ms": round(dt * 1e3, 3), "GBps": round(nbytes / dt / 1e9, 1), "outputs": n_final}
+            dt, dmin = timed(lambda: engine.reduce_axes_grid(ctx, plan.batch, plan.mask_up.struct, g, fin.ptr,
+                                                            True, st))
+            res[str(axes)] = {"ms": round(dt * 1e3, 3), "ms_min": round(dmin * 1e3, 3),
+                              "GBps": round(nbytes / dt / 1e9, 1), "outputs": n_final}
             del fin
         print(json.dumps({"workload": "c3 box query, chunk layers folded in-kernel (pyas_reduce_axes_grid)"
                           + (", byte-shuffled chunks" if shuffled else ""), "results": res}))
@@ -71,15 +85,10 @@ def main():
             mask |= 1 << a
         for _ in range(2):
             engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, mask, offs.data_ptr(), out.ptr, st)
-        torch.cuda.synchronize()
-        reps = 5
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, mask, offs.data_ptr(), out.ptr, st)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / reps
-        res[str(axes)] = {"ms": round(dt * 1e3, 3), "GBps": round(nbytes / dt / 1e9, 1),
-                          "outputs_per_chunk": n_out}
+        dt, dmin = timed(lambda: engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, mask,
+                                                    offs.data_ptr(), out.ptr, st))
+        res[str(axes)] = {"ms": round(dt * 1e3, 3), "ms_min": round(dmin * 1e3, 3),
+                          "GBps": round(nbytes / dt / 1e9, 1), "outputs_per_chunk": n_out}
         del out
     print(json.dumps({"workload": "c3 partial-axis per-chunk reduce_axes" + (", byte-shuffled chunks" if shuffled else ""),
                       "results": res}))
