@@ -1292,6 +1292,81 @@ __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base
     }
 }
 
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Shuffled column layout in load units (ES >= 4): the G = ES lanes of an
+// item group (consecutive items of one kept run) each load ONE unit -- 16
+// elements = G vectors, one 16-B piece from each byte plane -- of a
+// different row, and exchange them through the wave's LDS area (a G x G
+// transpose, row stride 65 vectors: conflict-free writes and reads), after
+// which each lane holds its own item's vectors for G rows, consumed in row
+// order like col_rows' steps.  A wave's plane loads are then 16 B per lane
+// (up to 1 KiB per plane per instruction) instead of N-byte pieces, which
+// fetched half cache lines.  col_units_ok() is the block-uniform guard;
+// `xch` holds kBlock / kWave * G * 65 vectors.
+template <typename T>
+__device__ __forceinline__ bool col_units_ok(const AxesDense &d) {
+    constexpr int ES = sizeof(T), N = 16 / ES, G = ES;
+    if constexpr (ES < 4) {
+        return false;
+    } else {
+        const int64_t R = d.RO * d.RI;
+        return d.it % G == 0 && (d.KI / N) % G == 0 && R % d.split == 0 && (R / d.split) % G == 0;
+    }
+}
+template <typename T>
+constexpr int col_units_lds() { return (kBlock / kWave) * (int)sizeof(T) * 65; }   // vectors
+
+template <typename T, bool BSWAP, int MASKED>
+__device__ void col_rows_units(const AxesDense &d, const uint8_t *base, int64_t n, int64_t i, int sp,
+                               const MaskT<T> &mk, TileAcc<T> *acc, uint4 *xch) {
+    constexpr int ES = sizeof(T), N = 16 / ES, G = ES;
+    const int S = d.split;
+    const int lane = threadIdx.x & (kWave - 1), j = lane & (G - 1), gl = lane - j;
+    const int64_t KIV = d.KI / N, R = d.RO * d.RI;
+    const int64_t gi = i - j;                       // the group's first item
+    const int64_t ko = gi / KIV, v = gi - ko * KIV;
+    const int64_t SG = (int64_t)S * G;              // a lane's row step
+    const int64_t sRO = d.KO * d.RI * d.KI;
+    const int64_t dq = SG / d.RI, dr = SG - dq * d.RI;
+    const int64_t step_off = (dq * sRO + dr * d.KI) * ES, wrap_off = (sRO - d.RI * d.KI) * ES;
+    const int64_t r0 = sp + (int64_t)j * S;         // this lane's first row
+    int64_t ro = r0 / d.RI, ri = r0 - ro * d.RI;
+    const uint8_t *p = base + ((ro * d.KO + ko) * d.RI * d.KI + ri * d.KI + v * N) * ES;
+    const int64_t steps = R / SG;
+    uint4 *wx = xch + (threadIdx.x / kWave) * (G * 65);
+    auto adv = [&]() {
+        p += step_off;
+        ri += dr;
+        if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
+    };
+    uint4 nx[G];   // the next step's unit is in flight while this one is consumed
+    if (steps > 0) { ldu<T, true, true>(base, p, n, nx); adv(); }
+    for (int64_t t = 0; t < steps; ++t) {
+        uint4 u[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) u[k] = nx[k];
+        if (t + 1 < steps) { ldu<T, true, true>(base, p, n, nx); adv(); }
+        // u[k]: row t*G + j of item gi + k  ->  area[j][gl + k]
+#pragma unroll
+        for (int k = 0; k < G; ++k) wx[j * 65 + gl + k] = u[k];
+        wave_sync_lds();
+        uint4 w[G];
+#pragma unroll
+        for (int r = 0; r < G; ++r) w[r] = wx[r * 65 + lane];
+        wave_sync_lds();
+        col_consume<T, BSWAP, MASKED, G>(w, acc, mk);
+    }
+    if constexpr (!MASKED) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k].count += (uint32_t)(R / S);
+    }
+}
+
 template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL>
 __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                           const MaskT<T> &mk, uint4 *stage) {
@@ -1301,13 +1376,22 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     const int il = threadIdx.x & (IT - 1), sp = threadIdx.x / IT;
     const int64_t items = d.KO * (d.KI / N);
     pyas_partial *out = a.out + a.out_offsets[c];
+    const bool units = SHUF && AL && col_units_ok<T>(d) && ldu_aligned<T, SHUF>(base, a.r.chunk_elems);
     for (int64_t i0 = j * IT; i0 < items; i0 += d.bpc * IT) {   // block-uniform
         const int64_t i = i0 + il;
         TileAcc<T> acc[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) acc[k].init();
-        if (i < items && sp < S && sp < d.RO * d.RI)
+        if constexpr (SHUF && sizeof(T) >= 4) {
+            if (units) {
+                if (i < items && sp < S) col_rows_units<T, BSWAP, MASKED>(d, base, a.r.chunk_elems, i, sp, mk, acc, stage);
+                __syncthreads();   // the exchange area is reused below
+            } else if (i < items && sp < S && sp < d.RO * d.RI) {
+                col_rows<T, SHUF, BSWAP, MASKED, AL>(d, base, a.r.chunk_elems, i, sp, mk, acc);
+            }
+        } else if (i < items && sp < S && sp < d.RO * d.RI) {
             col_rows<T, SHUF, BSWAP, MASKED, AL>(d, base, a.r.chunk_elems, i, sp, mk, acc);
+        }
         if constexpr (N <= 4) {
             // Stage the pass's IT*N partials (<= 32 KiB) in LDS, then write
             // them as consecutive 16-B stores (a lane's own N partials are
@@ -1427,11 +1511,6 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
 // the current tile is folded.
 constexpr int kRowLdsStride = 17;   // 16-B vectors per LDS run (V <= 16, + 1 pad)
 
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int H>
 __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
@@ -1512,7 +1591,8 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
     const bool al = MODE == 1 ? ldv_aligned<T, SHUF>(base, r.chunk_elems) : ldu_aligned<T, SHUF>(base, r.chunk_elems);
     if constexpr (MODE == 1) {
         // staging for coalesced partial stores (dense_col, N <= 4): 32 KiB
-        __shared__ uint4 stage[sizeof(T) >= 4 ? kBlock * 4 * 2 : 1];
+        // (also the shuffled unit exchange area: col_units_lds <= 2080 vectors)
+        __shared__ uint4 stage[sizeof(T) >= 4 ? (kBlock * 8 > col_units_lds<T>() ? kBlock * 8 : col_units_lds<T>()) : 1];
         if (al) dense_col<T, SHUF, BSWAP, MASKED, true>(a, c, j, base, mk, stage);
         else dense_col<T, SHUF, BSWAP, MASKED, false>(a, c, j, base, mk, stage);
     } else if constexpr (MODE >= 4) {
@@ -1581,7 +1661,11 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes
     const int il = threadIdx.x & (IT - 1), sp = threadIdx.x / IT;
     const int64_t items = d.KO * (d.KI / N);
     const bool round = (g.flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
-    __shared__ __attribute__((aligned(16))) uint8_t fold_lds[fold_lds_bytes<T, N>()];
+    // split-fold area; for shuffled chunks also the unit exchange area
+    // (col_rows_units), the two separated by barriers
+    constexpr int kFoldLds = fold_lds_bytes<T, N>() > col_units_lds<T>() * 16 ? fold_lds_bytes<T, N>()
+                                                                               : col_units_lds<T>() * 16;
+    __shared__ __attribute__((aligned(16))) uint8_t fold_lds[kFoldLds];
     auto layer_base = [&](int64_t l) {
         int64_t n = nk, rr = l;
 #pragma unroll
@@ -1602,6 +1686,12 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes
     const int64_t R = d.RO * d.RI;
     bool pipe = R % S == 0 && (R / S) % U == 0;
     for (int64_t l = 0; pipe && l < g.n_layers; ++l) pipe = ldv_aligned<T, SHUF>(layer_base(l), r.chunk_elems);
+    // shuffled chunks outside the pipelined walk: unit loads + LDS exchange
+    // per layer when the geometry admits it (measured on C3 (0,)/(1,): the
+    // pipelined dword-piece walk 0.78/0.90 ms, the unit exchange 0.80-0.82/
+    // 0.97-0.98 ms, so the pipeline wins where it applies)
+    bool units = SHUF && !pipe && col_units_ok<T>(d);
+    for (int64_t l = 0; units && l < g.n_layers; ++l) units = ldu_aligned<T, SHUF>(layer_base(l), r.chunk_elems);
     const int64_t KIV = d.KI / N, sRO = d.KO * d.RI * d.KI;
     const int64_t dq = S / d.RI, dr = S - dq * d.RI;
     const int64_t step_off = (dq * sRO + dr * d.KI) * ES, wrap_off = (sRO - d.RI * d.KI) * ES;
@@ -1670,7 +1760,14 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes
                 TileAcc<T> acc[N];
 #pragma unroll
                 for (int k = 0; k < N; ++k) acc[k].init();
-                if (act) {
+                if (units) {
+                    if constexpr (SHUF && sizeof(T) >= 4) {
+                        if (act)
+                            col_rows_units<T, BSWAP, MASKED>(d, base, r.chunk_elems, i, sp, mk, acc,
+                                                             reinterpret_cast<uint4 *>(fold_lds));
+                    }
+                    __syncthreads();   // the exchange area is the split-fold area
+                } else if (act) {
                     if (ldv_aligned<T, SHUF>(base, r.chunk_elems))
                         col_rows<T, SHUF, BSWAP, MASKED, true>(d, base, r.chunk_elems, i, sp, mk, acc);
                     else
