@@ -15,8 +15,9 @@ The lane count and the lane tree depend on the SIMD target NumPy dispatches
 on the host CPU (AVX512: 16 float32 / 8 float64 lanes; AVX2 has fewer), so
 the rule is not hard-coded: :func:`tie_rule` derives it from NumPy itself
 on this host (a few tiny ``np.min`` calls) and checks it on random data
-before the device uses it.  The device then reproduces the sign
-(``pyas_zero_sign_fixup``): ``tests/test_zero_sign.py`` pins the derived
+before the device uses it.  The device then reproduces the sign per chunk
+(``pyas_zero_sign_chunks``) and across the chunk sequence
+(``pyas_zero_sign_seq``):``tests/test_zero_sign.py`` pins the derived
 rule against NumPy and ``tests/test_gpu_zero_sign.py`` the device result.
 """
 from __future__ import annotations
