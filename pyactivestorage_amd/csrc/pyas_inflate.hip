@@ -7,18 +7,22 @@
 // chunk of a query, so thousands of streams decode concurrently.
 //
 // Per wave:
-//   * input: 128 dwords of the stream held lane-distributed in two VGPRs and
-//     read with v_readlane (no per-symbol memory access);
+//   * input: a 128-dword LDS ring refilled 64 dwords at a time from a block
+//     loaded one refill ahead, so the window's bits are two LDS dwords per
+//     lane and the symbol loop never waits on a global load;
 //   * Huffman decode: 10-bit literal/length and 8-bit distance lookup tables
 //     in LDS, canonical walk for longer codes;
-//   * output: the most recent 2^WBITS bytes (8-32 KiB) live in an LDS ring; a
-//     match is copied lane-parallel as out[p+i] = out[p-d+(i mod d)] (all
-//     sources precede p); the ring is flushed to HBM in coalesced 1 KiB
-//     pieces, and Adler-32 is folded in per flush with a wave reduction;
+//   * symbols: a speculative window -- every lane decodes the symbol that
+//     would start at its bit offset, one v_readlane per symbol walks the real
+//     chain, and the window's output bytes are produced lane-parallel (one
+//     lane per output byte, matches resolved by pointer jumping);
+//   * output: the most recent 2^WBITS bytes (8-32 KiB) live in an LDS ring,
+//     flushed to HBM in coalesced 1 KiB pieces with Adler-32 folded in per
+//     flush by a wave reduction;
 //   * a match reaching further back than the ring (d > 2^WBITS, up to
 //     DEFLATE's 32 KiB) reads the already-flushed output from HBM after the
 //     wave's stores have drained, with L1-bypassing (agent-scope) loads.
-//     A smaller ring is what buys occupancy: 2^13 B + tables ~= 12.5 KiB of
+//     A smaller ring is what buys occupancy: 2^13 B + tables ~= 12.7 KiB of
 //     LDS per wave -> 12 streams per CU instead of 4.
 // Error behaviour follows zlib's inflate(): bad header, preset dictionary,
 // invalid block type, stored-length mismatch, over-subscribed or incomplete
@@ -30,6 +34,7 @@ namespace pyas {
 namespace {
 
 constexpr int kLitBits = 10, kDistBits = 8;
+
 constexpr uint32_t kFlush = 1024;   // bytes per coalesced flush (16 per lane)
 
 __constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -57,43 +62,48 @@ struct Lds {
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Lane-distributed bit reader over dword-aligned input.
+// Bit reader over dword-aligned input, staged through a 128-dword LDS ring:
+// the wave's window bits come from two LDS dwords per lane (no readlanes, no
+// vector-memory wait in the symbol loop).  The ring is refilled 64 dwords at
+// a time from a block loaded into one VGPR per lane a refill earlier, so the
+// global load latency is off the decode path.
+constexpr uint32_t kInRing = 128, kInBlock = 64;
+
 struct BitIn {
     const uint32_t *w;
     uint32_t nwords;   // readable dwords from w
     uint32_t nbits;    // valid bits from w (stream end)
     uint32_t pos;      // bit position from w
-    uint32_t base;     // dword index held by lane 0 of cur
-    uint32_t cur, nxt;
+    uint32_t filled;   // dwords [filled - kInRing, filled) are in the ring
+    uint32_t stage;    // w[filled + lane], loaded ahead
+    uint32_t *ring;    // LDS
 
     __device__ __forceinline__ uint32_t load(uint32_t k) const {
         const uint32_t i = k + (threadIdx.x & 63);
         return i < nwords ? __builtin_nontemporal_load(w + i) : 0u;
     }
-    __device__ __forceinline__ void seek() {   // after a jump (stored blocks)
-        base = pos >> 5;
-        cur = load(base);
-        nxt = load(base + 64);
+    __device__ __forceinline__ void seek() {   // at the start and after stored blocks
+        filled = pos >> 5;
+        ring[(filled + (threadIdx.x & 63)) & (kInRing - 1)] = load(filled);
+        filled += kInBlock;
+        stage = load(filled);
     }
-    __device__ __forceinline__ uint32_t word(uint32_t k) const {
-        const uint32_t r = k - base;
-        return r < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)r)
-                      : (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)(r - 64));
-    }
-    // At least 32 valid bits starting at pos (LSB first).
-    __device__ __forceinline__ uint32_t peek() {
-        const uint32_t k = pos >> 5;
-        if (k >= base + 64) {
-            if (k >= base + 128) {
-                seek();
-            } else {
-                cur = nxt;
-                base += 64;
-                nxt = load(base + 64);
-            }
+    __device__ __forceinline__ void ensure() {
+        if ((pos >> 5) + 32u > filled) {
+            ring[(filled + (threadIdx.x & 63)) & (kInRing - 1)] = stage;
+            filled += kInBlock;
+            stage = load(filled);
         }
-        const uint64_t v = (uint64_t)word(k) | ((uint64_t)word(k + 1) << 32);
-        return uni((uint32_t)(v >> (pos & 31)));
+    }
+    // 32 bits at pos + off (LSB first), per lane
+    __device__ __forceinline__ uint32_t bits_at(uint32_t off) const {
+        const uint32_t t = pos + off, k = t >> 5;
+        return __builtin_amdgcn_alignbit(ring[(k + 1) & (kInRing - 1)], ring[k & (kInRing - 1)], t & 31);
+    }
+    // At least 32 valid bits starting at pos (uniform).
+    __device__ __forceinline__ uint32_t peek() {
+        ensure();
+        return uni(bits_at(0));
     }
 };
 
@@ -220,6 +230,45 @@ __device__ void flush(const uint8_t *win, Out &o, uint32_t n) {
 
 }  // namespace
 
+// Inclusive prefix sum over the wave: DPP shifts inside each 16-lane row,
+// then the row totals (lanes 15, 31, 47) added with three readlanes.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
+    const uint32_t row = (uint32_t)lane >> 4;
+    return x + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+}
+
+// LDS written by other lanes of this wave is read after this point (the
+// compiler may not forward a lane's own earlier store across it).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
+    const uint32_t row = (uint32_t)lane >> 4;
+    uint32_t c = row >= 1 ? r0 : 0u;
+    c = row >= 2 ? max(c, r1) : c;
+    c = row >= 3 ? max(c, r2) : c;
+    return max(x, c);
+}
+
 // Byte of already-flushed output, coherent with this wave's earlier stores.
 __device__ __forceinline__ uint32_t far_byte(const uint8_t *p) {
     const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)p & ~(uintptr_t)3);
@@ -227,8 +276,23 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *p) {
     return (v >> (((uintptr_t)p & 3) * 8)) & 255u;
 }
 
+// Phase timing (diagnostic build, -DPYAS_INFLATE_PROF): per-wave cycle sums
+// of the decode phases, printed for the first streams of a launch.
+#ifdef PYAS_INFLATE_PROF
+#define PYAS_PROF_INIT uint64_t pf_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}; uint64_t pf_last = clock64(); \
+                       uint64_t pf_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PYAS_STAT(i, v) (pf_st[i] += (v))
+#define PYAS_PROF(i) do { const uint64_t pf_n = clock64(); pf_acc[i] += pf_n - pf_last; pf_last = pf_n; \
+                          if ((i) == 0) pf_acc[8]++; } while (0)
+#else
+#define PYAS_PROF_INIT
+#define PYAS_PROF(i) do { } while (0)
+#define PYAS_STAT(i, v) ((void)0)
+#endif
+
 template <int WBITS>
 __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
+    PYAS_PROF_INIT
     constexpr uint32_t kWin = 1u << WBITS, kWinMask = kWin - 1;
     static_assert(kWin >= 4096, "ring must exceed the unflushed bytes plus one match");
     __shared__ Lds L;
@@ -238,7 +302,10 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
     const uint8_t *src = x.src + x.src_offsets[c];
     const int64_t n_in = x.src_sizes[c];
     const uint32_t mis = (uint32_t)((uintptr_t)src & 3);
+    __shared__ uint32_t in_ring[kInRing];
+    __shared__ uint8_t mark[64];              // symbol starts of one 64-byte output step
     BitIn in;
+    in.ring = in_ring;
     in.w = reinterpret_cast<const uint32_t *>(src - mis);
     in.nbits = (uint32_t)((n_in + mis) * 8);
     in.nwords = (uint32_t)((n_in + mis + 3) / 4);
@@ -278,11 +345,29 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
             if ((len ^ 0xffffu) != nlen) { status = PYAS_INFLATE_BAD_STORED; break; }
             if (in.pos + len * 8 > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
             if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
-            const uint8_t *bytes = reinterpret_cast<const uint8_t *>(in.w) + (in.pos >> 3);
+            // 16 bytes per lane per 1 KiB step: five independent dword loads
+            // (the stream is dword-aligned at in.w), realigned with alignbyte
+            const uint32_t byte0 = in.pos >> 3;
             for (uint32_t done = 0; done < len;) {
                 while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
                 const uint32_t step = min(len - done, kFlush);
-                for (uint32_t i = lane; i < step; i += 64) win[(o.pos + i) & kWinMask] = bytes[done + i];
+                const uint32_t mine = (uint32_t)lane * 16u;
+                if (mine < step) {
+                    const uint32_t b = byte0 + done + mine;
+                    const uint32_t wi = b >> 2, sh = b & 3u;
+                    uint32_t dw[5];
+#pragma unroll
+                    for (uint32_t k = 0; k < 5; ++k)
+                        dw[k] = wi + k < in.nwords ? __builtin_nontemporal_load(in.w + wi + k) : 0u;
+                    const uint32_t n = min(step - mine, 16u);
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k) {
+                        const uint32_t q = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
+#pragma unroll
+                        for (uint32_t m = 0; m < 4; ++m)
+                            if (k * 4 + m < n) win[(o.pos + mine + k * 4 + m) & kWinMask] = (uint8_t)(q >> (8 * m));
+                    }
+                }
                 o.pos += step;
                 done += step;
                 __syncthreads();
@@ -438,31 +523,194 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
             copy_match(d, len);
             return 0;
         };
-        // Symbol loop.  Fast path: a speculative window.  Lane k holds the 32
-        // bits at pos + k and looks up both root tables there, in one LDS
-        // round trip for the whole wave; the symbol chain is then walked on
-        // the scalar unit with v_readlane (a symbol at window offset `off`
-        // is lane off's entry; its length extra bits come from lane off's
-        // bits, the distance code from lane off + l + le).  A code longer
-        // than its root table, or a length/distance pair that would start
-        // its distance past the window, drops to one_symbol / a new window.
+        // Symbol loop over speculative windows.  Lane k holds the 32 bits
+        // at pos + k and looks up both root tables there (one LDS round trip
+        // for the whole wave).
+        //
+        // Parallel walk (the common case): every lane decodes the symbol
+        // that WOULD start at its bit offset -- literal, or length plus the
+        // distance code read from lane k + l + le -- and its successor
+        // offset nxt.  Only the chain of successors from offset 0 is then
+        // walked on the scalar unit (one v_readlane per symbol); the chain's
+        // output offsets come from one wave prefix sum, its literals are
+        // written by their own lanes, and its matches are copied in order
+        // (literals between two matches are written before the later match
+        // reads the ring, as a serial decoder would).  A lane whose symbol
+        // cannot be finished inside the window ends the chain there: a code
+        // longer than its root table (one_symbol), end of block, or a
+        // distance code past the window (next window).  Anything else
+        // unusual -- an invalid symbol, truncated input, a distance before
+        // the output start, output past capacity -- sends the whole window
+        // to the serial walk below, which reports zlib's error at the right
+        // symbol.  At most kBudget output bytes per window keep the ring
+        // invariants of the serial decoder (unflushed bytes + window output
+        // fit the ring; a match source further back than the ring is
+        // already flushed to dst).
+        constexpr uint32_t kBudget = kWin / 4;
         bool eob = false;
+        uint32_t windows_left = in.nbits + 64u;   // every window consumes input; a stuck walk ends here
         while (!eob) {
-            in.peek();                                   // cur/nxt hold the window
-            const uint32_t k0 = in.pos >> 5, sh = in.pos & 31;
-            const uint32_t w0 = in.word(k0), w1 = in.word(k0 + 1), w2 = in.word(k0 + 2),
-                           w3 = in.word(k0 + 3);
-            const uint32_t t = sh + (uint32_t)lane;       // 0..94
-            const uint32_t wb = t >> 5;
-            const uint32_t lo = wb == 0 ? w0 : wb == 1 ? w1 : w2;
-            const uint32_t hi = wb == 0 ? w1 : wb == 1 ? w2 : w3;
-            const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (t & 31));
+            PYAS_PROF(7);
+            if (windows_left-- == 0u) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
+            while (o.pos - o.fpos >= kFlush) {
+                issue_pending();
+                flush<kWinMask>(win, o, kFlush);
+            }
+            PYAS_PROF(5);
+            in.ensure();                                 // the ring holds the window
+            const uint32_t v = in.bits_at((uint32_t)lane);
             const uint32_t E = lit[v & ((1u << kLitBits) - 1u)];
             const uint32_t D = dist[v & ((1u << kDistBits) - 1u)];
             auto rl = [](uint32_t x, uint32_t k) {
                 return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)k);
             };
-            uint32_t off = 0;
+            PYAS_PROF(0);
+
+            // ---- per-lane speculative symbol -------------------------------
+            enum : uint32_t { kLit = 0, kMatch = 1, kStop = 2 };
+            enum : uint32_t { rSlow = 1, rEob = 2, rNewWin = 3, rSerial = 4 };
+            const uint32_t l = E >> 9;
+            const uint32_t sym = E & 511u;
+            const uint32_t ls = sym - 257u;              // length symbol index (wraps for < 257)
+            const uint32_t le = (ls < 8u || ls == 28u) ? 0u : (ls - 4u) >> 2;
+            const uint32_t doff = (uint32_t)lane + l + le;
+            const uint32_t dsrc = doff < 64u ? doff : 63u;
+            const uint32_t f = (uint32_t)__shfl((int)D, (int)dsrc, 64);
+            const uint32_t vd = (uint32_t)__shfl((int)v, (int)dsrc, 64);
+            // every lane computes all fields; selects pick the symbol's kind
+            const uint32_t dl = f >> 9, ds = f & 511u;
+            const uint32_t lec = le < 5u ? le : 5u;
+            const uint32_t lbase = ls < 8u ? ls + 3u : ls == 28u ? 258u : ((4u + (ls & 3u)) << lec) + 3u;
+            const uint32_t de0 = ds < 4u ? 0u : (ds - 2u) >> 1;
+            const uint32_t de = de0 < 13u ? de0 : 13u;
+            const uint32_t dbase = ds < 4u ? ds + 1u : ((2u + (ds & 1u)) << de) + 1u;
+            const uint32_t mlen = lbase + ((v >> l) & ((1u << lec) - 1u));
+            const uint32_t mdist = dbase + ((vd >> dl) & ((1u << de) - 1u));
+            const bool trunc = in.pos + (uint32_t)lane > in.nbits;
+            const uint32_t why = trunc ? rSerial
+                               : !l ? rSlow
+                               : sym < 256u ? 0u
+                               : sym == 256u ? rEob
+                               : ls >= 29u ? rSerial
+                               : doff > 63u ? rNewWin
+                               : !dl ? rSlow
+                               : ds >= 30u ? rSerial : 0u;
+            const bool is_lit = why == 0u && sym < 256u;
+            const uint32_t kind = why ? kStop : is_lit ? kLit : kMatch;
+            const uint32_t olen = why ? 0u : is_lit ? 1u : mlen;
+            const uint32_t dd = mdist;
+            uint32_t nxt = is_lit ? (uint32_t)lane + l : doff + dl + de;
+            if (kind == kStop) nxt = 128u + why;         // >= 128: the chain stops here
+            PYAS_PROF(1);
+
+            // ---- the chain from offset 0 (scalar) --------------------------
+            uint64_t M = 0;
+            uint32_t off = 0, prev = 0, stop = 0;
+            do {
+                M |= 1ull << off;
+                prev = off;
+                off = rl(nxt, off);
+            } while (off < 64u);
+            if (off >= 128u) {                           // ended on a stop lane: not consumed
+                stop = off - 128u;
+                off = prev;
+                M &= ~(1ull << prev);
+            }
+            PYAS_PROF(2);
+            const bool on = (M >> lane) & 1ull;
+            const uint32_t incl = wave_incl_sum(on ? olen : 0u);   // output bytes up to this lane
+            const uint32_t excl = incl - (on ? olen : 0u);
+            uint32_t T = rl(incl, 63);
+            bool par = stop != rSerial || off > 0;
+            if (par && T > kBudget) {                    // end the window before the first symbol past it
+                const uint64_t over = __ballot(on && incl > kBudget);
+                const uint32_t cut = (uint32_t)__builtin_ctzll(over);
+                M &= (1ull << cut) - 1ull;
+                off = cut;
+                stop = 0;
+                T = rl(excl, cut);
+            }
+            const bool on2 = (M >> lane) & 1ull;
+            if (par) {
+                if (o.pos + T > o.cap) par = false;
+                if (__ballot(on2 && kind == kMatch && dd > o.pos + excl)) par = false;
+            }
+            PYAS_PROF(3);
+            if (par) {
+                issue_pending();
+                const uint32_t pos0 = o.pos;
+                uint64_t mm = __ballot(on2 && kind == kMatch);
+                PYAS_STAT(0, __builtin_popcountll(M));
+                PYAS_STAT(1, __builtin_popcountll(mm));
+                PYAS_STAT(2, __builtin_popcountll(__ballot(on2 && kind == kMatch && olen > 64u)));
+                PYAS_STAT(3, __builtin_popcountll(__ballot(on2 && kind == kMatch && dd < olen)));
+                PYAS_STAT(4, __builtin_popcountll(__ballot(on2 && kind == kMatch && dd < excl + 1u)));
+                PYAS_STAT(5, stop == rSlow ? 1u : 0u);
+                PYAS_STAT(6, T);
+                PYAS_STAT(7, __builtin_popcountll(__ballot(on2 && kind == kMatch && dd > kWin)));
+                (void)mm;
+                // The window's output, 64 positions per step, one per lane.
+                // Lane j takes position p = c + j: the symbol covering p is
+                // the last one starting at or before p (start marks in LDS,
+                // then a max scan).  A literal gives its byte.  A match byte
+                // p copies byte p - d: from the ring when p - d precedes this
+                // step (from dst when d exceeds the ring: those bytes are
+                // flushed), else from the lane producing p - d in this step;
+                // pointer jumping over those lanes ends at a lane whose byte
+                // is known (an overlapping match, d < len, chains this way).
+                const bool any_far = __ballot(on2 && kind == kMatch && dd > kWin) != 0;
+                if (any_far) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t pk = (kind << 16) | (sym & 255u);
+                uint32_t carry = 0;                      // lane + 1 of the symbol covering position c
+                for (uint32_t c = 0; c < T; c += 64) {
+                    const uint32_t p = c + (uint32_t)lane;
+                    mark[lane] = 0;
+                    if (on2 && excl >= c && excl < c + 64u) mark[excl - c] = (uint8_t)(lane + 1);
+                    wave_lds_sync();                     // other lanes' marks (no store forwarding)
+                    uint32_t S = wave_incl_max(mark[lane]);
+                    S = S > carry ? S : carry;
+                    carry = rl(S, 63);
+                    const uint32_t k = (S - 1u) & 63u;
+                    const uint32_t s_d = (uint32_t)__shfl((int)dd, (int)k, 64);
+                    const uint32_t s_pk = (uint32_t)__shfl((int)pk, (int)k, 64);
+                    const bool valid = p < T;
+                    const bool is_m = (s_pk >> 16) == kMatch;
+                    const int32_t src = (int32_t)p - (int32_t)s_d;   // window-relative source
+                    const bool inner = is_m && src >= (int32_t)c;
+                    uint32_t val = s_pk & 255u;
+                    if (valid && is_m && !inner)
+                        val = s_d > kWin ? far_byte(o.dst + (pos0 + src)) : (uint32_t)win[(pos0 + src) & kWinMask];
+                    if (__ballot(valid && inner)) {
+                        // pd = lane whose byte this lane copies | 64 once that
+                        // lane's byte is known (a root); undone lanes jump
+                        // to their target's pd until every lane has a root
+                        uint32_t pd = inner ? (uint32_t)(src - (int32_t)c) : ((uint32_t)lane | 64u);
+                        while (__ballot(!(pd & 64u))) {
+                            const uint32_t q = (uint32_t)__shfl((int)pd, (int)(pd & 63u), 64);
+                            if (!(pd & 64u)) pd = q;
+                        }
+                        val = (uint32_t)__shfl((int)val, (int)(pd & 63u), 64);
+                    }
+                    if (valid) win[(pos0 + p) & kWinMask] = (uint8_t)val;
+                    wave_lds_sync();
+                }
+                o.pos = pos0 + T;
+                in.pos += off;
+                if (stop == rEob) {
+                    in.pos += rl(l, off);
+                    eob = true;
+                } else if (stop == rSlow) {
+                    const int r = one_symbol();
+                    if (r == 2) break;
+                    if (r == 1) eob = true;
+                }
+                // rNewWin / rSerial past offset 0 / budget cut: next window
+                PYAS_PROF(4);
+                continue;
+            }
+
+            // ---- serial walk of the same window ----------------------------
+            off = 0;
             bool slow = false;
             for (;;) {
                 if (o.pos - o.fpos >= kFlush) {
@@ -472,36 +720,35 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
                 if (off > 63) break;
                 if (in.pos + off > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
                 const uint32_t e = rl(E, off);
-                const uint32_t l = e >> 9;
-                if (!l) { slow = true; break; }
-                uint32_t sym = e & 511u;
-                if (sym < 256) {
+                const uint32_t el = e >> 9;
+                if (!el) { slow = true; break; }
+                uint32_t es = e & 511u;
+                if (es < 256) {
                     if (o.pos >= o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
-                    if (lane == 0) win[o.pos & kWinMask] = (uint8_t)sym;
+                    if (lane == 0) win[o.pos & kWinMask] = (uint8_t)es;
                     o.pos++;
-                    off += l;
+                    off += el;
                     continue;
                 }
-                if (sym == 256) { off += l; eob = true; break; }
-                sym -= 257;
-                if (sym >= 29) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
-                // RFC 1951 3.2.5 length/distance bases, arithmetic form
-                const uint32_t le = (sym < 8 || sym == 28) ? 0u : (sym - 4u) >> 2;
-                const uint32_t lbase = sym < 8 ? sym + 3u : sym == 28 ? 258u : ((4u + (sym & 3u)) << le) + 3u;
-                const uint32_t doff = off + l + le;
-                if (doff > 63) break;                    // next window starts at this symbol
-                const uint32_t len = lbase + ((rl(v, off) >> l) & ((1u << le) - 1u));
-                const uint32_t f = rl(D, doff);
-                const uint32_t dl = f >> 9;
+                if (es == 256) { off += el; eob = true; break; }
+                es -= 257;
+                if (es >= 29) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
+                const uint32_t sle = (es < 8 || es == 28) ? 0u : (es - 4u) >> 2;
+                const uint32_t lbase = es < 8 ? es + 3u : es == 28 ? 258u : ((4u + (es & 3u)) << sle) + 3u;
+                const uint32_t sdoff = off + el + sle;
+                if (sdoff > 63) break;                   // next window starts at this symbol
+                const uint32_t len = lbase + ((rl(v, off) >> el) & ((1u << sle) - 1u));
+                const uint32_t sf = rl(D, sdoff);
+                const uint32_t dl = sf >> 9;
                 if (!dl) { slow = true; break; }         // long distance code
-                const uint32_t ds = f & 511u;
+                const uint32_t ds = sf & 511u;
                 if (ds >= 30) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
                 const uint32_t de = ds < 4 ? 0u : (ds - 2u) >> 1;
                 const uint32_t dbase = ds < 4 ? ds + 1u : ((2u + (ds & 1u)) << de) + 1u;
-                const uint32_t d = dbase + ((rl(v, doff) >> dl) & ((1u << de) - 1u));
+                const uint32_t d = dbase + ((rl(v, sdoff) >> dl) & ((1u << de) - 1u));
                 if (d > o.pos) { status = PYAS_INFLATE_BAD_DISTANCE; break; }
                 if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
-                off = doff + dl + de;
+                off = sdoff + dl + de;
                 start_match(d, len);
             }
             if (status) break;
@@ -512,6 +759,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
                 if (r == 2) break;
                 if (r == 1) eob = true;
             }
+            PYAS_PROF(6);
         }
         issue_pending();
         if (status) break;
@@ -533,6 +781,17 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
         x.status[c] = status;
         x.out_sizes[c] = o.pos;
     }
+#ifdef PYAS_INFLATE_PROF
+    PYAS_PROF(7);
+    if (c < 4 && lane == 0)
+    {
+        printf("inflate stream %d out %u windows %lu: setup %lu decode %lu walk %lu scan %lu write %lu flush %lu serial %lu other %lu\n",
+               (int)c, o.pos, pf_acc[8], pf_acc[0], pf_acc[1], pf_acc[2], pf_acc[3], pf_acc[4], pf_acc[5], pf_acc[6],
+               pf_acc[7]);
+        printf("inflate stream %d stats: symbols %lu matches %lu long %lu overlapping %lu src_in_window %lu slow %lu bytes %lu far %lu\n",
+               (int)c, pf_st[0], pf_st[1], pf_st[2], pf_st[3], pf_st[4], pf_st[5], pf_st[6], pf_st[7]);
+    }
+#endif
 }
 
 hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t stream) {

@@ -11,6 +11,7 @@ coalescer (``pyas_coalesced_reduce``) and holds no per-thread device state.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 import weakref
 
@@ -93,6 +94,10 @@ class Context:
         _lib.check(self.lib.pyas_ctx_create(self.device, ctypes.byref(h)), "pyas_ctx_create")
         self.handle = h.value
         self._set_tie_rules()
+        slots = os.environ.get("PYAS_INGEST_SLOTS")   # e.g. "64x16": 64 pinned slots of 16 MiB
+        if slots:
+            n, mib = (int(x) for x in slots.lower().split("x"))
+            _lib.check(self.lib.pyas_ctx_set_ingest_slots(self.handle, n, mib << 20), "pyas_ctx_set_ingest_slots")
         self._tls = threading.local()
         self._stats_lock = threading.Lock()
         self.live_streams = 0        # per-thread streams currently alive

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--wbits", type=int, default=13, help="LDS history ring (13-15)")
+    ap.add_argument("--no-check", action="store_true", help="timing experiments: skip status/output checks")
+    ap.add_argument("--sweep", default="", help="comma list of stream counts: per-stream rate vs streams in flight")
     args = ap.parse_args()
     import torch
     from pyactivestorage_amd.device import DeviceBuffer, get_context
@@ -57,11 +59,12 @@ def main():
     ib = InflateBatch(ctx, soffs, ssizes, np.arange(args.chunks, dtype=np.int64) * plain_n,
                       np.full(args.chunks, plain_n, dtype=np.int64))
     ib.launch(src.ptr, dst.ptr, st)
-    ib.check(st)
-    out = np.zeros(plain_n, dtype=np.uint8)
-    ctx.d2h(out, dst.ptr + (args.chunks - 1) * plain_n, st)
-    ctx.synchronize(st)
-    assert out.tobytes() == uniq[(args.chunks - 1) % len(uniq)][0]
+    if not args.no_check:
+        ib.check(st)
+        out = np.zeros(plain_n, dtype=np.uint8)
+        ctx.d2h(out, dst.ptr + (args.chunks - 1) * plain_n, st)
+        ctx.synchronize(st)
+        assert out.tobytes() == uniq[(args.chunks - 1) % len(uniq)][0]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     times = []
     for _ in range(args.reps):
@@ -76,6 +79,24 @@ def main():
     wall_ms = (time.perf_counter() - t0) * 1e3
     ms = float(np.median(times))
     total_plain = args.chunks * plain_n
+    sweep = {}
+    for n in [int(x) for x in args.sweep.split(",") if x]:
+        n = min(n, args.chunks)
+        sb = InflateBatch(ctx, soffs[:n], ssizes[:n], np.arange(n, dtype=np.int64) * plain_n,
+                          np.full(n, plain_n, dtype=np.int64))
+        sb.launch(src.ptr, dst.ptr, st)
+        if not args.no_check:
+            sb.check(st)
+        ts = []
+        for _ in range(args.reps):
+            e0.record(stream)
+            sb.launch(src.ptr, dst.ptr, st)
+            e1.record(stream)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        m = float(np.median(ts))
+        sweep[n] = {"ms": round(m, 3), "GBps": round(n * plain_n / m / 1e6, 2),
+                    "MBps_per_stream": round(plain_n / m / 1e3, 1)}
     # host zlib for context (bounded sample)
     sample = comps[: min(len(comps), 256)]
     t0 = time.perf_counter()
@@ -92,6 +113,7 @@ def main():
         "cpu_GBps_decompressed": round(len(sample) * plain_n / cpu_s / 1e9, 2),
         "cpu_threads": args.cpu_threads,
         "wbits": args.wbits,
+        "sweep": sweep,
     }))
 
 
