@@ -150,7 +150,7 @@ def _unhold(store) -> None:
 
 
 # read -> inflate pipeline stages of a compressed query (PYAS_INFLATE_GROUPS)
-_INFLATE_GROUPS = int(os.environ.get("PYAS_INFLATE_GROUPS", "4"))
+_INFLATE_GROUPS = int(os.environ.get("PYAS_INFLATE_GROUPS", "3"))
 
 
 def _pipeline_groups(sizes, n_groups):
@@ -458,14 +458,16 @@ class Active:
                 # as its copies land (inflate waves of every group can be
                 # resident together: one stream per wave, so concurrency is
                 # what buys inflate throughput), while the host reads on
-                padded = -(-fsize // 16) * 16
-                soffs = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
-                src = DeviceBuffer(ctx, max(int(padded.sum()), 16))
+                # compressed streams back to back (the inflater reads any
+                # alignment), so file-contiguous chunks stay one H2D copy per
+                # staging slot instead of one per chunk
+                soffs = np.concatenate([[0], np.cumsum(fsize)[:-1]]).astype(np.int64)
+                src = DeviceBuffer(ctx, int(fsize.sum()) + 16)
                 buf = dst if dst is not None else DeviceBuffer(ctx, max(n, 1) * stride)
                 copy_st = ctx.thread_aux_stream(0)
                 ctx.stream_wait(copy_st, st)      # order after prior work on st
                 batches = []
-                groups = _pipeline_groups(padded, _INFLATE_GROUPS)
+                groups = _pipeline_groups(fsize, _INFLATE_GROUPS)
                 for g, (lo, hi) in enumerate(groups):
                     read_ranges(ctx, ds.filename, foff[lo:hi], fsize[lo:hi], src.ptr, soffs[lo:hi],
                                 copy_st, self._max_threads)
