@@ -773,7 +773,19 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
     // n_cols x bpc: trade items per pass for splits of the reduced rows
     // until the launch fills the chip (>= 8 workgroups per CU by default).
     const int64_t min_blocks = ctx->fold_min_blocks;
-    if (x.d.mode >= 4) {   // LDS row layout: one output tile per wave
+    // Lean column fold (k_axes_fold_lean): the split-1 geometry the two-step
+    // path uses (so bit-identical), whole 4-row groups, and enough lanes in
+    // the grid that no split is needed (PYAS_FOLD_LEAN=0 turns it off).
+    const char *e_lean = getenv("PYAS_FOLD_LEAN");   // per call: tests and benches switch it
+    const bool lean_on = !e_lean || atoi(e_lean) != 0;
+    const int64_t lean_bpc =
+        x.d.mode == 1 ? (x.d.KO * (x.d.KI / (16 / es)) + pyas::kBlock - 1) / pyas::kBlock : 0;
+    if (lean_on && x.d.mode == 1 && x.d.split == 1 && (x.d.RO * x.d.RI) % 4 == 0 &&
+        fg.n_layers * x.d.RO * x.d.RI < (int64_t(1) << 31) &&   // per-lane uint32 counts
+        fg.n_cols * lean_bpc >= min_blocks / 2) {
+        fg.lean = 1;
+        x.d.bpc = lean_bpc;
+    } else if (x.d.mode >= 4) {   // LDS row layout: one output tile per wave
         const int64_t rpw = pyas::kWave / x.d.group, per_block = (pyas::kBlock / pyas::kWave) * rpw;
         x.d.bpc = (x.d.KO + per_block - 1) / per_block;
     } else {

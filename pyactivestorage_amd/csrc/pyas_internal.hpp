@@ -77,6 +77,7 @@ struct FoldGrid {
     int64_t ostride[PYAS_MAX_DIMS];   // final-output element strides (kept dims)
     int64_t n_layers, n_cols;         // chunks along the reduced dims / kept dims
     uint32_t flags;                   // PYAS_COMBINE_*
+    int32_t lean;                     // column layout: k_axes_fold_lean (split 1, rows % 4 == 0)
 };
 
 struct InflateArgs {

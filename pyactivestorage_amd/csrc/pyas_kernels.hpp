@@ -1802,6 +1802,182 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes
     }
 }
 
+#ifndef PYAS_LEAN_DEPTH
+#define PYAS_LEAN_DEPTH 2   // 4-row load groups in flight per lane (k_axes_fold_lean)
+#endif
+#ifndef PYAS_LEAN_WAVES
+#define PYAS_LEAN_WAVES 4   // occupancy floor: <= 128 VGPRs, 16 waves per CU
+#endif
+
+// One lane's row walk of k_axes_fold_lean over every layer of its column:
+// groups of 4 rows (the two-step path's PYAS_COL_U grouping, so the sums are
+// bit-identical), DEPTH groups of 16-B loads in flight while the oldest is
+// consumed.  The fetch cursor runs ahead of the consume cursor across layer
+// boundaries; a layer's partial is merged into w[] when its last group is
+// consumed (tile_store_lane + merge, as k_combine_grid would).
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, typename LB>
+__device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t off0, int64_t n_layers,
+                                          bool round, const MaskT<T> &mk, const LB &layer_base,
+                                          WAcc<T> *w) {
+    constexpr int N = 16 / sizeof(T), ES = sizeof(T), U = 4;
+    const int64_t R = d.RO * d.RI;                      // rows per layer, a multiple of U
+    const int64_t step = d.KI * ES;                     // next ri
+    const int64_t wrap = (d.KO * d.RI * d.KI - d.RI * d.KI) * ES;   // ri wrapped: next ro
+    const int64_t gpl = R / U, total = n_layers * gpl;  // groups per layer, in all
+    // fetch cursor
+    const uint8_t *fb = layer_base(0);
+    int64_t foff = off0, fl = 0;
+    int64_t fri = 0, fg = 0;
+    auto fetch = [&](uint4 *buf) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            buf[u] = ldv<T, SHUF, AL>(fb, fb + foff, n);
+            foff += step;
+            if (++fri == d.RI) { fri = 0; foff += wrap; }
+        }
+        if (++fg == gpl) {   // next layer (wave-uniform)
+            fg = 0;
+            if (++fl < n_layers) {
+                fb = layer_base(fl);
+                foff = off0;
+                fri = 0;
+            }
+        }
+    };
+    // acc[k]: the current layer's sum / min / max; its count and NaN flag run
+    // over every layer (merge adds counts, and a NaN layer min/max stays NaN
+    // through pmin/pmax).  A layer's sum is rounded and added to w[k].sum and
+    // its min/max folded into w[k] with merge's pmin/pmax, in layer order; an
+    // empty layer's +-inf (or integer extremes) leave w[k] unchanged, as
+    // merge's count > 0 guard does.  (Fewer live registers than a full
+    // TileAcc -> pyas_partial -> merge per layer, same results.)
+    TileAcc<T> acc[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) acc[k].init();
+    int64_t cg = 0;   // consumed groups of the current layer
+    auto consume = [&](const uint4 *buf) {
+        col_consume<T, BSWAP, MASKED, U>(buf, acc, mk);
+        if (++cg == gpl) {
+            cg = 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                if constexpr (!MASKED) acc[k].count += (uint32_t)R;
+                pyas_scalar s;
+                TT<T>::put_acc(s, acc[k].sum);
+                w[k].sum += sum_of<T>(s, round);
+                w[k].mn = pmin(w[k].mn, acc[k].mn);
+                w[k].mx = pmax(w[k].mx, acc[k].mx);
+                acc[k].sum = 0;
+                acc[k].mn = TT<T>::highest();
+                acc[k].mx = TT<T>::lowest();
+            }
+        }
+    };
+    uint4 buf[DEPTH][U];
+#pragma unroll
+    for (int s = 0; s < DEPTH; ++s)
+        if (s < total) fetch(buf[s]);
+    for (int64_t t = 0; t < total; t += DEPTH) {   // wave-uniform
+#pragma unroll
+        for (int s = 0; s < DEPTH; ++s) {
+            if (t + s < total) {
+                uint4 cur[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = buf[s][u];
+                if (t + s + DEPTH < total) fetch(buf[s]);
+                consume(cur);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        w[k].count = (int64_t)acc[k].count;   // host: n_layers * rows < 2^31
+        if constexpr (TT<T>::kind == 0) {
+            if (acc[k].nan) {
+                w[k].mn = (T)__builtin_nan("");
+                w[k].mx = w[k].mn;
+            }
+        }
+    }
+}
+
+// Whole-chunk box query, column layout, one lane per item and no split of
+// the reduced rows (dense_geometry's split == 1, rows per chunk a multiple
+// of 4): the lean form of k_axes_fold.  No LDS and no barriers; each lane
+// streams its item's rows through every layer of its column with
+// PYAS_LEAN_DEPTH x 4 loads in flight, and the kernel stays under 128 VGPRs
+// so 16 waves per CU are resident (k_axes_fold carries 146-173 VGPRs, 12
+// waves, and folds its split rows through LDS behind a barrier per layer).
+// Same arithmetic as k_axes_dense (split 1) + k_combine_grid: bit-identical.
+template <typename T, bool SHUF, bool BSWAP, int MASKED>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fold_lean(AxesArgs a, FoldGrid g) {
+    constexpr int N = 16 / sizeof(T), ES = sizeof(T);
+    const AxesDense &d = a.d;
+    const ReduceArgs &r = a.r;
+    const int64_t col = blockIdx.x / d.bpc;
+    const int64_t j = blockIdx.x - col * d.bpc;
+    const int64_t items = d.KO * (d.KI / N);
+    const int64_t i = j * kBlock + threadIdx.x;
+    if (i >= items) return;   // no barriers below
+    const uint32_t red = a.axes;
+    int64_t ac[PYAS_MAX_DIMS], gstride[PYAS_MAX_DIMS];
+    int64_t rest = col, st = 1, nk = 0;
+#pragma unroll
+    for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+        ac[dd] = 0;
+        gstride[dd] = st;
+        if (dd < r.ndim) {
+            st *= g.n_coords[dd];
+            if (!((red >> dd) & 1u)) {
+                const int64_t q = rest / g.n_coords[dd];
+                ac[dd] = rest - q * g.n_coords[dd];
+                rest = q;
+                nk += ac[dd] * gstride[dd];
+            }
+        }
+    }
+    auto layer_base = [&](int64_t l) {
+        int64_t cn = nk, rr = l;
+#pragma unroll
+        for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+            if (dd < r.ndim && ((red >> dd) & 1u)) {
+                const int64_t q = rr / g.n_coords[dd];
+                cn += (rr - q * g.n_coords[dd]) * gstride[dd];
+                rr = q;
+            }
+        }
+        return r.data + r.offsets[cn];
+    };
+    MaskT<T> mk;
+    mk.init(r.mask);
+    const bool round = (g.flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
+    const int64_t KIV = d.KI / N, ko = i / KIV, v = i - ko * KIV;
+    const int64_t off0 = (ko * d.RI * d.KI + v * N) * ES;   // row 0 of item i
+    bool al = true;   // block-uniform: every layer's plane pieces aligned
+    for (int64_t l = 0; al && l < g.n_layers; ++l) al = ldv_aligned<T, SHUF>(layer_base(l), r.chunk_elems);
+    WAcc<T> w[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) w[k].init();
+    if (al)
+        lean_walk<T, SHUF, BSWAP, MASKED, true, PYAS_LEAN_DEPTH>(d, r.chunk_elems, off0, g.n_layers, round, mk,
+                                                                layer_base, w);
+    else
+        lean_walk<T, SHUF, BSWAP, MASKED, false, 1>(d, r.chunk_elems, off0, g.n_layers, round, mk, layer_base, w);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        int64_t loc = i * N + k, f = 0;   // kept-dims index in the chunk -> final element
+#pragma unroll
+        for (int dd = PYAS_MAX_DIMS - 1; dd >= 0; --dd) {
+            if (dd < r.ndim && !((red >> dd) & 1u)) {
+                const int64_t q = loc / r.shape[dd];
+                f += (ac[dd] * r.shape[dd] + (loc - q * r.shape[dd])) * g.ostride[dd];
+                loc = q;
+            }
+        }
+        store_wpartial(a.out + f, w[k]);
+    }
+}
+
 // Whole-chunk box query, LDS row layout (modes 4/5/6), chunk layers folded
 // in the kernel (pyas_reduce_axes_grid).  Block (col, j), wave w owns the
 // output tiles j*4 + w, + 4*bpc, ... of kept-dims chunk column `col`; for
@@ -2315,10 +2491,29 @@ static void launch_fold_row(const AxesArgs &a, const FoldGrid &g, bool masked, d
 }
 
 template <typename T, bool SHUF>
-static void launch_fold_col(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
+static void launch_fold_lean(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
     const dim3 blk(kBlock);
     const int mm = mask_mode(a.r.mask, masked);
     if (a.bswap) {
+        if (mm) hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, true, kMaskAll>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, true, 0>), gr, blk, 0, st, a, g);
+    } else if (mm == kMaskRange) {
+        hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, kMaskRange>), gr, blk, 0, st, a, g);
+    } else if (mm == kMaskNoEq1) {
+        hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, kMaskNoEq1>), gr, blk, 0, st, a, g);
+    } else {
+        if (mm) hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, kMaskAll>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, 0>), gr, blk, 0, st, a, g);
+    }
+}
+
+template <typename T, bool SHUF>
+static void launch_fold_col(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
+    const dim3 blk(kBlock);
+    const int mm = mask_mode(a.r.mask, masked);
+    if (g.lean) {
+        launch_fold_lean<T, SHUF>(a, g, masked, gr, st);
+    } else if (a.bswap) {
         if (mm) hipLaunchKernelGGL((k_axes_fold<T, SHUF, true, kMaskAll>), gr, blk, 0, st, a, g);
         else hipLaunchKernelGGL((k_axes_fold<T, SHUF, true, 0>), gr, blk, 0, st, a, g);
     } else if (mm == kMaskRange) {

@@ -102,7 +102,13 @@ CASES = [
     ((16, 12, 20, 24), (4, 6, 5, 8), (3,), np.s_[4:16]),
     ((24, 96), (8, 32), (1,), np.s_[...]),
     ((40, 8, 32), (8, 8, 32), (2,), np.s_[...]),   # 64 outputs per chunk: a partial last tile
+    # >= 256 items per chunk, no split, rows a multiple of 4: the lean column fold
+    ((32, 64, 64), (8, 16, 64), (0,), np.s_[...]),
+    ((8, 64, 256), (8, 16, 256), (1,), np.s_[...]),
+    ((36, 32, 96), (12, 16, 96), (0,), np.s_[12:36]),
+    ((30, 32, 64), (10, 16, 64), (0,), np.s_[...]),   # 10 rows: not whole 4-row groups, k_axes_fold
 ]
+LEAN_CASES = (15, 16, 17)
 
 
 @pytest.mark.parametrize("dtype", ["<f4", ">f4", "<f8", "<i4", "<u4", "<i8"])
@@ -112,7 +118,7 @@ def test_fold_matches_two_step(gpu, dtype, masked, case, monkeypatch):
     gpu.set_fold_min_blocks(1)            # small test grids: fold whatever the size
     shape, chunks, axis, index = CASES[case]
     rng = np.random.default_rng(case * 31 + len(dtype))
-    var, data = _variable(shape, chunks, dtype, rng, masked, nan=(case == 0))
+    var, data = _variable(shape, chunks, dtype, rng, masked, nan=(case in (0, 15)))
     f1, r1, n1 = _partials(var, axis, index, True, monkeypatch)
     f0, r0, n0 = _partials(var, axis, index, False, monkeypatch)
     assert n1 == 1 and n0 == 0            # the fold ran, then the two-step path
@@ -128,7 +134,7 @@ def test_fold_matches_two_step(gpu, dtype, masked, case, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", ["<f4", ">f8", "<i4"])
-@pytest.mark.parametrize("case", [0, 1, 2, 5, 8, 10, 11, 14])
+@pytest.mark.parametrize("case", [0, 1, 2, 5, 8, 10, 11, 14, 16])
 def test_fold_shuffled_matches_two_step(gpu, dtype, case, monkeypatch):
     """Byte-shuffled chunks (the un-shuffle fused into the dense loads, one
     piece per byte plane): fold == two-step bit for bit, and the same result
@@ -136,7 +142,7 @@ def test_fold_shuffled_matches_two_step(gpu, dtype, case, monkeypatch):
     gpu.set_fold_min_blocks(1)
     shape, chunks, axis, index = CASES[case]
     rng = np.random.default_rng(case * 7 + len(dtype))
-    var, data = _variable(shape, chunks, dtype, rng, True, nan=(case == 0), shuffle=True)
+    var, data = _variable(shape, chunks, dtype, rng, True, nan=(case in (0, 16)), shuffle=True)
     f1, r1, n1 = _partials(var, axis, index, True, monkeypatch)
     f0, r0, n0 = _partials(var, axis, index, False, monkeypatch)
     # case 11's 20-element runs are not whole 16-element shuffled load units:
@@ -144,7 +150,7 @@ def test_fold_shuffled_matches_two_step(gpu, dtype, case, monkeypatch):
     assert n1 == (0 if case == 11 else 1) and n0 == 0
     assert f1.tobytes() == f0.tobytes()
     rng = np.random.default_rng(case * 7 + len(dtype))
-    plain, _ = _variable(shape, chunks, dtype, rng, True, nan=(case == 0), shuffle=False)
+    plain, _ = _variable(shape, chunks, dtype, rng, True, nan=(case in (0, 16)), shuffle=False)
     fp, rp, _ = _partials(plain, axis, index, True, monkeypatch)
     if case != 11:     # same kernel, same order: bit-identical
         assert fp.tobytes() == f1.tobytes()
@@ -179,3 +185,40 @@ def test_fold_refuses_too_few_workgroups(gpu, monkeypatch):
     f1, r1, n1 = _partials(var, (0, 1), np.s_[...], True, monkeypatch)
     assert n1 == 1 and f.tobytes() == f1.tobytes()
     gpu.set_fold_min_blocks(0)
+
+
+@pytest.mark.parametrize("dtype", ["<f4", "<f8", "<i4"])
+@pytest.mark.parametrize("case", LEAN_CASES)
+def test_lean_fold_matches_split_fold(gpu, dtype, case, monkeypatch):
+    """k_axes_fold_lean against k_axes_fold (PYAS_FOLD_LEAN=0) and the
+    two-step path, bit for bit, on data with signed zeros in every layer and
+    NaN: the lean kernel folds layer min/max straight into the running
+    min/max with merge's pmin/pmax, which must keep the same zero sign."""
+    gpu.set_fold_min_blocks(1)
+    shape, chunks, axis, index = CASES[case]
+    rng = np.random.default_rng(case * 13 + len(dtype))
+    var, data = _variable(shape, chunks, dtype, rng, True, nan=True)
+    if np.dtype(dtype).kind == "f":
+        flat = data.reshape(-1)
+        z = rng.choice(flat.size, flat.size // 5, replace=False)
+        flat[z] = np.where(rng.random(z.size) < 0.5, -0.0, 0.0).astype(data.dtype)
+        flat[rng.choice(flat.size, 2, replace=False)] = np.nan
+        var, data = _rewrite(var, data)
+    f_lean, r_lean, n_lean = _partials(var, axis, index, True, monkeypatch)
+    monkeypatch.setenv("PYAS_FOLD_LEAN", "0")
+    f_split, _, n_split = _partials(var, axis, index, True, monkeypatch)
+    monkeypatch.delenv("PYAS_FOLD_LEAN")
+    f_two, _, n_two = _partials(var, axis, index, False, monkeypatch)
+    assert n_lean == 1 and n_split == 1 and n_two == 0
+    assert f_lean.tobytes() == f_split.tobytes()
+    assert f_lean.tobytes() == f_two.tobytes()
+
+
+def _rewrite(var, data):
+    """Write `data` back into var's chunk file (same layout, unshuffled)."""
+    with open(var.filename, "r+b") as fh:
+        for cc, (pos, n) in var.chunk_index.items():
+            sl = tuple(slice(i * c, (i + 1) * c) for i, c in zip(cc, var.chunks))
+            fh.seek(pos)
+            fh.write(np.ascontiguousarray(data[sl]).tobytes())
+    return var, data
