@@ -1292,6 +1292,65 @@ __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base
     }
 }
 
+// col_rows over 16-B aligned vectors with two 4-row load groups in flight
+// while the oldest is consumed (col_rows waits for each group before issuing
+// the next).  Same 4-row groups and tail as col_rows: bit-identical.
+#ifndef PYAS_COL_RING
+#define PYAS_COL_RING 1
+#endif
+template <typename T, bool SHUF, bool BSWAP, int MASKED>
+__device__ __forceinline__ void col_rows_ring(const AxesDense &d, const uint8_t *base, int64_t n, int64_t i,
+                                              int sp, const MaskT<T> &mk, TileAcc<T> *acc) {
+    constexpr int ES = sizeof(T), N = 16 / ES, U = PYAS_COL_U;
+    const int S = d.split;
+    const int64_t KIV = d.KI / N, R = d.RO * d.RI;
+    const int64_t sRO = d.KO * d.RI * d.KI;
+    const int64_t dq = S / d.RI, dr = S - dq * d.RI;
+    const int64_t step_off = (dq * sRO + dr * d.KI) * ES;
+    const int64_t wrap_off = (sRO - d.RI * d.KI) * ES;
+    const int64_t ko = i / KIV, v = i - ko * KIV;
+    int64_t ro = sp / d.RI, ri = sp - ro * d.RI;
+    const uint8_t *p = base + ((ro * d.KO + ko) * d.RI * d.KI + ri * d.KI + v * N) * ES;
+    const int64_t nt = (R - sp + S - 1) / S, ng = nt / U;
+    auto fetch = [&](uint4 *b) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            b[u] = ldv<T, SHUF, true>(base, p, n);
+            p += step_off;
+            ri += dr;
+            if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
+        }
+    };
+    uint4 buf[2][U];
+    if (ng > 0) fetch(buf[0]);
+    if (ng > 1) fetch(buf[1]);
+    for (int64_t g = 0; g < ng; g += 2) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            if (g + s < ng) {
+                uint4 cur[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = buf[s][u];
+                if (g + s + 2 < ng) fetch(buf[s]);
+                col_consume<T, BSWAP, MASKED, U>(cur, acc, mk);
+            }
+        }
+    }
+    for (int64_t t = ng * U; t < nt; ++t) {   // p is at row ng * U
+        T x[N];
+        unpack16<T, BSWAP>(ldv<T, SHUF, true>(base, p, n), x);
+        p += step_off;
+        ri += dr;
+        if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k].template add_n<1, MASKED, false>(x + k, mk);
+    }
+    if constexpr (!MASKED) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k].count += (uint32_t)nt;
+    }
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1376,13 +1435,19 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     const int il = threadIdx.x & (IT - 1), sp = threadIdx.x / IT;
     const int64_t items = d.KO * (d.KI / N);
     pyas_partial *out = a.out + a.out_offsets[c];
-    const bool units = SHUF && AL && col_units_ok<T>(d) && ldu_aligned<T, SHUF>(base, a.r.chunk_elems);
+    // aligned chunks: the ring walk (measured faster than the shuffled unit
+    // exchange too); PYAS_COL_RING=0 builds the earlier walks
+    constexpr bool ring = PYAS_COL_RING && AL;
+    const bool units = !ring && SHUF && AL && col_units_ok<T>(d) && ldu_aligned<T, SHUF>(base, a.r.chunk_elems);
     for (int64_t i0 = j * IT; i0 < items; i0 += d.bpc * IT) {   // block-uniform
         const int64_t i = i0 + il;
         TileAcc<T> acc[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) acc[k].init();
-        if constexpr (SHUF && sizeof(T) >= 4) {
+        if constexpr (ring) {
+            if (i < items && sp < S && sp < d.RO * d.RI)
+                col_rows_ring<T, SHUF, BSWAP, MASKED>(d, base, a.r.chunk_elems, i, sp, mk, acc);
+        } else if constexpr (SHUF && sizeof(T) >= 4) {
             if (units) {
                 if (i < items && sp < S) col_rows_units<T, BSWAP, MASKED>(d, base, a.r.chunk_elems, i, sp, mk, acc, stage);
                 __syncthreads();   // the exchange area is reused below
