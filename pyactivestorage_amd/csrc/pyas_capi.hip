@@ -776,15 +776,24 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
     // Lean column fold (k_axes_fold_lean): the split-1 geometry the two-step
     // path uses (so bit-identical), whole 4-row groups, and enough lanes in
     // the grid that no split is needed (PYAS_FOLD_LEAN=0 turns it off).
+    // Split each column's layers in two halves (twice the lanes) when the
+    // unsplit grid is under two rounds of 1024 workgroups and the second half
+    // fits the LDS sums.  PYAS_FOLD_LEAN: 0 off, 1 unsplit, 2 split, unset auto.
     const char *e_lean = getenv("PYAS_FOLD_LEAN");   // per call: tests and benches switch it
-    const bool lean_on = !e_lean || atoi(e_lean) != 0;
-    const int64_t lean_bpc =
-        x.d.mode == 1 ? (x.d.KO * (x.d.KI / (16 / es)) + pyas::kBlock - 1) / pyas::kBlock : 0;
-    if (lean_on && x.d.mode == 1 && x.d.split == 1 && (x.d.RO * x.d.RI) % 4 == 0 &&
+    const int lean_env = e_lean ? atoi(e_lean) : -1;
+    const int64_t lean_items = x.d.mode == 1 ? x.d.KO * (x.d.KI / (16 / es)) : 0;
+    const int64_t lean_bpc1 = (lean_items + pyas::kBlock - 1) / pyas::kBlock;
+    const bool can_split = fg.n_layers >= 2 && fg.n_layers - (fg.n_layers + 1) / 2 <= pyas::kLeanMaxB;
+    if (lean_env != 0 && x.d.mode == 1 && x.d.split == 1 && (x.d.RO * x.d.RI) % 4 == 0 &&
         fg.n_layers * x.d.RO * x.d.RI < (int64_t(1) << 31) &&   // per-lane uint32 counts
-        fg.n_cols * lean_bpc >= min_blocks / 2) {
-        fg.lean = 1;
-        x.d.bpc = lean_bpc;
+        fg.n_cols * lean_bpc1 >= min_blocks / 2) {
+        // auto: only where the rows of a chunk sit inside a kept-outer run
+        // (RI > 1, e.g. C3 axis (1,): 0.71 -> 0.67 ms); with RO rows 16 KiB+
+        // apart (axis (0,)) the split measured 0.71 -> 0.73 ms
+        const bool split = can_split && (lean_env == 2 ||
+                                         (lean_env < 0 && x.d.RI > 1 && fg.n_cols * lean_bpc1 < 2048));
+        fg.lean = split ? 2 : 1;
+        x.d.bpc = (lean_items + pyas::kBlock / fg.lean - 1) / (pyas::kBlock / fg.lean);
     } else if (x.d.mode >= 4) {   // LDS row layout: one output tile per wave
         const int64_t rpw = pyas::kWave / x.d.group, per_block = (pyas::kBlock / pyas::kWave) * rpw;
         x.d.bpc = (x.d.KO + per_block - 1) / per_block;

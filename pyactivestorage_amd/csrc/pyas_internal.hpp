@@ -72,12 +72,15 @@ struct AxesArgs {
 
 // pyas_reduce_axes_grid: the chunk layers of a whole-chunk box query folded
 // inside the dense column kernel (no per-chunk partial arrays)
+constexpr int kLeanMaxB = 8;         // k_axes_fold_lean: layers of a split column's second half (LDS sums)
+
 struct FoldGrid {
     int64_t n_coords[PYAS_MAX_DIMS];  // chunk coordinates per dim (chunk n = C-order position)
     int64_t ostride[PYAS_MAX_DIMS];   // final-output element strides (kept dims)
     int64_t n_layers, n_cols;         // chunks along the reduced dims / kept dims
     uint32_t flags;                   // PYAS_COMBINE_*
-    int32_t lean;                     // column layout: k_axes_fold_lean (split 1, rows % 4 == 0)
+    int32_t lean;                     // column layout: k_axes_fold_lean (split 1, rows % 4 == 0),
+                                      // 1 = one lane per column item, 2 = layers split over two
 };
 
 struct InflateArgs {

@@ -1879,18 +1879,23 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes
 // bit-identical), DEPTH groups of 16-B loads in flight while the oldest is
 // consumed.  The fetch cursor runs ahead of the consume cursor across layer
 // boundaries; a layer's partial is merged into w[] when its last group is
-// consumed (tile_store_lane + merge, as k_combine_grid would).
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, typename LB>
-__device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t off0, int64_t n_layers,
-                                          bool round, const MaskT<T> &mk, const LB &layer_base,
-                                          WAcc<T> *w) {
+// consumed (tile_store_lane + merge, as k_combine_grid would).  The walk
+// covers layers [l0, l0 + n_layers); with `sink` set, each layer's rounded
+// sum is stored at sink[(layer - l0) * sstride + k * IB] instead of being
+// added to w[k].sum (the second half of a split column, added in order by
+// the first half's lane).
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, bool SINK, typename LB>
+__device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t off0, int64_t l0,
+                                          int64_t n_layers, bool round, const MaskT<T> &mk,
+                                          const LB &layer_base, WAcc<T> *w,
+                                          typename TT<T>::Acc *sink, int sstride, int IB) {
     constexpr int N = 16 / sizeof(T), ES = sizeof(T), U = 4;
     const int64_t R = d.RO * d.RI;                      // rows per layer, a multiple of U
     const int64_t step = d.KI * ES;                     // next ri
     const int64_t wrap = (d.KO * d.RI * d.KI - d.RI * d.KI) * ES;   // ri wrapped: next ro
     const int64_t gpl = R / U, total = n_layers * gpl;  // groups per layer, in all
     // fetch cursor
-    const uint8_t *fb = layer_base(0);
+    const uint8_t *fb = layer_base(l0);
     int64_t foff = off0, fl = 0;
     int64_t fri = 0, fg = 0;
     auto fetch = [&](uint4 *buf) {
@@ -1903,7 +1908,7 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
         if (++fg == gpl) {   // next layer (wave-uniform)
             fg = 0;
             if (++fl < n_layers) {
-                fb = layer_base(fl);
+                fb = layer_base(l0 + fl);
                 foff = off0;
                 fri = 0;
             }
@@ -1919,7 +1924,7 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
     TileAcc<T> acc[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) acc[k].init();
-    int64_t cg = 0;   // consumed groups of the current layer
+    int64_t cg = 0, cl = 0;   // consumed groups of the current layer, consumed layers
     auto consume = [&](const uint4 *buf) {
         col_consume<T, BSWAP, MASKED, U>(buf, acc, mk);
         if (++cg == gpl) {
@@ -1929,13 +1934,15 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
                 if constexpr (!MASKED) acc[k].count += (uint32_t)R;
                 pyas_scalar s;
                 TT<T>::put_acc(s, acc[k].sum);
-                w[k].sum += sum_of<T>(s, round);
+                if constexpr (SINK) sink[cl * sstride + k * IB] = sum_of<T>(s, round);
+                else w[k].sum += sum_of<T>(s, round);
                 w[k].mn = pmin(w[k].mn, acc[k].mn);
                 w[k].mx = pmax(w[k].mx, acc[k].mx);
                 acc[k].sum = 0;
                 acc[k].mn = TT<T>::highest();
                 acc[k].mx = TT<T>::lowest();
             }
+            ++cl;
         }
     };
     uint4 buf[DEPTH][U];
@@ -1968,22 +1975,33 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
 
 // Whole-chunk box query, column layout, one lane per item and no split of
 // the reduced rows (dense_geometry's split == 1, rows per chunk a multiple
-// of 4): the lean form of k_axes_fold.  No LDS and no barriers; each lane
-// streams its item's rows through every layer of its column with
-// PYAS_LEAN_DEPTH x 4 loads in flight, and the kernel stays under 128 VGPRs
-// so 16 waves per CU are resident (k_axes_fold carries 146-173 VGPRs, 12
-// waves, and folds its split rows through LDS behind a barrier per layer).
-// Same arithmetic as k_axes_dense (split 1) + k_combine_grid: bit-identical.
+// of 4): the lean form of k_axes_fold.  No barrier inside the walk; each
+// lane streams its item's rows through the layers of its column with
+// PYAS_LEAN_DEPTH x 4 loads in flight, under 128 VGPRs (16 waves per CU;
+// k_axes_fold carries 146-173 VGPRs, 12 waves, and folds its split rows
+// through LDS behind a barrier per layer).
+// g.lean == 2 splits each column's layers in two halves walked by two lanes
+// of the block (twice the waves, each half as long: measured on C3 (0,)
+// 6.1 -> 6.8 TB/s with tools/colwalk_probe.hip).  The second half stores
+// its per-layer sums in LDS, and the first half's lane adds them after its
+// own, in layer order, and folds in the second half's min/max (pmin/pmax,
+// earlier half first), count and NaN.  Either way the arithmetic is
+// k_axes_dense (split 1) + k_combine_grid's: bit-identical.
 template <typename T, bool SHUF, bool BSWAP, int MASKED>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fold_lean(AxesArgs a, FoldGrid g) {
-    constexpr int N = 16 / sizeof(T), ES = sizeof(T);
+    constexpr int N = 16 / sizeof(T), ES = sizeof(T), IB2 = kBlock / 2;
+    using A = typename TT<T>::Acc;
     const AxesDense &d = a.d;
     const ReduceArgs &r = a.r;
+    const int LS = g.lean;                             // 1 or 2 (host)
+    const int IB = kBlock / LS;                        // items per block
+    const int half = threadIdx.x / IB, il = threadIdx.x - half * IB;   // wave-uniform half
     const int64_t col = blockIdx.x / d.bpc;
     const int64_t j = blockIdx.x - col * d.bpc;
     const int64_t items = d.KO * (d.KI / N);
-    const int64_t i = j * kBlock + threadIdx.x;
-    if (i >= items) return;   // no barriers below
+    const int64_t i = j * IB + il;
+    const bool act = i < items;
+    if (LS == 1 && !act) return;   // unsplit: no barrier below
     const uint32_t red = a.axes;
     int64_t ac[PYAS_MAX_DIMS], gstride[PYAS_MAX_DIMS];
     int64_t rest = col, st = 1, nk = 0;
@@ -2020,14 +2038,51 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
     const int64_t off0 = (ko * d.RI * d.KI + v * N) * ES;   // row 0 of item i
     bool al = true;   // block-uniform: every layer's plane pieces aligned
     for (int64_t l = 0; al && l < g.n_layers; ++l) al = ldv_aligned<T, SHUF>(layer_base(l), r.chunk_elems);
+    const int64_t hA = LS == 2 ? (g.n_layers + 1) / 2 : g.n_layers;   // host: n_layers - hA <= kLeanMaxB
+    const int64_t l0 = half ? hA : 0, nl = half ? g.n_layers - hA : hA;
+    __shared__ A s_sum[kLeanMaxB * N * IB2];      // second half: per-layer sums [layer][k][item]
+    __shared__ T s_mn[N * IB2], s_mx[N * IB2];
+    __shared__ uint32_t s_cnt[N * IB2];
+    A *sink = half ? s_sum + il : nullptr;
     WAcc<T> w[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) w[k].init();
-    if (al)
-        lean_walk<T, SHUF, BSWAP, MASKED, true, PYAS_LEAN_DEPTH>(d, r.chunk_elems, off0, g.n_layers, round, mk,
-                                                                layer_base, w);
-    else
-        lean_walk<T, SHUF, BSWAP, MASKED, false, 1>(d, r.chunk_elems, off0, g.n_layers, round, mk, layer_base, w);
+    if (act) {
+        if (al && half)
+            lean_walk<T, SHUF, BSWAP, MASKED, true, PYAS_LEAN_DEPTH, true>(d, r.chunk_elems, off0, l0, nl, round,
+                                                                          mk, layer_base, w, sink, N * IB, IB);
+        else if (al)
+            lean_walk<T, SHUF, BSWAP, MASKED, true, PYAS_LEAN_DEPTH, false>(d, r.chunk_elems, off0, l0, nl, round,
+                                                                           mk, layer_base, w, sink, N * IB, IB);
+        else if (half)
+            lean_walk<T, SHUF, BSWAP, MASKED, false, 1, true>(d, r.chunk_elems, off0, l0, nl, round, mk,
+                                                               layer_base, w, sink, N * IB, IB);
+        else
+            lean_walk<T, SHUF, BSWAP, MASKED, false, 1, false>(d, r.chunk_elems, off0, l0, nl, round, mk,
+                                                                layer_base, w, sink, N * IB, IB);
+    }
+    if (LS == 2) {
+        if (half && act) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                s_mn[k * IB + il] = w[k].mn;
+                s_mx[k * IB + il] = w[k].mx;
+                s_cnt[k * IB + il] = (uint32_t)w[k].count;
+            }
+        }
+        __syncthreads();
+        if (half || !act) return;
+        for (int64_t l = 0; l < g.n_layers - hA; ++l) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) w[k].sum += s_sum[(l * N + k) * IB + il];
+        }
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            w[k].mn = pmin(w[k].mn, s_mn[k * IB + il]);
+            w[k].mx = pmax(w[k].mx, s_mx[k * IB + il]);
+            w[k].count += (int64_t)s_cnt[k * IB + il];
+        }
+    }
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         int64_t loc = i * N + k, f = 0;   // kept-dims index in the chunk -> final element

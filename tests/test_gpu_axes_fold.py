@@ -187,14 +187,18 @@ def test_fold_refuses_too_few_workgroups(gpu, monkeypatch):
     gpu.set_fold_min_blocks(0)
 
 
+@pytest.mark.parametrize("lean", ["1", "2"])
 @pytest.mark.parametrize("dtype", ["<f4", "<f8", "<i4"])
 @pytest.mark.parametrize("case", LEAN_CASES)
-def test_lean_fold_matches_split_fold(gpu, dtype, case, monkeypatch):
-    """k_axes_fold_lean against k_axes_fold (PYAS_FOLD_LEAN=0) and the
+def test_lean_fold_matches_split_fold(gpu, dtype, case, lean, monkeypatch):
+    """k_axes_fold_lean (PYAS_FOLD_LEAN=1: one lane per column item; 2: the
+    column's layers split over two lanes, the second half's per-layer sums
+    handed over in LDS) against k_axes_fold (PYAS_FOLD_LEAN=0) and the
     two-step path, bit for bit, on data with signed zeros in every layer and
     NaN: the lean kernel folds layer min/max straight into the running
     min/max with merge's pmin/pmax, which must keep the same zero sign."""
     gpu.set_fold_min_blocks(1)
+    monkeypatch.setenv("PYAS_FOLD_LEAN", lean)
     shape, chunks, axis, index = CASES[case]
     rng = np.random.default_rng(case * 13 + len(dtype))
     var, data = _variable(shape, chunks, dtype, rng, True, nan=True)
@@ -207,7 +211,6 @@ def test_lean_fold_matches_split_fold(gpu, dtype, case, monkeypatch):
     f_lean, r_lean, n_lean = _partials(var, axis, index, True, monkeypatch)
     monkeypatch.setenv("PYAS_FOLD_LEAN", "0")
     f_split, _, n_split = _partials(var, axis, index, True, monkeypatch)
-    monkeypatch.delenv("PYAS_FOLD_LEAN")
     f_two, _, n_two = _partials(var, axis, index, False, monkeypatch)
     assert n_lean == 1 and n_split == 1 and n_two == 0
     assert f_lean.tobytes() == f_split.tobytes()
