@@ -148,11 +148,15 @@ int main() {
         snprintf(nm, sizeof nm, "contig grid %d", blocks);
         report(nm, time_ms([&] { hipLaunchKernelGGL(k_contig, dim3(blocks), dim3(256), 0, 0, buf, out, 4096); }, reps));
     }
-#define COL(I, D, L) report("col I" #I " D" #D " L" #L, time_ms([&] { \
-        hipLaunchKernelGGL((k_col<I, D, L>), dim3(256 * (4 / I) * L), dim3(256), 0, 0, buf, out); }, reps))
-    COL(1, 1, 1); COL(1, 2, 1); COL(1, 3, 1); COL(1, 2, 2); COL(1, 2, 4);
-    COL(2, 1, 2); COL(2, 2, 2); COL(2, 1, 4);
-    COL(4, 1, 4); COL(4, 2, 4); COL(4, 1, 8);
+    // SH: dynamic LDS per block, 40 KiB caps residency at 4 blocks (16 waves) per CU
+#define COL(I, D, L, SH) report("col I" #I " D" #D " L" #L " lds" #SH, time_ms([&] { \
+        hipLaunchKernelGGL((k_col<I, D, L>), dim3(256 * (4 / I) * L), dim3(256), SH, 0, buf, out); }, reps))
+    COL(1, 1, 1, 0); COL(1, 2, 1, 0); COL(1, 3, 1, 0); COL(1, 2, 2, 0); COL(1, 2, 4, 0);
+    COL(2, 1, 2, 0); COL(2, 2, 2, 0); COL(2, 1, 4, 0);
+    COL(4, 1, 4, 0); COL(4, 2, 4, 0); COL(4, 1, 8, 0);
+    // fewer waves with more contiguity; more waves at capped residency
+    COL(2, 1, 1, 0); COL(2, 2, 1, 0); COL(4, 1, 1, 0); COL(4, 1, 2, 0);
+    COL(1, 2, 2, 40960); COL(2, 1, 2, 40960); COL(4, 1, 4, 40960); COL(2, 1, 4, 40960);
     CK(hipFree(buf));
     CK(hipFree(out));
     return 0;
