@@ -807,12 +807,12 @@ class Active:
         vbuf, mbuf, cbuf = have
         engine.format_partials(ctx, dt, fin.ptr, n, method, vbuf.ptr, mbuf.ptr,
                                cbuf.ptr if cbuf is not None else None, st)
-        vals = np.empty(n, dtype=vdt)
-        mask = np.empty(n, dtype=np.bool_)
+        vals = ctx.result_array(n, vdt)
+        mask = ctx.result_array(n, np.bool_)
         ctx.d2h(vals, vbuf.ptr, st)
         ctx.d2h(mask, mbuf.ptr, st)
         if cbuf is not None:
-            cnt = np.empty(n, dtype=np.int64)
+            cnt = ctx.result_array(n, np.int64)
             ctx.d2h(cnt, cbuf.ptr, st)
         ctx.synchronize(st)
         out = np.ma.MaskedArray(vals.reshape(shape), mask=mask.reshape(shape))
@@ -1034,8 +1034,8 @@ class Active:
         sc.pos, sc.chunk_base = pb.ptr, cb.ptr
         for d in range(nd):
             sc.out_stride[d] = int(ostride[d])
-        vals = np.empty(total, dtype=nd_native)
-        msk = np.empty(total, dtype=np.uint8)
+        vals = ctx.result_array(total, nd_native)
+        msk = ctx.result_array(total, np.uint8)
         vb = DeviceBuffer(ctx, vals.nbytes)
         mb = DeviceBuffer(ctx, msk.nbytes)
         engine.select_scatter(ctx, plan.batch, plan.mask_up.struct, sc, vb.ptr, mb.ptr, st)

@@ -932,6 +932,10 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, cons
     }
     if (!in || !out || !g->chunk_out_offsets) return fail(PYAS_EINVAL, "NULL argument");
     PYAS_HIP(hipSetDevice(ctx->device));
+    // PYAS_COMBINE_WAVE=0 (read per call: tests switch it) keeps the
+    // per-thread fold for every layer count
+    const char *e_wave = getenv("PYAS_COMBINE_WAVE");
+    if (e_wave && std::strcmp(e_wave, "0") == 0) combine_flags |= pyas::kCombineThreadOnly;
     PYAS_HIP(pyas::launch_combine_grid(dtype, in, *g, n_out, n_layers, combine_flags, out,
                                        (hipStream_t)stream));
     return PYAS_OK;

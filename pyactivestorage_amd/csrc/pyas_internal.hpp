@@ -72,6 +72,9 @@ struct AxesArgs {
 
 // pyas_reduce_axes_grid: the chunk layers of a whole-chunk box query folded
 // inside the dense column kernel (no per-chunk partial arrays)
+// pyas_combine_grid: internal combine flag (PYAS_COMBINE_WAVE=0) keeping the
+// per-thread fold (k_combine_grid) for every layer count
+constexpr uint32_t kCombineThreadOnly = 1u << 31;
 constexpr int kLeanMaxB = 8;         // k_axes_fold_lean: layers of a split column's second half (LDS sums)
 
 struct FoldGrid {

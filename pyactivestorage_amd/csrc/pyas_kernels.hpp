@@ -606,6 +606,13 @@ __global__ __launch_bounds__(kBlock) void k_reduce_u(ReduceArgs a) {
     reduce_body<T, SHUF, BSWAP, MASKED, SEL>(a);
 }
 
+// LDS writes of a wave visible to its other lanes (no block barrier)
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // segmented combine: one thread per output segment, sequential fixed order
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_combine_segments(const pyas_partial *in, const int64_t *index,
@@ -694,6 +701,136 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
             if (l0 + u < n_layers) merge(acc, p[u], round);
     }
     store_wpartial(out + f, acc);
+}
+
+// k_combine_grid for few outputs with many layers each (C3 axes (0,1)/(1,2)/
+// (0,2): 1024 outputs x 256 layers, where one thread per output leaves 16
+// waves on the device, each waiting on its layers' loads in turn): one wave
+// per output, lane t holding layer l0 + t of a 64-layer tile, up to kCwTiles
+// tiles' loads in flight per lane.  Per tile:
+//  - count, min and max go through an in-order butterfly (the lower lane
+//    block is the left operand): merge's min/max keep the earlier of equal
+//    values and the later NaN, and the count guard makes an empty layer the
+//    identity, so this operator is associative and the tree equals the
+//    sequential fold;
+//  - each lane rounds its layer's sum (sum_of) and lane 0 adds the 64 sums
+//    from LDS in layer order, the only sequential chain left.
+// Same values as k_combine_grid's merges, in the same order: bit-identical.
+constexpr int kCombineWaveMinLayers = 32;   // below this the per-thread form is used
+constexpr int kCwTiles = 4;                 // 64-layer tiles in flight per lane
+
+template <typename T>
+__device__ __forceinline__ void cw_combine(int64_t &c, T &mn, T &mx, int64_t c2, T mn2, T mx2) {
+    c += c2;
+    mn = pmin(mn, mn2);   // (left, right)
+    mx = pmax(mx, mx2);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_combine_grid_wave(const pyas_partial *in, pyas_grid g,
+                                                              int64_t n_out, int64_t n_layers,
+                                                              uint32_t flags, pyas_partial *out) {
+    using A = typename TT<T>::Acc;
+    __shared__ A s_sum[kBlock / kWave][kWave];
+    const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    const int64_t f = (int64_t)blockIdx.x * (kBlock / kWave) + w;
+    if (f >= n_out) return;   // wave-uniform; only wave-level syncs below
+    const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
+    int64_t gstride[PYAS_MAX_DIMS];
+    int64_t j = 0, jstride = 1, rest = f, st = 1, nk = 0;
+#pragma unroll
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+        gstride[d] = st;
+        if (d < g.ndim) {
+            st *= g.n_coords[d];
+            if (!((g.axes_mask >> d) & 1u)) {
+                const int64_t e = g.out_extent[d];
+                const int64_t p = rest % e;
+                rest /= e;
+                const int64_t c = g.pos_coord[d][p];
+                nk += c * gstride[d];
+                j += (int64_t)g.pos_local[d][p] * jstride;
+                jstride *= g.coord_count[d][c];
+            }
+        }
+    }
+    auto offset = [&](int64_t l) {   // layer l (< 2^31, host) -> its chunk's partial array
+        int64_t n = nk;
+        uint32_t rr = (uint32_t)l;
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            if (d < g.ndim && ((g.axes_mask >> d) & 1u)) {
+                const uint32_t nc = (uint32_t)g.n_coords[d], q = rr / nc;
+                n += (int64_t)(rr - q * nc) * gstride[d];
+                rr = q;
+            }
+        }
+        return g.chunk_out_offsets[n];
+    };
+    WAcc<T> acc;
+    acc.init();
+    for (int64_t l0 = 0; l0 < n_layers; l0 += kCwTiles * kWave) {   // wave-uniform
+        pyas_partial p[kCwTiles];
+        int64_t off[kCwTiles];
+#pragma unroll
+        for (int u = 0; u < kCwTiles; ++u) {
+            const int64_t l = l0 + u * kWave + lane;
+            off[u] = l < n_layers ? offset(l) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kCwTiles; ++u) {
+            const int64_t l = l0 + u * kWave + lane;
+            if (l < n_layers) p[u] = in[off[u] + j];
+        }
+#pragma unroll
+        for (int u = 0; u < kCwTiles; ++u) {
+            const int64_t t0 = l0 + u * kWave;
+            if (t0 >= n_layers) break;
+            const bool live = t0 + lane < n_layers;
+            int64_t c = 0;
+            T mn = TT<T>::highest(), mx = TT<T>::lowest();
+            A sm = 0;
+            if (live) {
+                sm = sum_of<T>(p[u].sum, round);
+                if (p[u].count > 0) {
+                    c = p[u].count;
+                    mn = TT<T>::from(p[u].min);
+                    mx = TT<T>::from(p[u].max);
+                }
+            }
+#pragma unroll
+            for (int m = 1; m < kWave; m <<= 1) {
+                const int64_t c2 = shfl_xor(c, m);
+                const T mn2 = shfl_xor(mn, m), mx2 = shfl_xor(mx, m);
+                if (lane & m) {            // partner block is the earlier one
+                    int64_t cl = c2;
+                    T lmn = mn2, lmx = mx2;
+                    cw_combine(cl, lmn, lmx, c, mn, mx);
+                    c = cl; mn = lmn; mx = lmx;
+                } else {
+                    cw_combine(c, mn, mx, c2, mn2, mx2);
+                }
+            }
+            s_sum[w][lane] = sm;
+            wave_sync_lds();
+            if (lane == 0) {
+                const int m = (int)(n_layers - t0 < kWave ? n_layers - t0 : kWave);
+                A x = acc.sum;
+                if (m == kWave) {
+#pragma unroll 16
+                    for (int k = 0; k < kWave; ++k) x += s_sum[w][k];
+                } else {
+                    for (int k = 0; k < m; ++k) x += s_sum[w][k];
+                }
+                acc.sum = x;
+                acc.count += c;
+                acc.mn = pmin(acc.mn, mn);
+                acc.mx = pmax(acc.mx, mx);
+            }
+            wave_sync_lds();   // lane 0's reads before the next tile's writes
+        }
+    }
+    if (lane == 0) store_wpartial(out + f, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1010,10 +1147,15 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
 }
 
 // One byte-plane piece of a shuffled vector: W bytes at q (AL: W-aligned)
+#ifndef PYAS_PLANE_NT
+#define PYAS_PLANE_NT 1   // plane pieces loaded non-temporal (0: plain loads, a tuning variant)
+#endif
 template <typename W, bool AL>
 __device__ __forceinline__ W ldp(const uint8_t *q) {
-    if constexpr (AL) {
+    if constexpr (AL && PYAS_PLANE_NT) {
         return __builtin_nontemporal_load(reinterpret_cast<const W *>(q));
+    } else if constexpr (AL) {
+        return *reinterpret_cast<const W *>(q);
     } else {
         W r;
         __builtin_memcpy(&r, q, sizeof(W));
@@ -1351,11 +1493,6 @@ __device__ __forceinline__ void col_rows_ring(const AxesDense &d, const uint8_t 
     }
 }
 
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Shuffled column layout in load units (ES >= 4): the G = ES lanes of an
 // item group (consecutive items of one kept run) each load ONE unit -- 16
@@ -2536,7 +2673,14 @@ template <typename T>
 hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int64_t n_out,
                                  int64_t n_layers, uint32_t flags, pyas_partial *out,
                                  hipStream_t st) {
-    const dim3 grid((unsigned)((n_out + kBlock - 1) / kBlock)), blk(kBlock);
+    const dim3 blk(kBlock);
+    if (n_layers >= kCombineWaveMinLayers && !(flags & kCombineThreadOnly)) {
+        constexpr int64_t wpb = kBlock / kWave;
+        const dim3 grid((unsigned)((n_out + wpb - 1) / wpb));
+        hipLaunchKernelGGL((k_combine_grid_wave<T>), grid, blk, 0, st, in, g, n_out, n_layers, flags, out);
+        return hipGetLastError();
+    }
+    const dim3 grid((unsigned)((n_out + kBlock - 1) / kBlock));
     hipLaunchKernelGGL((k_combine_grid<T>), grid, blk, 0, st, in, g, n_out, n_layers, flags, out);
     return hipGetLastError();
 }

@@ -84,6 +84,64 @@ def _release_thread(ctx: "Context", state) -> None:
     state.clear()
 
 
+class _ResultPool:
+    """Pinned host blocks for query results that come back from the device
+    (``Active``'s formatted values and mask): a D2H copy into pinned memory
+    is DMA at the PCIe rate, into a fresh pageable ``np.empty`` it is staged
+    by the runtime.  A block is leased to the array built on it and returns
+    to the pool's free list when that array (and every view of it) is
+    collected.  Blocks are power-of-two sized; at most ``cap`` bytes are
+    pinned, beyond that callers get pageable arrays."""
+
+    MIN_BYTES = 64 << 10   # smaller results: pageable (the copy is latency-bound)
+
+    def __init__(self, ctx: "Context", cap: int):
+        self.ctx, self.cap = ctx, int(cap)
+        self.lock = threading.Lock()
+        self.free: dict[int, list[int]] = {}
+        self.pinned = 0          # bytes pinned by the pool (leased + free)
+
+    def array(self, n: int, dtype) -> np.ndarray:
+        dt = np.dtype(dtype)
+        nbytes = int(n) * dt.itemsize
+        if nbytes < self.MIN_BYTES or self.cap <= 0:
+            return np.empty(n, dtype=dt)
+        size = 1 << (nbytes - 1).bit_length()
+        with self.lock:
+            blocks = self.free.get(size)
+            ptr = blocks.pop() if blocks else None
+            if ptr is None:
+                if self.pinned + size > self.cap:
+                    return np.empty(n, dtype=dt)
+                p = ctypes.c_void_p()
+                _lib.check(self.ctx.lib.pyas_host_alloc(self.ctx.handle, size, ctypes.byref(p)),
+                           "pyas_host_alloc")
+                ptr = p.value
+                self.pinned += size
+        raw = (ctypes.c_uint8 * nbytes).from_address(ptr)
+        raw._lease = _Lease(self, ptr, size)
+        return np.frombuffer(raw, dtype=dt, count=n)
+
+    def put(self, ptr: int, size: int) -> None:
+        with self.lock:
+            self.free.setdefault(size, []).append(ptr)
+
+
+class _Lease:
+    """Returns a pinned block to its pool when the result array is gone."""
+
+    __slots__ = ("pool", "ptr", "size")
+
+    def __init__(self, pool: _ResultPool, ptr: int, size: int):
+        self.pool, self.ptr, self.size = pool, ptr, size
+
+    def __del__(self):
+        try:
+            self.pool.put(self.ptr, self.size)
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass
+
+
 class Context:
     """A ``pyas_ctx`` bound to one device."""
 
@@ -103,6 +161,8 @@ class Context:
         self.live_streams = 0        # per-thread streams currently alive
         self.pinned_bytes = 0        # per-thread pinned staging currently alive
         self._coalescer = None
+        # PYAS_RESULT_PINNED_MIB: pinned bytes for result arrays (0: pageable)
+        self._results = _ResultPool(self, int(os.environ.get("PYAS_RESULT_PINNED_MIB", "256")) << 20)
 
     def _set_tie_rules(self):
         """NumPy's zero-sign tie rule of this host for f32/f64 (zerosign.py),
@@ -191,6 +251,11 @@ class Context:
             arr = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(p.value))
             hb = st["host"] = (p.value, size, arr)
         return hb[2]
+
+    def result_array(self, n: int, dtype) -> np.ndarray:
+        """A host array of ``n`` elements for a device result to be copied
+        into: pinned (leased from the context's pool) when large enough."""
+        return self._results.array(n, dtype)
 
     # -- copies --------------------------------------------------------------
     def h2d(self, dst_ptr: int, host: np.ndarray, stream: int | None) -> None:

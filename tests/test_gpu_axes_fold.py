@@ -225,3 +225,44 @@ def _rewrite(var, data):
             fh.seek(pos)
             fh.write(np.ascontiguousarray(data[sl]).tobytes())
     return var, data
+
+
+WAVE_CASES = [
+    # many chunk layers per output: pyas_combine_grid's one-wave-per-output form
+    ((130, 8, 16), (1, 4, 16), (0,), np.s_[...]),                   # 130 layers: 2 full tiles + 2
+    ((10, 12, 64), (1, 1, 64), (0, 1), np.s_[...]),                 # 120 layers
+    ((3, 40, 8, 24), (1, 1, 4, 8), (0, 1), np.s_[:, 3:37, 1:7, 5:20]),   # 102 layers, hyperslab tables
+    ((4, 96, 8), (2, 1, 8), (1,), np.s_[1:4, :, 2:8]),              # 96 layers between kept dims
+    ((64, 4, 8), (2, 4, 8), (0,), np.s_[...]),                      # 32 layers: the threshold
+]
+
+
+@pytest.mark.parametrize("dtype", ["<f4", ">f4", "<f8", "<i4"])
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("case", range(len(WAVE_CASES)))
+def test_combine_grid_wave_matches_thread(gpu, dtype, masked, case, monkeypatch):
+    """k_combine_grid_wave (one wave per output; lanes load 64 layers into
+    LDS, lane 0 merges them in layer order) against k_combine_grid
+    (PYAS_COMBINE_WAVE=0, one thread per output), bit for bit, on the
+    two-step path, with signed zeros and NaN in the data; then the result
+    against NumPy's masked mean of the selection."""
+    shape, chunks, axis, index = WAVE_CASES[case]
+    rng = np.random.default_rng(case * 17 + len(dtype) + masked)
+    var, data = _variable(shape, chunks, dtype, rng, masked, nan=True)
+    if np.dtype(dtype).kind == "f":
+        flat = data.reshape(-1)
+        z = rng.choice(flat.size, flat.size // 5, replace=False)
+        flat[z] = np.where(rng.random(z.size) < 0.5, -0.0, 0.0).astype(data.dtype)
+        var, data = _rewrite(var, data)
+    monkeypatch.delenv("PYAS_COMBINE_WAVE", raising=False)
+    f_wave, r_wave, n_wave = _partials(var, axis, index, False, monkeypatch)
+    monkeypatch.setenv("PYAS_COMBINE_WAVE", "0")
+    f_thr, _, n_thr = _partials(var, axis, index, False, monkeypatch)
+    assert n_wave == 0 and n_thr == 0       # the two-step path both times
+    assert f_wave.tobytes() == f_thr.tobytes()
+    sel = data[index]
+    m = (np.ma.masked_equal(sel, var.attrs["_FillValue"][0]) if masked else np.ma.MaskedArray(sel))
+    want = np.ma.masked_invalid(np.ma.mean(m.astype(np.float64), axis=axis, keepdims=True))
+    np.testing.assert_array_equal(np.ma.getmaskarray(r_wave), np.ma.getmaskarray(want))
+    ok = ~np.ma.getmaskarray(want)
+    np.testing.assert_allclose(np.ma.getdata(r_wave)[ok], np.ma.getdata(want)[ok], rtol=1e-5, atol=1e-4)
