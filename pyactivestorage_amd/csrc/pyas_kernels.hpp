@@ -1150,9 +1150,9 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
 #ifndef PYAS_PLANE_NT
 #define PYAS_PLANE_NT 1   // plane pieces loaded non-temporal (0: plain loads, a tuning variant)
 #endif
-template <typename W, bool AL>
+template <typename W, bool AL, bool NT = true>
 __device__ __forceinline__ W ldp(const uint8_t *q) {
-    if constexpr (AL && PYAS_PLANE_NT) {
+    if constexpr (AL && NT && PYAS_PLANE_NT) {
         return __builtin_nontemporal_load(reinterpret_cast<const W *>(q));
     } else if constexpr (AL) {
         return *reinterpret_cast<const W *>(q);
@@ -1170,7 +1170,9 @@ __device__ __forceinline__ W ldp(const uint8_t *q) {
 // of N bytes (f32: 4 dwords, 256 contiguous bytes per plane per wave),
 // reassembled into the plain bytes with v_perm; the caller's unpack16 then
 // applies the byte order as for plain chunks.  AL: see ldv_aligned.
-template <typename T, bool SHUF, bool AL>
+// NT = false: plain loads for the plane pieces (the lean fold's walk over
+// rows whose plane pieces share 128-B lines, measured faster there).
+template <typename T, bool SHUF, bool AL, bool NT = true>
 __device__ __forceinline__ uint4 ldv(const uint8_t *base, const uint8_t *p, int64_t n) {
     constexpr int ES = sizeof(T);
     if constexpr (!SHUF || ES == 1) {
@@ -1180,18 +1182,18 @@ __device__ __forceinline__ uint4 ldv(const uint8_t *base, const uint8_t *p, int6
         if constexpr (ES == 4) {          // 4 planes x 4 bytes
             uint32_t w[4], e[4];
 #pragma unroll
-            for (int b = 0; b < 4; ++b) w[b] = ldp<uint32_t, AL>(q + b * n);
+            for (int b = 0; b < 4; ++b) w[b] = ldp<uint32_t, AL, NT>(q + b * n);
             transpose4(w[0], w[1], w[2], w[3], e);
             return make_uint4(e[0], e[1], e[2], e[3]);
         } else if constexpr (ES == 2) {   // 2 planes x 8 bytes
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-            const u32x2 a = ldp<u32x2, AL>(q), b = ldp<u32x2, AL>(q + n);
+            const u32x2 a = ldp<u32x2, AL, NT>(q), b = ldp<u32x2, AL, NT>(q + n);
             return make_uint4(perm(b.x, a.x, 0x05010400u), perm(b.x, a.x, 0x07030602u),
                               perm(b.y, a.y, 0x05010400u), perm(b.y, a.y, 0x07030602u));
         } else {                          // 8 planes x 2 bytes
             uint32_t h[8];
 #pragma unroll
-            for (int b = 0; b < 8; ++b) h[b] = ldp<uint16_t, AL>(q + b * n);
+            for (int b = 0; b < 8; ++b) h[b] = ldp<uint16_t, AL, NT>(q + b * n);
             const uint32_t x01 = h[0] | (h[1] << 16), x23 = h[2] | (h[3] << 16);
             const uint32_t x45 = h[4] | (h[5] << 16), x67 = h[6] | (h[7] << 16);
             return make_uint4(perm(x23, x01, 0x06040200u), perm(x67, x45, 0x06040200u),
@@ -2021,7 +2023,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes
 // sum is stored at sink[(layer - l0) * sstride + k * IB] instead of being
 // added to w[k].sum (the second half of a split column, added in order by
 // the first half's lane).
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, bool SINK, typename LB>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, bool SINK, bool NT, typename LB>
 __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t off0, int64_t l0,
                                           int64_t n_layers, bool round, const MaskT<T> &mk,
                                           const LB &layer_base, WAcc<T> *w,
@@ -2038,7 +2040,7 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
     auto fetch = [&](uint4 *buf) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            buf[u] = ldv<T, SHUF, AL>(fb, fb + foff, n);
+            buf[u] = ldv<T, SHUF, AL, NT>(fb, fb + foff, n);
             foff += step;
             if (++fri == d.RI) { fri = 0; foff += wrap; }
         }
@@ -2184,19 +2186,33 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
     WAcc<T> w[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) w[k].init();
-    if (act) {
-        if (al && half)
-            lean_walk<T, SHUF, BSWAP, MASKED, true, PYAS_LEAN_DEPTH, true>(d, r.chunk_elems, off0, l0, nl, round,
-                                                                          mk, layer_base, w, sink, N * IB, IB);
-        else if (al)
-            lean_walk<T, SHUF, BSWAP, MASKED, true, PYAS_LEAN_DEPTH, false>(d, r.chunk_elems, off0, l0, nl, round,
-                                                                           mk, layer_base, w, sink, N * IB, IB);
-        else if (half)
-            lean_walk<T, SHUF, BSWAP, MASKED, false, 1, true>(d, r.chunk_elems, off0, l0, nl, round, mk,
-                                                               layer_base, w, sink, N * IB, IB);
+    // AL_ / NT_: compile-time aligned walk / non-temporal plane loads
+    auto walk = [&](auto al_c, auto nt_c) {
+        constexpr bool AL_ = decltype(al_c)::value, NT_ = decltype(nt_c)::value;
+        constexpr int DEP = AL_ ? PYAS_LEAN_DEPTH : 1;
+        if (half)
+            lean_walk<T, SHUF, BSWAP, MASKED, AL_, DEP, true, NT_>(d, r.chunk_elems, off0, l0, nl, round,
+                                                                 mk, layer_base, w, sink, N * IB, IB);
         else
-            lean_walk<T, SHUF, BSWAP, MASKED, false, 1, false>(d, r.chunk_elems, off0, l0, nl, round, mk,
-                                                                layer_base, w, sink, N * IB, IB);
+            lean_walk<T, SHUF, BSWAP, MASKED, AL_, DEP, false, NT_>(d, r.chunk_elems, off0, l0, nl, round,
+                                                                  mk, layer_base, w, sink, N * IB, IB);
+    };
+    if (act) {
+        bool done = false;
+        if constexpr (SHUF) {
+            // rows under 128 elements: a row's plane piece shares its 128-B
+            // line with the next row's, read by the lane's next load; plain
+            // loads keep the line for it (C3 shuffled (1,): 64-B pieces,
+            // 0.785 -> 0.751 ms; (0,)'s 4-KiB pieces stay non-temporal)
+            if (al && d.KI < 128) {
+                walk(std::true_type{}, std::false_type{});
+                done = true;
+            }
+        }
+        if (!done) {
+            if (al) walk(std::true_type{}, std::true_type{});
+            else walk(std::false_type{}, std::true_type{});
+        }
     }
     if (LS == 2) {
         if (half && act) {
