@@ -717,6 +717,10 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
 //    from LDS in layer order, the only sequential chain left.
 // Same values as k_combine_grid's merges, in the same order: bit-identical.
 constexpr int kCombineWaveMinLayers = 32;   // below this the per-thread form is used
+// Above this many outputs the per-thread form has enough waves to hide its
+// loads (>= 8 per CU) and reads each layer's partials coalesced across
+// adjacent outputs, where the wave form reads 32 B per lane from 64 chunks
+constexpr int64_t kCombineWaveMaxOut = int64_t(1) << 17;
 constexpr int kCwTiles = 4;                 // 64-layer tiles in flight per lane
 
 template <typename T>
@@ -2690,7 +2694,7 @@ hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int
                                  int64_t n_layers, uint32_t flags, pyas_partial *out,
                                  hipStream_t st) {
     const dim3 blk(kBlock);
-    if (n_layers >= kCombineWaveMinLayers && !(flags & kCombineThreadOnly)) {
+    if (n_layers >= kCombineWaveMinLayers && n_out <= kCombineWaveMaxOut && !(flags & kCombineThreadOnly)) {
         constexpr int64_t wpb = kBlock / kWave;
         const dim3 grid((unsigned)((n_out + wpb - 1) / wpb));
         hipLaunchKernelGGL((k_combine_grid_wave<T>), grid, blk, 0, st, in, g, n_out, n_layers, flags, out);
