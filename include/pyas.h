@@ -234,6 +234,22 @@ int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch,
                        pyas_partial *total, uint32_t combine_flags,
                        void *stream);
 
+/* pyas_reduce_chunks for a selection batch (sel != NULL) whose chunks split
+ * into wholly selected ones (whole_ids, device int32, n_whole entries) and
+ * the rest (part_ids): two reduce launches, the first with the lean
+ * whole-chunk kernel (no table reads, occupancy-capped registers), the second
+ * with the selection-aware kernel; chunk_out / total are the same as from one
+ * pyas_reduce_chunks call (same per-chunk arithmetic, same k_finish order).
+ * n_whole + n_part must equal n_chunks; no vector mask tables.  Replaces the
+ * same call as pyas_reduce_chunks (storage.py:8-104 over a box query whose
+ * interior chunks are whole, active.py:557-598). */
+int pyas_reduce_chunks_split(pyas_ctx *ctx, const pyas_batch *batch,
+                             const pyas_mask *mask, const int32_t *whole_ids,
+                             int64_t n_whole, const int32_t *part_ids,
+                             int64_t n_part, pyas_partial *chunk_out,
+                             pyas_partial *total, uint32_t combine_flags,
+                             void *stream);
+
 /* Partial-axis reduction: for chunk c the selected block is reduced over the
  * chunk dims whose bit is set in axes_mask; outputs (row-major over the
  * remaining selected dims, keepdims) start at out[out_offsets[c]]. */

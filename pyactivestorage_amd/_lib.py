@@ -145,6 +145,8 @@ SIGNATURES = {
     "pyas_stream_synchronize": [_vp, _vp],
     "pyas_stream_wait": [_vp, _vp, _vp],
     "pyas_reduce_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _u32, _vp],
+    "pyas_reduce_chunks_split": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _i64, _vp, _i64,
+                                 _vp, _vp, _u32, _vp],
     "pyas_reduce_axes": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _u32, _vp, _vp, _vp],
     "pyas_select_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _vp, _vp],
     "pyas_select_scatter": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(Scatter),

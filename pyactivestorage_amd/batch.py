@@ -11,6 +11,7 @@ be timed or captured.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -53,6 +54,8 @@ class ReductionPlan:
         st = stream
         self.offsets_buf = self._upload(offsets, st)
         sel_ptr = pool_ptr = None
+        self.split = None        # (whole ids ptr, n, other ids ptr, n): pyas_reduce_chunks_split
+        table = None
         sel_shape, kept = self.chunk_shape, tuple(range(len(self.chunk_shape)))
         if selections is not None:
             if len(selections) != self.n_chunks:
@@ -81,6 +84,18 @@ class ReductionPlan:
             sel_ptr = self._upload(table, st).ptr
             pool_ptr = self._upload(index_pool if index_pool is not None
                                     else np.zeros(1, dtype=np.int32), st).ptr
+        vector_tables = self.cm.tables[0] is not None or self.cm.tables[1] is not None
+        if sel_ptr is not None and not vector_tables and os.environ.get("PYAS_SPLIT_WHOLE", "0") == "1":
+            # opt-in: a box query's interior chunks are whole; reduce them with
+            # the lean kernel and only the boundary chunks with the
+            # selection-aware one (measured slower on C5: DESIGN §6.1)
+            full = _full_rows(table, self.chunk_shape)
+            n_whole = int(full.sum())
+            if 0 < n_whole < self.n_chunks:
+                whole = np.flatnonzero(full).astype(np.int32)
+                part = np.flatnonzero(~full).astype(np.int32)
+                self.split = (self._upload(whole, st).ptr, n_whole, self._upload(part, st).ptr,
+                              self.n_chunks - n_whole)
         self.layout = engine.Layout(self.dtype, self.chunk_shape,
                                     shuffle if (shuffle and shuffle > 1 and es > 1) else 0)
         self.batch = self.layout.batch_struct(self.n_chunks, data_ptr, self.offsets_buf.ptr,
@@ -101,9 +116,14 @@ class ReductionPlan:
     def launch(self, stream=None, chunk_partials=True) -> None:
         """Enqueue: fused reduce of every chunk -> per-chunk partials ->
         fixed-order combine into ``self.total``."""
-        engine.reduce_chunks(self.ctx, self.batch, self.mask_up.struct,
-                             self.chunk_partials.ptr if chunk_partials else None, self.total.ptr,
-                             self.round_to_var, stream)
+        out = self.chunk_partials.ptr if chunk_partials else None
+        if self.split is not None:
+            w, nw, p, n_p = self.split
+            engine.reduce_chunks_split(self.ctx, self.batch, self.mask_up.struct, w, nw, p, n_p,
+                                       out, self.total.ptr, self.round_to_var, stream)
+        else:
+            engine.reduce_chunks(self.ctx, self.batch, self.mask_up.struct, out, self.total.ptr,
+                                 self.round_to_var, stream)
 
     def total_tensor(self, torch):
         """Zero-copy torch view (32 uint8) of the device total, e.g. to hand
@@ -126,6 +146,14 @@ class ReductionPlan:
             self.ctx.d2h(host, self.chunk_partials.ptr, stream)
         self.ctx.synchronize(stream)
         return host
+
+
+def _full_rows(table, chunk_shape) -> np.ndarray:
+    """Per chunk: whether its selection is its whole box in C order."""
+    nd = len(chunk_shape)
+    t = table[:, :nd, :]
+    return ((t[:, :, 0] == 0).all(axis=1) & (t[:, :, 1] == 1).all(axis=1)
+            & (t[:, :, 2] == np.asarray(chunk_shape, dtype=np.int32)).all(axis=1))
 
 
 def _all_full(table, chunk_shape) -> bool:

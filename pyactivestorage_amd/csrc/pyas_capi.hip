@@ -509,9 +509,15 @@ int pyas_stream_wait(pyas_ctx *ctx, void *waiter, void *waitee) {
     return PYAS_OK;
 }
 
-int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
-                       pyas_partial *chunk_out, pyas_partial *total, uint32_t combine_flags,
-                       void *stream) {
+// pyas_reduce_chunks, optionally as two reduce launches over a selection
+// batch's whole chunks (whole_ids: the capped lean kernel, no selection
+// table) and its other chunks (part_ids: the selection-aware kernel); both
+// write their tile partials at the chunks' places, so k_finish folds them in
+// chunk order as for one launch.
+static int reduce_chunks_impl(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                              const int32_t *whole_ids, int64_t n_whole, const int32_t *part_ids,
+                              int64_t n_part, pyas_partial *chunk_out, pyas_partial *total,
+                              uint32_t combine_flags, void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     if (!chunk_out && !total) return fail(PYAS_EINVAL, "neither chunk_out nor total given");
     if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
@@ -560,7 +566,21 @@ int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *
 
     const bool timed = ctx->timing_n < (int32_t)ctx->ev0.size();
     if (timed) PYAS_HIP(hipEventRecord(ctx->ev0[ctx->timing_n], st));
-    PYAS_HIP(pyas::launch_reduce(batch->dtype, a, shuf, bsw, masked, grid, st));
+    if (whole_ids) {
+        if (n_whole > 0) {
+            pyas::ReduceArgs w = a;
+            w.sel = nullptr;   // whole chunks: the lean kernel, no table
+            w.pool = nullptr;
+            w.ids = whole_ids;
+            PYAS_HIP(pyas::launch_reduce(batch->dtype, w, shuf, bsw, masked, n_whole * tpc, st));
+        }
+        if (n_part > 0) {
+            a.ids = part_ids;
+            PYAS_HIP(pyas::launch_reduce(batch->dtype, a, shuf, bsw, masked, n_part * tpc, st));
+        }
+    } else {
+        PYAS_HIP(pyas::launch_reduce(batch->dtype, a, shuf, bsw, masked, grid, st));
+    }
     if (timed) {
         PYAS_HIP(hipEventRecord(ctx->ev1[ctx->timing_n], st));
         ctx->timing_n++;
@@ -570,6 +590,29 @@ int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *
     if (total && !f.cnt)   // unchained: fold the group partials in a second launch
         PYAS_HIP(pyas::launch_combine(batch->dtype, f.gtmp, ng, ng, 1, 0u, total, st));
     return PYAS_OK;
+}
+
+int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                       pyas_partial *chunk_out, pyas_partial *total, uint32_t combine_flags,
+                       void *stream) {
+    return reduce_chunks_impl(ctx, batch, mask, nullptr, 0, nullptr, 0, chunk_out, total,
+                              combine_flags, stream);
+}
+
+int pyas_reduce_chunks_split(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                             const int32_t *whole_ids, int64_t n_whole, const int32_t *part_ids,
+                             int64_t n_part, pyas_partial *chunk_out, pyas_partial *total,
+                             uint32_t combine_flags, void *stream) {
+    if (!batch) return fail(PYAS_EINVAL, "batch is NULL");
+    if (!batch->sel) return fail(PYAS_EINVAL, "split launch needs a selection table");
+    if (mask && (mask->flags & (PYAS_MASK_TAB0 | PYAS_MASK_TAB1)))
+        return fail(PYAS_ENOTSUP, "split launch with vector mask tables");
+    if (n_whole < 0 || n_part < 0 || n_whole + n_part != batch->n_chunks)
+        return fail(PYAS_EINVAL, "%lld + %lld chunk ids for %lld chunks", (long long)n_whole,
+                    (long long)n_part, (long long)batch->n_chunks);
+    if ((n_whole && !whole_ids) || (n_part && !part_ids)) return fail(PYAS_EINVAL, "NULL chunk id list");
+    return reduce_chunks_impl(ctx, batch, mask, whole_ids ? whole_ids : part_ids, n_whole, part_ids,
+                              n_part, chunk_out, total, combine_flags, stream);
 }
 
 // Dense partial-axis geometry: merge the chunk dims into runs of reduced /

@@ -26,6 +26,8 @@ struct ReduceArgs {
     pyas_mask mask;
     MaskTab tab;
     pyas_partial *out;                // one partial per workgroup (tile)
+    const int32_t *ids;               // chunk ids of this launch (pyas_reduce_chunks_split); NULL:
+                                      // workgroup b reduces tile b of chunk b / tpc
 };
 
 // Chunks per first-level combine group: one k_finish block, one thread per

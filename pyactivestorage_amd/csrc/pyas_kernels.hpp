@@ -486,11 +486,15 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinishArgs f) {
 // ---------------------------------------------------------------------------
 // SEL = false: every chunk fully selected (batch.sel == NULL) -> a lean
 // streaming-only kernel (no selection state, high occupancy).
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL>
+// IDS: the launch covers the chunks listed in a.ids (pyas_reduce_chunks_split);
+// tile partials still land at their chunk's place, so k_finish is unchanged.
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL, bool IDS = false>
 __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
     const int64_t b = blockIdx.x;
-    const int64_t c = b / a.tpc;
-    const int64_t t = b - c * a.tpc;
+    const int64_t cb = b / a.tpc;
+    const int64_t t = b - cb * a.tpc;
+    const int64_t c = IDS ? (int64_t)a.ids[cb] : cb;
+    pyas_partial *const tout = a.out + (IDS ? c * a.tpc + t : b);
     const uint8_t *base = a.data + a.offsets[c];
     MaskT<T> mk;
     if constexpr (MASKED) mk.init(a.mask);
@@ -506,7 +510,7 @@ __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
             else
                 run_plain<T, BSWAP, MASKED>(base, e0, e1, acc, mk);
         }
-        tile_finish(acc, (!MASKED && e0 < e1) ? (uint64_t)(e1 - e0) : 0u, a.out + b);
+        tile_finish(acc, (!MASKED && e0 < e1) ? (uint64_t)(e1 - e0) : 0u, tout);
         return;
     }
     Sel s;
@@ -579,7 +583,7 @@ __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
     }
     // unmasked contiguous tiles count every element; the generic path counts itself
     const uint64_t extra = (!MASKED && !generic && e0 < e1) ? (uint64_t)(e1 - e0) : 0u;
-    tile_finish(acc, extra, a.out + b);
+    tile_finish(acc, extra, tout);
 }
 
 // Every chunk whole (batch.sel == NULL), 4-/8-byte dtypes: the lean
@@ -598,12 +602,18 @@ __global__ __launch_bounds__(kBlock) PYAS_WAVES_ATTR void k_reduce(ReduceArgs a)
     reduce_body<T, SHUF, BSWAP, MASKED, false>(a);
 }
 
+// k_reduce over the whole chunks of a selection batch (pyas_reduce_chunks_split)
+template <typename T, bool SHUF, bool BSWAP, int MASKED>
+__global__ __launch_bounds__(kBlock) PYAS_WAVES_ATTR void k_reduce_ids(ReduceArgs a) {
+    reduce_body<T, SHUF, BSWAP, MASKED, false, true>(a);
+}
+
 // Uncapped: per-chunk selections (hyperslabs, strides, lists), where the cap
 // spills (C5 measured 46 % slower), and 1-/2-byte dtypes (16 or 8 values per
 // 16-B load also spill under the cap).  Keeps the compiler's allocation.
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL, bool IDS = false>
 __global__ __launch_bounds__(kBlock) void k_reduce_u(ReduceArgs a) {
-    reduce_body<T, SHUF, BSWAP, MASKED, SEL>(a);
+    reduce_body<T, SHUF, BSWAP, MASKED, SEL, IDS>(a);
 }
 
 // LDS writes of a wave visible to its other lanes (no block barrier)
@@ -2615,14 +2625,16 @@ inline int mask_mode(const pyas_mask &m, bool masked) {
     return kMaskAll;
 }
 
-template <typename T, bool SEL>
+template <typename T, bool SEL, bool IDS = false>
 static void launch_reduce_ts(const ReduceArgs &a, bool shuf, bool bsw, bool masked, dim3 g,
                              hipStream_t st) {
     const dim3 blk(kBlock);
 #define PYAS_L(S, B, M)                                                                \
     do {                                                                               \
         if constexpr (SEL || sizeof(T) < 4)                                            \
-            hipLaunchKernelGGL((k_reduce_u<T, S, B, M, SEL>), g, blk, 0, st, a);       \
+            hipLaunchKernelGGL((k_reduce_u<T, S, B, M, SEL, IDS>), g, blk, 0, st, a);  \
+        else if constexpr (IDS)                                                        \
+            hipLaunchKernelGGL((k_reduce_ids<T, S, B, M>), g, blk, 0, st, a);          \
         else hipLaunchKernelGGL((k_reduce<T, S, B, M>), g, blk, 0, st, a);             \
     } while (0)
     // the lean kernel also has variants with fewer rules (mask_mode)
@@ -2660,8 +2672,15 @@ hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool masked
     const dim3 g((unsigned)grid);
     // vector fill/missing tables are applied by the selection-aware path only
     // (a NULL table there means every chunk whole)
-    if (a.sel || a.tab.on[0] || a.tab.on[1]) launch_reduce_ts<T, true>(a, shuf, bsw, masked, g, st);
-    else launch_reduce_ts<T, false>(a, shuf, bsw, masked, g, st);
+    const bool sel = a.sel || a.tab.on[0] || a.tab.on[1];
+    if (a.ids) {   // one half of pyas_reduce_chunks_split
+        if (sel) launch_reduce_ts<T, true, true>(a, shuf, bsw, masked, g, st);
+        else launch_reduce_ts<T, false, true>(a, shuf, bsw, masked, g, st);
+    } else if (sel) {
+        launch_reduce_ts<T, true>(a, shuf, bsw, masked, g, st);
+    } else {
+        launch_reduce_ts<T, false>(a, shuf, bsw, masked, g, st);
+    }
     return hipGetLastError();
 }
 

@@ -86,6 +86,18 @@ def reduce_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, chunk_out_pt
                "pyas_reduce_chunks")
 
 
+def reduce_chunks_split(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, whole_ptr, n_whole: int,
+                        part_ptr, n_part: int, chunk_out_ptr, total_ptr, round_to_var: bool,
+                        stream) -> None:
+    """reduce_chunks as two launches: whole chunks on the lean kernel, the
+    rest on the selection-aware one (pyas_reduce_chunks_split)."""
+    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
+    _lib.check(ctx.lib.pyas_reduce_chunks_split(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
+                                                whole_ptr, int(n_whole), part_ptr, int(n_part),
+                                                chunk_out_ptr, total_ptr, flags, stream),
+               "pyas_reduce_chunks_split")
+
+
 def zero_sign_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, which: int, partials_ptr,
                      stream) -> bool:
     """NumPy's sign of each chunk's zero min (which & 1) / max (which & 2)
