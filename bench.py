@@ -73,7 +73,7 @@ def parse(argv=None):
     p.add_argument("--extra", default="c4,c5",
                    help="comma list of configs also measured at this N with strong scaling "
                         "(reported under 'extra'; 'none' to skip)")
-    p.add_argument("--extra-steps", type=int, default=10)
+    p.add_argument("--extra-steps", type=int, default=20)
     p.add_argument("--cpu-chunks", type=int, default=4096,
                    help="chunks in the CPU-baseline sample (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=30)
@@ -617,7 +617,7 @@ def main():
     for name in names:
         if name not in CONFIGS:
             raise SystemExit(f"bench.py: unknown --extra config {name!r}")
-        rep, _ = run_config(env, name, "strong", args.extra_steps, 2, args)
+        rep, _ = run_config(env, name, "strong", args.extra_steps, args.warmup, args)
         rep.pop("check", None)
         extra[f"{name}_strong"] = rep
 
