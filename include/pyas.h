@@ -240,6 +240,8 @@ int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch,
  * whole-chunk kernel (no table reads, occupancy-capped registers), the second
  * with the selection-aware kernel; chunk_out / total are the same as from one
  * pyas_reduce_chunks call (same per-chunk arithmetic, same k_finish order).
+ * The two id lists must partition 0..n_chunks-1 (the device trusts them,
+ * as it trusts the selection table; ReductionPlan builds them on the host).
  * n_whole + n_part must equal n_chunks; no vector mask tables.  Replaces the
  * same call as pyas_reduce_chunks (storage.py:8-104 over a box query whose
  * interior chunks are whole, active.py:557-598). */

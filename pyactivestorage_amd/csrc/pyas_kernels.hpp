@@ -2713,7 +2713,8 @@ hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int
                                  int64_t n_layers, uint32_t flags, pyas_partial *out,
                                  hipStream_t st) {
     const dim3 blk(kBlock);
-    if (n_layers >= kCombineWaveMinLayers && n_out <= kCombineWaveMaxOut && !(flags & kCombineThreadOnly)) {
+    if (n_layers >= kCombineWaveMinLayers && n_layers < (int64_t(1) << 31) && n_out <= kCombineWaveMaxOut &&
+        !(flags & kCombineThreadOnly)) {   // (the wave form decodes layer ids in 32 bits)
         constexpr int64_t wpb = kBlock / kWave;
         const dim3 grid((unsigned)((n_out + wpb - 1) / wpb));
         hipLaunchKernelGGL((k_combine_grid_wave<T>), grid, blk, 0, st, in, g, n_out, n_layers, flags, out);
