@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PYAS_ABI_VERSION 1
+#define PYAS_ABI_VERSION 2
 #define PYAS_MAX_DIMS 8
 
 typedef enum {
@@ -171,39 +171,63 @@ int pyas_ctx_set_chained_combine(pyas_ctx *ctx, int32_t on);
 int pyas_ctx_set_fold_min_blocks(pyas_ctx *ctx, int64_t n);
 
 /* ---- NumPy's sign of a zero min/max -------------------------------------
- * storage.py:99-100 returns np.ma.min/max of a chunk's selected, masked
- * elements, and active.py:598 reduces the per-chunk results the same way.
- * When that extreme is zero and +0.0 and -0.0 both occur, the zero NumPy
- * returns is decided by its reduction loop: one accumulator per SIMD lane
- * seeded with the running result (a later element wins a tie in its lane),
- * a fixed lane tree, a scalar remainder (later wins), over the flattened
- * C-ordered data in pieces of np.getbufsize() elements after the seeding
- * first element.  The lane count and tree depend on the SIMD target NumPy
- * dispatches on the host, so the host derives them from NumPy
- * (pyactivestorage_amd/zerosign.py) and sets them per float dtype:
- *   lanes 1..64, piece >= 1, rank[lane] = priority (0 = wins every tie). */
+ * storage.py:99-100 returns np.ma.min/max(chunk[sel], axis, keepdims=True),
+ * and active.py:594 reduces the `out` array of per-chunk results the same
+ * way.  When an extreme is zero and +0.0 and -0.0 both occur, the zero NumPy
+ * returns is decided by the order its reduction visits the elements
+ * (pyactivestorage_amd/zerosign.py states the measured rules): the iterator
+ * walks the reduced array in memory order; every run of the trailing
+ * reduced dims is one call of the reduce loop, cut into pieces of
+ * np.getbufsize() elements; a contiguous call keeps one accumulator per SIMD
+ * lane seeded with the running result (later wins in a lane, lanes folded
+ * in a fixed priority, then a scalar remainder); a strided call keeps `acc`
+ * accumulators seeded with its first elements; an elementwise loop (kept
+ * innermost dim) lets every later zero win.  The lane counts and priorities
+ * depend on the SIMD target NumPy dispatches on the host, so the host derives
+ * them from NumPy and sets them per float dtype:
+ *   lanes 1..64, piece 1..2^24, rank[lane] = priority (0 wins every tie),
+ *   acc 1..64 accumulators of the strided loop, acc_rank likewise. */
 typedef struct {
     int32_t lanes;
     int32_t piece;
+    int32_t acc;
     uint8_t rank[64];
+    uint8_t acc_rank[64];
 } pyas_tie_rule;
 /* dtype PYAS_F32 or PYAS_F64; rule NULL clears it (no sign rewriting). */
 int pyas_ctx_set_tie_rule(pyas_ctx *ctx, int32_t dtype, const pyas_tie_rule *rule);
-/* For every chunk c of `batch` (float dtypes; others: no-op) whose
- * partials[c] (device) has count > 0 and a zero min (which bit 0) / max
- * (bit 1): rewrite that zero's sign as NumPy's over the chunk's selected
- * elements in C order (masked elements never tie).  No-op without a rule.
- * PYAS_ENOTSUP when a chunk's selection exceeds the kernel's table (more
- * than ~60 KiB of (pieces x (lanes + 1)) slots). */
-int pyas_zero_sign_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, uint32_t which,
-                          pyas_partial *partials, void *stream);
-/* The same over a sequence: `total` (device) is the combine of partials[0,
- * n) (device, in the reference's `out` C order; count == 0 = masked); when
- * its min / max is zero, rewrite the sign as np.ma.min/max over the
- * per-chunk values would leave it (active.py:598). */
-int pyas_zero_sign_seq(pyas_ctx *ctx, int32_t dtype, const pyas_partial *partials, int64_t n,
-                       uint32_t which, pyas_partial *total, void *stream);
 
+/* How NumPy walks chunk[sel] (after mask_missing) for one query:
+ * perm = chunk dims (the batch's dim order) from outer to inner in memory;
+ * PYAS_TIE_VIEW: the array is the chunk[sel] view itself (no mask attribute
+ * and slices only), so its strides are step * chunk stride; otherwise it is
+ * a copy, contiguous in perm order; PYAS_TIE_BUFFERED: non-native byte
+ * order (NumPy reduces through a contiguous buffer). */
+#define PYAS_TIE_VIEW 1u
+#define PYAS_TIE_BUFFERED 2u
+typedef struct {
+    int32_t perm[PYAS_MAX_DIMS];
+    uint32_t flags;
+} pyas_tie_geom;
+
+/* Level 1, per chunk (storage.py:99-100): for every output of every chunk of
+ * `batch` (the chunk's selection reduced over the dims in axes_mask; outputs
+ * row-major over the kept selected dims, at partials[out_offsets[c] + o], or
+ * partials[c] when out_offsets is NULL) whose partial has count > 0 and a
+ * zero min (which bit 0) / max (bit 1): rewrite that zero's sign as NumPy's
+ * (masked elements never tie).  Float dtypes only; a no-op without a rule. */
+int pyas_tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                    const pyas_tie_geom *geom, uint32_t axes_mask, uint32_t which,
+                    const int64_t *out_offsets, pyas_partial *partials, void *stream);
+/* Level 1 for a result folded without per-chunk partials
+ * (pyas_reduce_axes_grid): when any of the n_final partials in `final_`
+ * has a zero min/max (which: 1 or 2), write one byte per chunk output to
+ * flags[out_offsets[c] + o] (bit 0: the output holds an unmasked zero, bit
+ * 1: the sign NumPy's reduction of it returns); otherwise write nothing. */
+int pyas_tie_chunk_flags(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                         const pyas_tie_geom *geom, uint32_t axes_mask, uint32_t which,
+                         const int64_t *out_offsets, const pyas_partial *final_, int64_t n_final,
+                         uint8_t *flags, void *stream);
 /* ---- memory helpers (so a non-torch host can drive the ABI) ------------- */
 int pyas_malloc(pyas_ctx *ctx, size_t nbytes, void **dptr);
 int pyas_free(pyas_ctx *ctx, void *dptr);
@@ -233,24 +257,6 @@ int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch,
                        const pyas_mask *mask, pyas_partial *chunk_out,
                        pyas_partial *total, uint32_t combine_flags,
                        void *stream);
-
-/* pyas_reduce_chunks for a selection batch (sel != NULL) whose chunks split
- * into wholly selected ones (whole_ids, device int32, n_whole entries) and
- * the rest (part_ids): two reduce launches, the first with the lean
- * whole-chunk kernel (no table reads, occupancy-capped registers), the second
- * with the selection-aware kernel; chunk_out / total are the same as from one
- * pyas_reduce_chunks call (same per-chunk arithmetic, same k_finish order).
- * The two id lists must partition 0..n_chunks-1 (the device trusts them,
- * as it trusts the selection table; ReductionPlan builds them on the host).
- * n_whole + n_part must equal n_chunks; no vector mask tables.  Replaces the
- * same call as pyas_reduce_chunks (storage.py:8-104 over a box query whose
- * interior chunks are whole, active.py:557-598). */
-int pyas_reduce_chunks_split(pyas_ctx *ctx, const pyas_batch *batch,
-                             const pyas_mask *mask, const int32_t *whole_ids,
-                             int64_t n_whole, const int32_t *part_ids,
-                             int64_t n_part, pyas_partial *chunk_out,
-                             pyas_partial *total, uint32_t combine_flags,
-                             void *stream);
 
 /* Partial-axis reduction: for chunk c the selected block is reduced over the
  * chunk dims whose bit is set in axes_mask; outputs (row-major over the
@@ -343,6 +349,34 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
 int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
                           const pyas_grid *grid, uint32_t combine_flags, pyas_partial *out,
                           void *stream);
+
+/* ---- NumPy's sign of a zero min/max, level 2 (see pyas_tie_chunks) ---- */
+/* Level 2, across chunks (active.py:594): every final output f (partials
+ * final_, device) whose min (which 1) / max (which 2) is a zero gets the sign
+ * NumPy's reduction of the `out` array returns.  The chunk layers of f are
+ * walked as pyas_combine_grid walks them; layer l's value comes from the
+ * level-1 partials (`parts`, pyas_reduce_axes layout) or flag bytes
+ * (`flags`).  lr: the length of one reduce call over `out` (the product of
+ * its trailing reduced extents, 1 when its innermost non-1 dim is kept).
+ * keys NULL: the sign is written to final_; else K1 keys are folded into
+ * keys[f] (max) and W keys into keys[n_out + f] (min), for ranks of a group
+ * to combine with pyas_tie_finalize (keys set up by pyas_tie_keys_reset). */
+int pyas_tie_grid(pyas_ctx *ctx, int32_t dtype, const pyas_grid *grid, const pyas_partial *parts,
+                  const uint8_t *flags, int64_t lr, uint32_t which, pyas_partial *final_,
+                  uint64_t *keys, void *stream);
+/* Level 2 over segments (pyas_combine_segments' layout: layer k of output s
+ * is parts[index[seg[s] + k]]), or, with index == seg == NULL, one output
+ * whose layers are parts[0 .. n_layers) (a full reduction; n_seg == 1).
+ * Layer k sits at reduced position layer_base + k (a rank's first chunk). */
+int pyas_tie_segments(pyas_ctx *ctx, int32_t dtype, const pyas_partial *parts, const int64_t *index,
+                      const int64_t *seg, int64_t n_seg, int64_t n_layers, int64_t layer_base,
+                      int64_t lr, uint32_t which, pyas_partial *final_, uint64_t *keys, void *stream);
+/* keys (device, 2 * n_out): K1 = 0, W = all ones. */
+int pyas_tie_keys_reset(pyas_ctx *ctx, uint64_t *keys, int64_t n_out, void *stream);
+/* Combine n_sets key arrays (device, n_sets x [K1[n_out], W[n_out]]) and
+ * write the signs into final_'s zero min/max. */
+int pyas_tie_finalize(pyas_ctx *ctx, int32_t dtype, const uint64_t *keys, int64_t n_out, int32_t n_sets,
+                      int64_t lr, uint32_t which, pyas_partial *final_, void *stream);
 
 /* Result formatting on the device: the last step of Active._from_storage
  * (active.py:591-630) applied to n combined partials (device), so that only
@@ -446,6 +480,8 @@ typedef struct {
     int32_t zlib;                      /* 1: the file bytes are one zlib stream
                                           (hdf2numcodec.py:34-35, storage.py:119-120) */
     uint32_t axes_mask;                /* chunk dims reduced (all dims: one partial) */
+    uint32_t tie_which;                /* NumPy's zero sign for min (1) / max (2): pyas_tie_chunks */
+    pyas_tie_geom tie;
 } pyas_chunk_desc;
 
 typedef struct pyas_coalescer pyas_coalescer;

@@ -12,7 +12,7 @@ import os
 import threading
 
 MAX_DIMS = 8
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # pyas_status
 OK, EINVAL, ENOTSUP, EDEVICE, ENOMEM, EINDEX, EIO = range(7)
@@ -89,6 +89,14 @@ class Scatter(ctypes.Structure):
     ]
 
 
+class TieGeom(ctypes.Structure):
+    """pyas_tie_geom: how NumPy walks chunk[sel] (zerosign.geometry)."""
+    _fields_ = [
+        ("perm", ctypes.c_int32 * MAX_DIMS),
+        ("flags", ctypes.c_uint32),
+    ]
+
+
 class ChunkDesc(ctypes.Structure):
     """pyas_chunk_desc: one chunk's layout for pyas_coalesced_reduce."""
     _fields_ = [
@@ -99,6 +107,8 @@ class ChunkDesc(ctypes.Structure):
         ("chunk_shape", ctypes.c_int64 * MAX_DIMS),
         ("zlib", ctypes.c_int32),
         ("axes_mask", ctypes.c_uint32),
+        ("tie_which", ctypes.c_uint32),
+        ("tie", TieGeom),
     ]
 
 
@@ -107,7 +117,9 @@ class TieRule(ctypes.Structure):
     _fields_ = [
         ("lanes", ctypes.c_int32),
         ("piece", ctypes.c_int32),
+        ("acc", ctypes.c_int32),
         ("rank", ctypes.c_uint8 * 64),
+        ("acc_rank", ctypes.c_uint8 * 64),
     ]
 
 
@@ -132,8 +144,14 @@ SIGNATURES = {
     "pyas_ctx_set_chained_combine": [_vp, _i32],
     "pyas_ctx_set_fold_min_blocks": [_vp, _i64],
     "pyas_ctx_set_tie_rule": [_vp, _i32, ctypes.POINTER(TieRule)],
-    "pyas_zero_sign_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _u32, _vp, _vp],
-    "pyas_zero_sign_seq": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
+    "pyas_tie_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(TieGeom), _u32, _u32,
+                        _vp, _vp, _vp],
+    "pyas_tie_chunk_flags": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(TieGeom), _u32,
+                             _u32, _vp, _vp, _i64, _vp, _vp],
+    "pyas_tie_grid": [_vp, _i32, ctypes.POINTER(Grid), _vp, _vp, _i64, _u32, _vp, _vp, _vp],
+    "pyas_tie_segments": [_vp, _i32, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _u32, _vp, _vp, _vp],
+    "pyas_tie_keys_reset": [_vp, _vp, _i64, _vp],
+    "pyas_tie_finalize": [_vp, _i32, _vp, _i64, _i32, _i64, _u32, _vp, _vp],
     "pyas_malloc": [_vp, _sz, ctypes.POINTER(_vp)],
     "pyas_free": [_vp, _vp],
     "pyas_host_alloc": [_vp, _sz, ctypes.POINTER(_vp)],
@@ -145,8 +163,6 @@ SIGNATURES = {
     "pyas_stream_synchronize": [_vp, _vp],
     "pyas_stream_wait": [_vp, _vp, _vp],
     "pyas_reduce_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _u32, _vp],
-    "pyas_reduce_chunks_split": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _i64, _vp, _i64,
-                                 _vp, _vp, _u32, _vp],
     "pyas_reduce_axes": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _u32, _vp, _vp, _vp],
     "pyas_select_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _vp, _vp],
     "pyas_select_scatter": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(Scatter),
@@ -197,7 +213,7 @@ def load(path: str | None = None):
             fn.argtypes = argtypes
             fn.restype = ctypes.c_char_p if name == "pyas_last_error" else ctypes.c_int
         if lib.pyas_abi_version() != ABI_VERSION:
-            raise RuntimeError("pyactivestorage_amd: ABI version mismatch with " + p)
+            raise RuntimeError("pyactivestorage_amd: ABI version mismatch with " + p + " (rebuild it)")
         if path is None:
             _lib = lib
         return lib

@@ -33,7 +33,7 @@ import threading
 
 import numpy as np
 
-from . import _lib, engine, selection
+from . import _lib, engine, selection, zerosign
 from .batch import ReductionPlan, _all_full
 from .device import DeviceBuffer, get_context
 from .dtypes import native, sum_dtype
@@ -106,8 +106,15 @@ class _CachedQuery:
         self.final_shape = final_shape
         self.grid = grid            # None: full reduction; else _grid_partials' record
         self.fmt = {}               # format buffers by result dtype / components
+        # one replay at a time: the plan's device buffers (partials, total,
+        # tie flags, result buffers) are shared by every replay of this key
+        self.lock = threading.Lock()
 
     def run(self, act):
+        with self.lock:
+            return self._run(act)
+
+    def _run(self, act):
         ctx = self.plan.ctx
         st = ctx.thread_stream()
         shape = self.final_shape
@@ -122,6 +129,7 @@ class _CachedQuery:
             engine.reduce_axes(ctx, self.plan.batch, self.plan.mask_up.struct, g["axes_mask"], g["obuf"].ptr,
                                g["parts"].ptr, st)
             engine.combine_grid(ctx, act.ds.dtype, g["parts"].ptr, g["g"], g["fin"].ptr, True, st)
+        act._tie_grid(ctx, st, self.plan, g)
         return act._format_device(ctx, st, g["fin"], g["n_final"], shape, bufs=self.fmt)
 
 
@@ -620,6 +628,7 @@ class Active:
             from .distributed import shard_ranges
             weights = np.prod(table[:, :ds.ndim, 2].astype(np.int64), axis=1)
             lo, hi = shard_ranges(weights, dist.get_world_size(self.group))[dist.get_rank(self.group)]
+        keys = [] if self.group is not None else None
         if hi > lo:
             ctx, st, buf, offsets, fused = self._ingest(coords[lo:hi], compressor, filters)
             sub = table[lo:hi]
@@ -629,7 +638,7 @@ class Active:
                                  missing=self.missing, round_to_var=True, stream=st)
             cacheable = cache_key is not None and self.resident and self.group is None
             if len(axes) == ds.ndim:
-                final = self._total(plan, st)
+                final = self._total(plan, st, layer_base=lo, n_layers=n, keys=keys)
                 if cacheable:
                     self._remember(cache_key, _CachedQuery(plan, final_shape))
             else:
@@ -641,49 +650,106 @@ class Active:
                     if cacheable:
                         self._remember(cache_key, _CachedQuery(plan, final_shape, rec))
                     return out
-                final = self._grid_partials(ctx, st, plan, grid, axes, final_shape, lo, hi)
+                final = self._grid_partials(ctx, st, plan, grid, axes, final_shape, lo, hi, keys=keys)
         else:
             final = np.zeros(n_final, dtype=pdt)   # count 0: neutral in every combine
         if self.group is not None:
-            final = self._exchange(final)
+            if not keys:   # no chunks here, or no zero-sign work: neutral keys
+                keys = [np.concatenate([np.zeros(n_final, np.uint64), np.full(n_final, ~np.uint64(0))])]
+            lr = n if len(axes) == ds.ndim else \
+                zerosign.grid_lr([len(dims[d]) if d in axes else final_shape[d] for d in range(ds.ndim)],
+                                 set(axes))
+            final = self._exchange(final, keys[0], lr)
         return self._format(final.reshape(final_shape), final_shape)
 
-    def _total(self, plan, st):
+    def _tie_which(self) -> int:
+        """1 / 2 when the query's min / max of a float variable must give
+        NumPy's sign of a zero extreme (pyas_tie_*), else 0."""
+        if self.ds.dtype.kind != "f":
+            return 0
+        return {"min": 1, "max": 2}.get(self._method, 0)
+
+    def _total(self, plan, st, layer_base=0, n_layers=None, keys=None):
         """Full reduction of the plan's chunks: the combined partial.  For
         min/max of a float variable the chunk partials are kept so that a
         zero extreme gets NumPy's sign: per chunk over its elements
-        (storage.py:99-100), then over the per-chunk values in the `out`
-        array's C order (active.py:598) -- pyas_zero_sign_chunks / _seq.
-        (Across a torch.distributed group the rank combine keeps the sign the
-        ranks' totals carry.)"""
-        zs = self._method in ("min", "max") and self.ds.dtype.kind == "f" and self.group is None
-        plan.launch(st, chunk_partials=zs)
-        if zs:
-            which = 1 if self._method == "min" else 2
-            if engine.zero_sign_chunks(plan.ctx, plan.batch, plan.mask_up.struct, which,
-                                       plan.chunk_partials.ptr, st):
-                engine.zero_sign_seq(plan.ctx, self.ds.dtype, plan.chunk_partials.ptr, plan.n_chunks, which,
-                                     plan.total.ptr, st)
+        (storage.py:99-100, pyas_tie_chunks), then over the per-chunk values
+        in the `out` array's C order (active.py:594, pyas_tie_segments).
+        Under a group the plan holds this rank's chunks, the first at
+        position ``layer_base`` of the ``n_layers`` in the query, and the
+        level-2 keys go to ``keys`` (a host list) for pyas_tie_finalize
+        after the exchange."""
+        which = self._tie_which()
+        plan.launch(st, chunk_partials=bool(which))
+        if which:
+            ctx, dt = plan.ctx, self.ds.dtype
+            n_all = plan.n_chunks if n_layers is None else int(n_layers)
+            engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, plan.tie_geom(), (1 << self.ds.ndim) - 1,
+                              which, None, plan.chunk_partials.ptr, st)
+            kbuf = None
+            if keys is not None:
+                kbuf = DeviceBuffer(ctx, 16)
+                engine.tie_keys_reset(ctx, kbuf.ptr, 1, st)
+            # `out` is one coordinate per chunk and every dim reduced: one call of n_all
+            engine.tie_segments(ctx, dt, plan.chunk_partials.ptr, None, None, 1, plan.n_chunks, int(layer_base),
+                                max(n_all, 1), which, plan.total.ptr, kbuf.ptr if kbuf else None, st)
+            if kbuf is not None:
+                host = np.zeros(2, dtype=np.uint64)
+                ctx.d2h(host, kbuf.ptr, st)
+                ctx.synchronize(st)
+                keys.append(host)
         return plan.read_total(st)
 
-    def _exchange(self, final):
+    def _tie_grid(self, ctx, st, plan, rec, keys_ptr=None):
+        """NumPy's sign of the zero min/max outputs of a partial-axis box
+        query (``rec``: _grid_partials' record): per chunk output
+        (storage.py:99-100), then over the chunk layers of the `out` array
+        (active.py:594)."""
+        which = self._tie_which()
+        if not which:
+            return
+        t = rec["tie"]
+        dt = self.ds.dtype
+        geom = plan.tie_geom()
+        if rec["folded"]:   # no per-chunk partials: per chunk output flags
+            if t.get("flags") is None:
+                t["flags"] = DeviceBuffer(ctx, max(t["n_parts"], 1))
+            engine.tie_chunk_flags(ctx, plan.batch, plan.mask_up.struct, geom, rec["axes_mask"], which,
+                                   rec["obuf"].ptr, rec["fin"].ptr, rec["n_final"], t["flags"].ptr, st)
+            engine.tie_grid(ctx, dt, rec["g"], None, t["flags"].ptr, t["lr"], which, rec["fin"].ptr, keys_ptr, st)
+        else:
+            engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, geom, rec["axes_mask"], which,
+                              rec["obuf"].ptr, rec["parts"].ptr, st)
+            engine.tie_grid(ctx, dt, rec["g"], rec["parts"].ptr, None, t["lr"], which, rec["fin"].ptr, keys_ptr,
+                            st)
+
+    def _exchange(self, final, keys=None, lr=1):
         """All-gather the per-rank partial grids (RCCL for an nccl group,
         else over the group's CPU backend) and fold them in rank order on
-        the device (pyas_combine_segments).  Every rank gets the result."""
+        the device (pyas_combine_segments).  ``keys``: this rank's zero-sign
+        keys (2 x n uint64), gathered in the same collective and combined
+        by pyas_tie_finalize, so a zero min/max carries NumPy's sign over
+        the whole `out` array (active.py:594).  Every rank gets the result."""
         import torch
         import torch.distributed as dist
         world = dist.get_world_size(self.group)
-        if world == 1:
-            return final
-        dev = torch.device("cuda", torch.cuda.current_device()) \
-            if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
-        t = torch.from_numpy(np.ascontiguousarray(final).view(np.uint8).copy()).to(dev)
-        parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t, group=self.group)
-        gathered = np.concatenate([p.cpu().numpy() for p in parts])
+        which = self._tie_which() if keys is not None else 0
         n = final.size
         ctx = get_context(self.device)
         st = ctx.thread_stream()
+        if world == 1 and not which:
+            return final
+        dev = torch.device("cuda", torch.cuda.current_device()) \
+            if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        blob = np.ascontiguousarray(final).view(np.uint8).reshape(-1)
+        if which:
+            blob = np.concatenate([blob, np.ascontiguousarray(keys, dtype=np.uint64).view(np.uint8)])
+        t = torch.from_numpy(blob.copy()).to(dev)
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=self.group)
+        host = [p.cpu().numpy() for p in parts]
+        gathered = np.concatenate([h[:final.nbytes] for h in host]).view(final.dtype)
+        gkeys = np.concatenate([h[final.nbytes:] for h in host]).view(np.uint64) if which else None
         index = (np.arange(world, dtype=np.int64)[None, :] * n
                  + np.arange(n, dtype=np.int64)[:, None]).reshape(-1)
         seg = np.arange(n + 1, dtype=np.int64) * world
@@ -695,6 +761,10 @@ class Active:
         fin = DeviceBuffer(ctx, max(n, 1) * _lib.PARTIAL_NBYTES)
         engine.combine_segments(ctx, self.ds.dtype, gbuf.ptr, mbuf.ptr, mbuf.ptr + 8 * index.size, n,
                                 fin.ptr, False, st)
+        if which:
+            kb = DeviceBuffer(ctx, gkeys.nbytes)
+            ctx.h2d(kb.ptr, gkeys, st)
+            engine.tie_finalize(ctx, self.ds.dtype, kb.ptr, n, world, lr, which, fin.ptr, st)
         out = np.zeros(n, dtype=final.dtype)
         ctx.d2h(out, fin.ptr, st)
         ctx.synchronize(st)
@@ -705,13 +775,16 @@ class Active:
         return self._grid_partials(ctx, st, plan, grid, axes, final_shape, 0, plan.n_chunks,
                                    formatted=True)
 
-    def _grid_partials(self, ctx, st, plan, grid, axes, final_shape, lo, hi, formatted=False, rec=None):
+    def _grid_partials(self, ctx, st, plan, grid, axes, final_shape, lo, hi, formatted=False, rec=None,
+                       keys=None):
         """Per-chunk partial arrays of chunks [lo, hi) of the box query
         (pyas_reduce_axes over ``plan``), then pyas_combine_grid into the
         final grid; chunks outside [lo, hi) read a zeroed (count 0, neutral)
         partial region.  ``formatted``: return the formatted result
         (``_format_device``) instead of the host partials.  ``rec``: filled
-        with what a replay of this query needs (_CachedQuery)."""
+        with what a replay of this query needs (_CachedQuery).  ``keys``
+        (group queries): a host list that receives this rank's zero-sign
+        keys of every output (pyas_tie_grid), for pyas_tie_finalize."""
         ds = self.ds
         dt = ds.dtype
         n_final = int(np.prod(final_shape))
@@ -764,9 +837,21 @@ class Active:
                 ctx.h2d(parts.ptr + n_parts * _lib.PARTIAL_NBYTES, zeros, st)
             engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st)
             engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st)
-        if rec is not None:
-            rec.update(folded=folded, g=g, fin=fin, obuf=obuf, abuf=abuf, tbuf=tbuf, parts=parts,
-                       axes_mask=axes_mask, n_final=n_final)
+        ext = [tables["n_coords"][d] if d in axes else final_shape[d] for d in range(ds.ndim)]
+        r = rec if rec is not None else {}
+        r.update(folded=folded, g=g, fin=fin, obuf=obuf, abuf=abuf, tbuf=tbuf, parts=parts,
+                 axes_mask=axes_mask, n_final=n_final,
+                 tie={"lr": zerosign.grid_lr(ext, set(axes)), "n_parts": n_parts_all, "flags": None})
+        if keys is not None and self._tie_which():
+            kbuf = DeviceBuffer(ctx, max(n_final, 1) * 16)
+            engine.tie_keys_reset(ctx, kbuf.ptr, n_final, st)
+            self._tie_grid(ctx, st, plan, r, kbuf.ptr)
+            host = np.zeros(2 * n_final, dtype=np.uint64)
+            ctx.d2h(host, kbuf.ptr, st)
+            ctx.synchronize(st)
+            keys.append(host)
+        else:
+            self._tie_grid(ctx, st, plan, r)
         if formatted:
             return self._format_device(ctx, st, fin, n_final, final_shape)
         final = np.zeros(n_final, dtype=engine.partial_dtype(dt))
@@ -870,6 +955,15 @@ class Active:
         engine.combine_segments(ctx, dt, parts.ptr, mbuf.ptr + 8 * len(chunk_list),
                                 mbuf.ptr + 8 * (len(chunk_list) + order.size), n_final, fin.ptr,
                                 True, st)
+        which = self._tie_which()
+        if which:   # NumPy's zero sign: per chunk output, then over each segment's layers
+            engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, plan.tie_geom(), axes_mask, which, mbuf.ptr,
+                              parts.ptr, st)
+            ncoord = [len({cc[d] for cc, _ in chunk_list}) for d in range(ds.ndim)]
+            lr = zerosign.grid_lr([ncoord[d] if d in axes else final_shape[d] for d in range(ds.ndim)], set(axes))
+            engine.tie_segments(ctx, dt, parts.ptr, mbuf.ptr + 8 * len(chunk_list),
+                                mbuf.ptr + 8 * (len(chunk_list) + order.size), n_final, int(np.diff(seg).max()),
+                                0, lr, which, fin.ptr, None, st)
         final = np.zeros(n_final, dtype=pdt)
         ctx.d2h(final, fin.ptr, st)
         ctx.synchronize(st)

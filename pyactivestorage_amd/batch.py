@@ -11,11 +11,10 @@ be timed or captured.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 
-from . import _lib, engine, selection
+from . import _lib, engine, selection, zerosign
 from .device import Context, DeviceBuffer
 from .dtypes import native
 from .masking import compile_missing
@@ -54,9 +53,9 @@ class ReductionPlan:
         st = stream
         self.offsets_buf = self._upload(offsets, st)
         sel_ptr = pool_ptr = None
-        self.split = None        # (whole ids ptr, n, other ids ptr, n): pyas_reduce_chunks_split
         table = None
         sel_shape, kept = self.chunk_shape, tuple(range(len(self.chunk_shape)))
+        self._sel0 = None        # a chunk's selection, for tie_geom
         if selections is not None:
             if len(selections) != self.n_chunks:
                 raise ValueError("one selection per chunk is required")
@@ -73,6 +72,7 @@ class ReductionPlan:
                 raise NotImplementedError("vector fill/missing values need equal selection shapes")
             if selections:
                 sel_shape, kept = selections[0].shape, selections[0].kept
+                self._sel0 = selections[0]
         elif sel_table is not None:
             # pre-packed ABI table (int32 [n, MAX_DIMS, 3]) for large planned queries
             table = np.ascontiguousarray(sel_table, dtype=np.int32)
@@ -84,18 +84,8 @@ class ReductionPlan:
             sel_ptr = self._upload(table, st).ptr
             pool_ptr = self._upload(index_pool if index_pool is not None
                                     else np.zeros(1, dtype=np.int32), st).ptr
-        vector_tables = self.cm.tables[0] is not None or self.cm.tables[1] is not None
-        if sel_ptr is not None and not vector_tables and os.environ.get("PYAS_SPLIT_WHOLE", "0") == "1":
-            # opt-in: a box query's interior chunks are whole; reduce them with
-            # the lean kernel and only the boundary chunks with the
-            # selection-aware one (measured slower on C5: DESIGN §6.1)
-            full = _full_rows(table, self.chunk_shape)
-            n_whole = int(full.sum())
-            if 0 < n_whole < self.n_chunks:
-                whole = np.flatnonzero(full).astype(np.int32)
-                part = np.flatnonzero(~full).astype(np.int32)
-                self.split = (self._upload(whole, st).ptr, n_whole, self._upload(part, st).ptr,
-                              self.n_chunks - n_whole)
+            if self.n_chunks:
+                self._sel0 = _row_sel(table[0], self.chunk_shape, index_pool)
         self.layout = engine.Layout(self.dtype, self.chunk_shape,
                                     shuffle if (shuffle and shuffle > 1 and es > 1) else 0)
         self.batch = self.layout.batch_struct(self.n_chunks, data_ptr, self.offsets_buf.ptr,
@@ -103,6 +93,16 @@ class ReductionPlan:
         self.mask_up = engine.MaskUpload(ctx, self.cm, sel_shape, kept, st)
         self.chunk_partials = DeviceBuffer(ctx, max(self.n_chunks, 1) * _lib.PARTIAL_NBYTES)
         self.total = DeviceBuffer(ctx, _lib.PARTIAL_NBYTES)
+
+    def tie_geom(self, order="C") -> _lib.TieGeom:
+        """How NumPy walks these chunks' ``chunk[sel]`` after mask_missing
+        (``pyas_tie_geom``, zerosign.geometry): the zero-sign passes'
+        geometry."""
+        g = getattr(self, "_geom", None)
+        if g is None:
+            cs = self._sel0 or selection.normalize((slice(None),) * len(self.chunk_shape), self.chunk_shape)
+            g = self._geom = zerosign.geometry(self.chunk_shape, order, cs, self.cm.masked, self.dtype)
+        return g
 
     def _upload(self, arr, stream):
         arr = np.ascontiguousarray(arr)
@@ -117,13 +117,8 @@ class ReductionPlan:
         """Enqueue: fused reduce of every chunk -> per-chunk partials ->
         fixed-order combine into ``self.total``."""
         out = self.chunk_partials.ptr if chunk_partials else None
-        if self.split is not None:
-            w, nw, p, n_p = self.split
-            engine.reduce_chunks_split(self.ctx, self.batch, self.mask_up.struct, w, nw, p, n_p,
-                                       out, self.total.ptr, self.round_to_var, stream)
-        else:
-            engine.reduce_chunks(self.ctx, self.batch, self.mask_up.struct, out, self.total.ptr,
-                                 self.round_to_var, stream)
+        engine.reduce_chunks(self.ctx, self.batch, self.mask_up.struct, out, self.total.ptr,
+                             self.round_to_var, stream)
 
     def total_tensor(self, torch):
         """Zero-copy torch view (32 uint8) of the device total, e.g. to hand
@@ -148,12 +143,16 @@ class ReductionPlan:
         return host
 
 
-def _full_rows(table, chunk_shape) -> np.ndarray:
-    """Per chunk: whether its selection is its whole box in C order."""
-    nd = len(chunk_shape)
-    t = table[:, :nd, :]
-    return ((t[:, :, 0] == 0).all(axis=1) & (t[:, :, 1] == 1).all(axis=1)
-            & (t[:, :, 2] == np.asarray(chunk_shape, dtype=np.int32)).all(axis=1))
+def _row_sel(row, chunk_shape, pool) -> selection.ChunkSel:
+    """ChunkSel of one row of a packed selection table."""
+    dims = []
+    for d in range(len(chunk_shape)):
+        start, step, cnt = (int(x) for x in row[d])
+        if step == 0:
+            dims.append(selection.DimSel(0, 0, cnt, False, np.asarray(pool[start:start + cnt], dtype=np.int64)))
+        else:
+            dims.append(selection.DimSel(start, step, cnt, False))
+    return selection.ChunkSel(dims, tuple(d.count for d in dims), tuple(range(len(chunk_shape))))
 
 
 def _all_full(table, chunk_shape) -> bool:

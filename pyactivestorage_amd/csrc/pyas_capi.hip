@@ -75,6 +75,7 @@ struct pyas_ctx {
     pyas::Ingest *ingest = nullptr;   // pinned staging ring of pyas_read_ranges (lazy)
     std::mutex mu;
     std::unordered_map<void *, Scratch> scratch;  // keyed by stream
+    std::unordered_map<void *, Scratch> tie_scratch;  // gate word / keys of the tie passes
     // timing
     std::vector<hipEvent_t> ev0, ev1;
     int32_t timing_n = 0;
@@ -293,6 +294,8 @@ int pyas_ctx_destroy(pyas_ctx *ctx) {
         if (kv.second.ptr) (void)hipFree(kv.second.ptr);
         if (kv.second.cnt) (void)hipFree(kv.second.cnt);
     }
+    for (auto &kv : ctx->tie_scratch)
+        if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     if (ctx->ingest) pyas::ingest_destroy(ctx->ingest);
     for (auto e : ctx->ev0) (void)hipEventDestroy(e);
     for (auto e : ctx->ev1) (void)hipEventDestroy(e);
@@ -336,62 +339,254 @@ int pyas_ctx_set_tie_rule(pyas_ctx *ctx, int32_t dtype, const pyas_tie_rule *rul
     pyas::TieRule &t = ctx->tie[dtype == PYAS_F64 ? 1 : 0];
     std::memset(&t, 0, sizeof(t));
     if (!rule) return PYAS_OK;
-    if (rule->lanes < 1 || rule->lanes > 64 || rule->piece < 1)
-        return fail(PYAS_EINVAL, "tie rule: lanes %d, piece %d", rule->lanes, rule->piece);
-    bool seen[64] = {false};
-    for (int l = 0; l < rule->lanes; ++l) {
-        if (rule->rank[l] >= rule->lanes || seen[rule->rank[l]])
-            return fail(PYAS_EINVAL, "tie rule: rank is not a permutation of 0..%d", rule->lanes - 1);
-        seen[rule->rank[l]] = true;
-    }
+    if (rule->lanes < 1 || rule->lanes > 64 || rule->piece < 1 || rule->piece >= (1 << 24) || rule->acc < 1 ||
+        rule->acc > 64)
+        return fail(PYAS_EINVAL, "tie rule: lanes %d, piece %d, acc %d", rule->lanes, rule->piece, rule->acc);
+    auto perm_ok = [](const uint8_t *rank, int n) {
+        bool seen[64] = {false};
+        for (int l = 0; l < n; ++l) {
+            if (rank[l] >= n || seen[rank[l]]) return false;
+            seen[rank[l]] = true;
+        }
+        return true;
+    };
+    if (!perm_ok(rule->rank, rule->lanes) || !perm_ok(rule->acc_rank, rule->acc))
+        return fail(PYAS_EINVAL, "tie rule: a rank table is not a permutation");
     t.lanes = rule->lanes;
     t.piece = rule->piece;
+    t.acc = rule->acc;
     std::memcpy(t.rank, rule->rank, sizeof(t.rank));
+    std::memcpy(t.acc_rank, rule->acc_rank, sizeof(t.acc_rank));
     return PYAS_OK;
 }
 
 namespace {
-// LDS table of the zero-sign kernels: (pieces) x (lanes + 1) 8-byte slots
-constexpr int64_t kTieLdsMax = 60 * 1024;
-int64_t tie_lds(const pyas::TieRule &t, int64_t elems) {
-    const int64_t npieces = elems > 1 ? (elems - 1) / t.piece + 1 : 1;
-    return npieces * (t.lanes + 1) * 8;
-}
-}  // namespace
 
-int pyas_zero_sign_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, uint32_t which,
-                          pyas_partial *partials, void *stream) {
-    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
-    pyas::ReduceArgs a;
-    int es;
-    bool shuf, bsw, masked;
-    int rc = prepare(ctx, batch, mask, a, es, shuf, bsw, masked);
-    if (rc) return rc;
-    if (batch->dtype != PYAS_F32 && batch->dtype != PYAS_F64) return PYAS_OK;
-    const pyas::TieRule &t = ctx->tie[batch->dtype == PYAS_F64 ? 1 : 0];
-    if (t.lanes == 0 || batch->n_chunks == 0 || (which & 3u) == 0) return PYAS_OK;
-    if (!partials) return fail(PYAS_EINVAL, "partials is NULL");
-    const int64_t lds = tie_lds(t, a.chunk_elems);   // a selection never exceeds its chunk
-    if (lds > kTieLdsMax) return fail(PYAS_ENOTSUP, "zero-sign table for %lld elements exceeds LDS",
-                                      (long long)a.chunk_elems);
-    if (batch->n_chunks >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
-    PYAS_HIP(hipSetDevice(ctx->device));
-    PYAS_HIP(pyas::launch_zero_sign_chunks(batch->dtype, a, shuf, bsw, t, which, partials, batch->n_chunks, lds,
-                                           (hipStream_t)stream));
+const pyas::TieRule *tie_of(const pyas_ctx *ctx, int32_t dtype) {
+    if (dtype != PYAS_F32 && dtype != PYAS_F64) return nullptr;
+    const pyas::TieRule &t = ctx->tie[dtype == PYAS_F64 ? 1 : 0];
+    return t.lanes ? &t : nullptr;
+}
+
+int check_geom(const pyas_tie_geom *g, int ndim) {
+    if (!g) return fail(PYAS_EINVAL, "tie geometry is NULL");
+    uint32_t seen = 0;
+    for (int i = 0; i < ndim; ++i) {
+        const int d = g->perm[i];
+        if (d < 0 || d >= ndim || ((seen >> d) & 1u)) return fail(PYAS_EINVAL, "tie geometry: perm is not a permutation");
+        seen |= 1u << d;
+    }
+    if (g->flags & ~(PYAS_TIE_VIEW | PYAS_TIE_BUFFERED)) return fail(PYAS_EINVAL, "tie geometry: unknown flags");
     return PYAS_OK;
 }
 
-int pyas_zero_sign_seq(pyas_ctx *ctx, int32_t dtype, const pyas_partial *partials, int64_t n,
-                       uint32_t which, pyas_partial *total, void *stream) {
-    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
-    if (dtype != PYAS_F32 && dtype != PYAS_F64) return PYAS_OK;
-    const pyas::TieRule &t = ctx->tie[dtype == PYAS_F64 ? 1 : 0];
-    if (t.lanes == 0 || n <= 0 || (which & 3u) == 0) return PYAS_OK;
-    if (!partials || !total) return fail(PYAS_EINVAL, "NULL argument");
-    const int64_t lds = tie_lds(t, n);
-    if (lds > kTieLdsMax) return fail(PYAS_ENOTSUP, "zero-sign table for %lld partials exceeds LDS", (long long)n);
+// Level 1 shared by pyas_tie_chunks / pyas_tie_chunk_flags.
+int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, const pyas_tie_geom *geom,
+               uint32_t axes_mask, uint32_t which, const int64_t *out_offsets, pyas_partial *partials,
+               uint8_t *flags, const uint32_t *gate, hipStream_t st) {
+    pyas::TieChunkArgs a;
+    std::memset(&a, 0, sizeof(a));
+    int es;
+    bool shuf, bsw, masked;
+    int rc = prepare(ctx, batch, mask, a.r, es, shuf, bsw, masked);
+    if (rc) return rc;
+    if ((rc = check_geom(geom, batch->ndim))) return rc;
+    const pyas::TieRule *t = tie_of(ctx, batch->dtype);
+    if (!t || batch->n_chunks == 0 || (which & 3u) == 0) return PYAS_OK;
+    const uint32_t full = (1u << batch->ndim) - 1u;
+    if ((axes_mask & ~full) != 0) return fail(PYAS_EINVAL, "axes_mask 0x%x outside the chunk rank", axes_mask);
+    if ((axes_mask & full) != full && !out_offsets)
+        return fail(PYAS_EINVAL, "out_offsets is NULL for a partial-axis reduction");
+    int64_t kept = 1;
+    for (int d = 0; d < batch->ndim; ++d)
+        if (!((axes_mask >> d) & 1u)) kept *= batch->chunk_shape[d];
+    a.t = *t;
+    a.g = *geom;
+    a.axes = axes_mask;
+    a.which = which & 3u;
+    a.shuf = shuf;
+    a.bswap = bsw;
+    a.out_offsets = out_offsets;
+    a.parts = partials;
+    a.flags = flags;
+    a.gate = gate;
+    a.tpc = (kept + pyas::kTieTile - 1) / pyas::kTieTile;
+    const int64_t grid = batch->n_chunks * a.tpc;
+    if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "tie grid too large");
     PYAS_HIP(hipSetDevice(ctx->device));
-    PYAS_HIP(pyas::launch_zero_sign_seq(dtype, partials, n, t, which, total, lds, (hipStream_t)stream));
+    PYAS_HIP(pyas::launch_tie_chunks(batch->dtype, a, grid, st));
+    return PYAS_OK;
+}
+
+// Per-stream gate word and key scratch of the tie passes.
+int tie_scratch(pyas_ctx *ctx, void *stream, size_t bytes, void **out) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Scratch &s = ctx->tie_scratch[stream];
+    if (s.bytes < bytes) {
+        if (s.ptr) {
+            PYAS_HIP(hipStreamSynchronize((hipStream_t)stream));
+            PYAS_HIP(hipFree(s.ptr));
+            s.ptr = nullptr;
+            s.bytes = 0;
+        }
+        const size_t want = bytes < 4096 ? 4096 : bytes;
+        PYAS_HIP(hipMalloc(&s.ptr, want));
+        s.bytes = want;
+    }
+    *out = s.ptr;
+    return PYAS_OK;
+}
+
+pyas::TieCall grid_call(const pyas::TieRule &t, int64_t lr) {
+    pyas::TieCall c;
+    c.acc = 0;
+    c.block = 0;
+    c.n_copy = 0;
+    c.lr = lr < 1 ? 1 : lr;
+    c.npr = (c.lr + t.piece - 1) / t.piece;
+    return c;
+}
+
+// Level 2: one wave per (output, layer slice); several slices per output
+// fold their keys through `keys` (or an internal buffer + finalize).
+int tie_level2(pyas_ctx *ctx, int32_t dtype, pyas::TieGridArgs &a, int64_t max_layers, uint64_t *keys,
+               hipStream_t st) {
+    const pyas::TieRule *t = tie_of(ctx, dtype);
+    if (!t || a.n_out <= 0 || max_layers <= 0) return PYAS_OK;
+    a.t = *t;
+    // few outputs with many layers: split the layers over waves
+    int64_t slices = 1;
+    if (a.n_out < 4096 && max_layers > 4 * pyas::kWave) {
+        slices = max_layers / (4 * pyas::kWave);
+        const int64_t cap = 8192 / a.n_out > 1 ? 8192 / a.n_out : 1;
+        if (slices > cap) slices = cap;
+    }
+    a.slices = slices;
+    if ((a.n_out * slices) / (pyas::kBlock / pyas::kWave) >= (int64_t(1) << 31))
+        return fail(PYAS_ENOTSUP, "tie grid too large");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    uint64_t *own = nullptr;
+    if (!keys && slices > 1) {
+        void *p = nullptr;
+        int rc = tie_scratch(ctx, st, (size_t)a.n_out * 16, &p);
+        if (rc) return rc;
+        own = (uint64_t *)p;
+        PYAS_HIP(hipMemsetAsync(own, 0, (size_t)a.n_out * 8, st));
+        PYAS_HIP(hipMemsetAsync(own + a.n_out, 0xff, (size_t)a.n_out * 8, st));
+    }
+    a.keys = keys ? keys : own;
+    PYAS_HIP(pyas::launch_tie_grid(dtype, a, st));
+    if (own) PYAS_HIP(pyas::launch_tie_finalize(dtype, own, a.n_out, 1, a.call, a.t, a.which, a.fin, st));
+    return PYAS_OK;
+}
+
+}  // namespace
+
+int pyas_tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, const pyas_tie_geom *geom,
+                    uint32_t axes_mask, uint32_t which, const int64_t *out_offsets, pyas_partial *partials,
+                    void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!partials && batch && batch->n_chunks > 0) return fail(PYAS_EINVAL, "partials is NULL");
+    return tie_chunks(ctx, batch, mask, geom, axes_mask, which, out_offsets, partials, nullptr, nullptr,
+                      (hipStream_t)stream);
+}
+
+int pyas_tie_chunk_flags(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, const pyas_tie_geom *geom,
+                         uint32_t axes_mask, uint32_t which, const int64_t *out_offsets, const pyas_partial *final_,
+                         int64_t n_final, uint8_t *flags, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!batch) return fail(PYAS_EINVAL, "batch is NULL");
+    if (which != 1u && which != 2u) return fail(PYAS_EINVAL, "which must be 1 (min) or 2 (max)");
+    if (!tie_of(ctx, batch->dtype) || batch->n_chunks == 0 || n_final <= 0) return PYAS_OK;
+    if (!final_ || !flags) return fail(PYAS_EINVAL, "NULL argument");
+    void *p = nullptr;
+    int rc = tie_scratch(ctx, stream, 16, &p);
+    if (rc) return rc;
+    uint32_t *gate = (uint32_t *)p;
+    hipStream_t st = (hipStream_t)stream;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(hipMemsetAsync(gate, 0, 4, st));
+    PYAS_HIP(pyas::launch_tie_gate(batch->dtype, final_, n_final, which, gate, st));
+    return tie_chunks(ctx, batch, mask, geom, axes_mask, which, out_offsets, nullptr, flags, gate, st);
+}
+
+int pyas_tie_grid(pyas_ctx *ctx, int32_t dtype, const pyas_grid *grid, const pyas_partial *parts,
+                  const uint8_t *flags, int64_t lr, uint32_t which, pyas_partial *final_, uint64_t *keys,
+                  void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!grid || !final_ || (!parts && !flags) || !grid->chunk_out_offsets)
+        return fail(PYAS_EINVAL, "NULL argument");
+    if (which != 1u && which != 2u) return fail(PYAS_EINVAL, "which must be 1 (min) or 2 (max)");
+    if (grid->ndim < 1 || grid->ndim > PYAS_MAX_DIMS) return fail(PYAS_EINVAL, "grid rank %d", grid->ndim);
+    const pyas::TieRule *t = tie_of(ctx, dtype);
+    if (!t) return PYAS_OK;
+    int64_t n_out = 1, n_layers = 1;
+    for (int d = 0; d < grid->ndim; ++d) {
+        if ((grid->axes_mask >> d) & 1u) n_layers *= grid->n_coords[d];
+        else n_out *= grid->out_extent[d];
+    }
+    if (n_layers >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "more than 2^31 chunk layers");
+    pyas::TieGridArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.g = *grid;
+    a.kind = 0;
+    a.parts = parts;
+    a.flags = flags;
+    a.fin = final_;
+    a.n_out = n_out;
+    a.n_layers = n_layers;
+    a.call = grid_call(*t, lr);
+    a.which = which;
+    return tie_level2(ctx, dtype, a, n_layers, keys, (hipStream_t)stream);
+}
+
+int pyas_tie_segments(pyas_ctx *ctx, int32_t dtype, const pyas_partial *parts, const int64_t *index,
+                      const int64_t *seg, int64_t n_seg, int64_t n_layers, int64_t layer_base, int64_t lr,
+                      uint32_t which, pyas_partial *final_, uint64_t *keys, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!parts || !final_) return fail(PYAS_EINVAL, "NULL argument");
+    if (which != 1u && which != 2u) return fail(PYAS_EINVAL, "which must be 1 (min) or 2 (max)");
+    if (!seg && (index || n_seg != 1)) return fail(PYAS_EINVAL, "seg NULL needs index NULL and one segment");
+    if (n_layers < 0 || layer_base < 0) return fail(PYAS_EINVAL, "negative layer count or base");
+    const pyas::TieRule *t = tie_of(ctx, dtype);
+    if (!t) return PYAS_OK;
+    pyas::TieGridArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.kind = seg ? 1 : 2;
+    a.index = index;
+    a.seg = seg;
+    a.parts = parts;
+    a.fin = final_;
+    a.n_out = n_seg;
+    a.n_layers = n_layers;
+    a.layer_base = layer_base;
+    a.call = grid_call(*t, lr);
+    a.which = which;
+    // segment lengths live on the device: the caller's n_layers bounds them
+    return tie_level2(ctx, dtype, a, n_layers, keys, (hipStream_t)stream);
+}
+
+int pyas_tie_keys_reset(pyas_ctx *ctx, uint64_t *keys, int64_t n_out, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (n_out <= 0) return PYAS_OK;
+    if (!keys) return fail(PYAS_EINVAL, "keys is NULL");
+    hipStream_t st = (hipStream_t)stream;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(hipMemsetAsync(keys, 0, (size_t)n_out * 8, st));
+    PYAS_HIP(hipMemsetAsync(keys + n_out, 0xff, (size_t)n_out * 8, st));
+    return PYAS_OK;
+}
+
+int pyas_tie_finalize(pyas_ctx *ctx, int32_t dtype, const uint64_t *keys, int64_t n_out, int32_t n_sets,
+                      int64_t lr, uint32_t which, pyas_partial *final_, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (which != 1u && which != 2u) return fail(PYAS_EINVAL, "which must be 1 (min) or 2 (max)");
+    const pyas::TieRule *t = tie_of(ctx, dtype);
+    if (!t || n_out <= 0 || n_sets <= 0) return PYAS_OK;
+    if (!keys || !final_) return fail(PYAS_EINVAL, "NULL argument");
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(pyas::launch_tie_finalize(dtype, keys, n_out, n_sets, grid_call(*t, lr), *t, which, final_,
+                                       (hipStream_t)stream));
     return PYAS_OK;
 }
 
@@ -482,7 +677,13 @@ int pyas_stream_destroy(pyas_ctx *ctx, void *stream) {
         auto it = ctx->scratch.find(stream);
         if (it != ctx->scratch.end()) {
             if (it->second.ptr) (void)hipFree(it->second.ptr);
+            if (it->second.cnt) (void)hipFree(it->second.cnt);
             ctx->scratch.erase(it);
+        }
+        auto jt = ctx->tie_scratch.find(stream);
+        if (jt != ctx->tie_scratch.end()) {
+            if (jt->second.ptr) (void)hipFree(jt->second.ptr);
+            ctx->tie_scratch.erase(jt);
         }
     }
     PYAS_HIP(hipStreamDestroy((hipStream_t)stream));
@@ -509,15 +710,9 @@ int pyas_stream_wait(pyas_ctx *ctx, void *waiter, void *waitee) {
     return PYAS_OK;
 }
 
-// pyas_reduce_chunks, optionally as two reduce launches over a selection
-// batch's whole chunks (whole_ids: the capped lean kernel, no selection
-// table) and its other chunks (part_ids: the selection-aware kernel); both
-// write their tile partials at the chunks' places, so k_finish folds them in
-// chunk order as for one launch.
-static int reduce_chunks_impl(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
-                              const int32_t *whole_ids, int64_t n_whole, const int32_t *part_ids,
-                              int64_t n_part, pyas_partial *chunk_out, pyas_partial *total,
-                              uint32_t combine_flags, void *stream) {
+int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                       pyas_partial *chunk_out, pyas_partial *total, uint32_t combine_flags,
+                       void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     if (!chunk_out && !total) return fail(PYAS_EINVAL, "neither chunk_out nor total given");
     if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
@@ -566,21 +761,7 @@ static int reduce_chunks_impl(pyas_ctx *ctx, const pyas_batch *batch, const pyas
 
     const bool timed = ctx->timing_n < (int32_t)ctx->ev0.size();
     if (timed) PYAS_HIP(hipEventRecord(ctx->ev0[ctx->timing_n], st));
-    if (whole_ids) {
-        if (n_whole > 0) {
-            pyas::ReduceArgs w = a;
-            w.sel = nullptr;   // whole chunks: the lean kernel, no table
-            w.pool = nullptr;
-            w.ids = whole_ids;
-            PYAS_HIP(pyas::launch_reduce(batch->dtype, w, shuf, bsw, masked, n_whole * tpc, st));
-        }
-        if (n_part > 0) {
-            a.ids = part_ids;
-            PYAS_HIP(pyas::launch_reduce(batch->dtype, a, shuf, bsw, masked, n_part * tpc, st));
-        }
-    } else {
-        PYAS_HIP(pyas::launch_reduce(batch->dtype, a, shuf, bsw, masked, grid, st));
-    }
+    PYAS_HIP(pyas::launch_reduce(batch->dtype, a, shuf, bsw, masked, grid, st));
     if (timed) {
         PYAS_HIP(hipEventRecord(ctx->ev1[ctx->timing_n], st));
         ctx->timing_n++;
@@ -590,29 +771,6 @@ static int reduce_chunks_impl(pyas_ctx *ctx, const pyas_batch *batch, const pyas
     if (total && !f.cnt)   // unchained: fold the group partials in a second launch
         PYAS_HIP(pyas::launch_combine(batch->dtype, f.gtmp, ng, ng, 1, 0u, total, st));
     return PYAS_OK;
-}
-
-int pyas_reduce_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
-                       pyas_partial *chunk_out, pyas_partial *total, uint32_t combine_flags,
-                       void *stream) {
-    return reduce_chunks_impl(ctx, batch, mask, nullptr, 0, nullptr, 0, chunk_out, total,
-                              combine_flags, stream);
-}
-
-int pyas_reduce_chunks_split(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
-                             const int32_t *whole_ids, int64_t n_whole, const int32_t *part_ids,
-                             int64_t n_part, pyas_partial *chunk_out, pyas_partial *total,
-                             uint32_t combine_flags, void *stream) {
-    if (!batch) return fail(PYAS_EINVAL, "batch is NULL");
-    if (!batch->sel) return fail(PYAS_EINVAL, "split launch needs a selection table");
-    if (mask && (mask->flags & (PYAS_MASK_TAB0 | PYAS_MASK_TAB1)))
-        return fail(PYAS_ENOTSUP, "split launch with vector mask tables");
-    if (n_whole < 0 || n_part < 0 || n_whole + n_part != batch->n_chunks)
-        return fail(PYAS_EINVAL, "%lld + %lld chunk ids for %lld chunks", (long long)n_whole,
-                    (long long)n_part, (long long)batch->n_chunks);
-    if ((n_whole && !whole_ids) || (n_part && !part_ids)) return fail(PYAS_EINVAL, "NULL chunk id list");
-    return reduce_chunks_impl(ctx, batch, mask, whole_ids ? whole_ids : part_ids, n_whole, part_ids,
-                              n_part, chunk_out, total, combine_flags, stream);
 }
 
 // Dense partial-axis geometry: merge the chunk dims into runs of reduced /

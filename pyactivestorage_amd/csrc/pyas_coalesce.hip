@@ -459,14 +459,19 @@ void launch_batch(pyas_coalescer *c, Slot *sl) {
         b.index_pool = (const int32_t *)(dm + m.pool_off);
         const uint32_t full = (g.key.desc.ndim >= 32) ? 0xffffffffu : ((1u << g.key.desc.ndim) - 1u);
         if (rc == PYAS_OK) {
+            // NumPy's sign of a zero min/max, for min/max call shapes only
+            const uint32_t tw = g.key.desc.tie_which;
             if ((g.key.desc.axes_mask & full) == full) {
                 rc = pyas_reduce_chunks(c->ctx, &b, &g.key.mask, dout + m.out_base, nullptr, 0u, sl->st);
-                // NumPy's sign of a zero min/max (the method is not known here: both)
-                if (rc == PYAS_OK)
-                    rc = pyas_zero_sign_chunks(c->ctx, &b, &g.key.mask, 3u, dout + m.out_base, sl->st);
-                if (rc == PYAS_ENOTSUP) rc = PYAS_OK;   // a chunk too large for the table: sign as reduced
-            } else
+                if (rc == PYAS_OK && tw)
+                    rc = pyas_tie_chunks(c->ctx, &b, &g.key.mask, &g.key.desc.tie, full, tw, nullptr,
+                                         dout + m.out_base, sl->st);
+            } else {
                 rc = pyas_reduce_axes(c->ctx, &b, &g.key.mask, g.key.desc.axes_mask, d_oofs, dout, sl->st);
+                if (rc == PYAS_OK && tw)
+                    rc = pyas_tie_chunks(c->ctx, &b, &g.key.mask, &g.key.desc.tie, g.key.desc.axes_mask, tw,
+                                         d_oofs, dout, sl->st);
+            }
         }
         if (rc != PYAS_OK) {
             const std::string msg = pyas_last_error();

@@ -25,9 +25,7 @@ struct ReduceArgs {
     int32_t ndim;
     pyas_mask mask;
     MaskTab tab;
-    pyas_partial *out;                // one partial per workgroup (tile)
-    const int32_t *ids;               // chunk ids of this launch (pyas_reduce_chunks_split); NULL:
-                                      // workgroup b reduces tile b of chunk b / tpc
+    pyas_partial *out;                // one partial per workgroup (tile b of chunk b / tpc)
 };
 
 // Chunks per first-level combine group: one k_finish block, one thread per
@@ -138,17 +136,52 @@ hipError_t launch_axes_fold_t(const AxesArgs &a, const FoldGrid &g, bool masked,
                               hipStream_t st);
 template <typename T>
 hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st);
-// NumPy's zero sign (pyas_zero_sign_chunks / _seq); float types only
+// NumPy's sign of a zero min/max (pyas_tie_*); float types only
 struct TieRule {
-    int32_t lanes, piece;
-    uint8_t rank[64];
+    int32_t lanes, piece, acc;        // lanes 0: no rule set
+    uint8_t rank[64], acc_rank[64];
+};
+struct TieCall {
+    int32_t acc;                      // 1: strided reduce loop (accumulator keys)
+    uint32_t block;                   // acc: kept dims of NumPy's copied first buffer fill
+    int64_t lr, npr;                  // call length (1: elementwise), pieces per call
+    int64_t n_copy;                   // acc: runs of that fill (contiguous calls), 0: none
+};
+constexpr int kTieTile = 2048;        // chunk outputs per k_tie_chunks workgroup (32 KiB of keys)
+struct TieChunkArgs {
+    ReduceArgs r;
+    TieRule t;
+    pyas_tie_geom g;
+    uint32_t axes, which;
+    bool shuf, bswap;
+    const int64_t *out_offsets;       // NULL: one output per chunk, at index c
+    pyas_partial *parts;              // rewrite mode, or NULL and:
+    uint8_t *flags;                   //   flag mode (one byte per chunk output)
+    const uint32_t *gate;             //   flag mode: skip when *gate == 0
+    int64_t tpc;                      // output tiles per chunk
+};
+struct TieGridArgs {
+    pyas_grid g;                      // kind 0: layers from the grid tables
+    const int64_t *index, *seg;       // kind 1: segments (index NULL: identity)
+    int32_t kind;                     // 2: one output, layer l = entry l
+    const pyas_partial *parts;        // level-1 partials, or
+    const uint8_t *flags;             //   level-1 flag bytes
+    pyas_partial *fin;
+    uint64_t *keys;
+    int64_t n_out, n_layers, layer_base, slices;
+    TieCall call;
+    TieRule t;
+    uint32_t which;
 };
 template <typename T>
-hipError_t launch_zero_sign_chunks_t(const ReduceArgs &r, bool shuf, bool bswap, const TieRule &t,
-                                     uint32_t which, pyas_partial *parts, int64_t n_chunks, int64_t lds_bytes, hipStream_t st);
+hipError_t launch_tie_chunks_t(const TieChunkArgs &a, int64_t grid, hipStream_t st);
 template <typename T>
-hipError_t launch_zero_sign_seq_t(const pyas_partial *parts, int64_t n, const TieRule &t, uint32_t which,
-                                  pyas_partial *total, int64_t lds_bytes, hipStream_t st);
+hipError_t launch_tie_gate_t(const pyas_partial *fin, int64_t n, uint32_t which, uint32_t *gate, hipStream_t st);
+template <typename T>
+hipError_t launch_tie_grid_t(const TieGridArgs &a, hipStream_t st);
+template <typename T>
+hipError_t launch_tie_finalize_t(const uint64_t *keys, int64_t n_out, int32_t n_sets, const TieCall &call,
+                                 const TieRule &t, uint32_t which, pyas_partial *fin, hipStream_t st);
 template <typename T>
 hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, void *values,
                            uint8_t *mask, int64_t *counts, hipStream_t st);
@@ -171,10 +204,12 @@ hipError_t launch_axes_fold(int dtype, const AxesArgs &a, const FoldGrid &g, boo
                             hipStream_t st);
 hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t st);
 hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream_t st);
-hipError_t launch_zero_sign_chunks(int dtype, const ReduceArgs &r, bool shuf, bool bswap, const TieRule &t,
-                                   uint32_t which, pyas_partial *parts, int64_t n_chunks, int64_t lds_bytes, hipStream_t st);
-hipError_t launch_zero_sign_seq(int dtype, const pyas_partial *parts, int64_t n, const TieRule &t,
-                                uint32_t which, pyas_partial *total, int64_t lds_bytes, hipStream_t st);
+hipError_t launch_tie_chunks(int dtype, const TieChunkArgs &a, int64_t grid, hipStream_t st);
+hipError_t launch_tie_gate(int dtype, const pyas_partial *fin, int64_t n, uint32_t which, uint32_t *gate,
+                           hipStream_t st);
+hipError_t launch_tie_grid(int dtype, const TieGridArgs &a, hipStream_t st);
+hipError_t launch_tie_finalize(int dtype, const uint64_t *keys, int64_t n_out, int32_t n_sets, const TieCall &call,
+                               const TieRule &t, uint32_t which, pyas_partial *fin, hipStream_t st);
 hipError_t launch_format(int dtype, const pyas_partial *in, int64_t n, int32_t method, void *values,
                          uint8_t *mask, int64_t *counts, hipStream_t st);
 // host ingest (pyas_ingest.hip): pread ring -> pinned slots -> H2D

@@ -134,15 +134,25 @@ hipError_t launch_select(int dtype, const SelectArgs &a, int64_t grid, hipStream
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_zero_sign_chunks(int dtype, const ReduceArgs &r, bool shuf, bool bswap, const TieRule &t,
-                                   uint32_t which, pyas_partial *parts, int64_t n_chunks, int64_t lds_bytes, hipStream_t st) {
-    PYAS_DISPATCH_T(dtype, return launch_zero_sign_chunks_t<T>(r, shuf, bswap, t, which, parts, n_chunks, lds_bytes, st));
+hipError_t launch_tie_chunks(int dtype, const TieChunkArgs &a, int64_t grid, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_tie_chunks_t<T>(a, grid, st));
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_zero_sign_seq(int dtype, const pyas_partial *parts, int64_t n, const TieRule &t,
-                                uint32_t which, pyas_partial *total, int64_t lds_bytes, hipStream_t st) {
-    PYAS_DISPATCH_T(dtype, return launch_zero_sign_seq_t<T>(parts, n, t, which, total, lds_bytes, st));
+hipError_t launch_tie_gate(int dtype, const pyas_partial *fin, int64_t n, uint32_t which, uint32_t *gate,
+                           hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_tie_gate_t<T>(fin, n, which, gate, st));
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_tie_grid(int dtype, const TieGridArgs &a, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_tie_grid_t<T>(a, st));
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_tie_finalize(int dtype, const uint64_t *keys, int64_t n_out, int32_t n_sets, const TieCall &call,
+                               const TieRule &t, uint32_t which, pyas_partial *fin, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_tie_finalize_t<T>(keys, n_out, n_sets, call, t, which, fin, st));
     return hipErrorInvalidValue;
 }
 

@@ -486,15 +486,12 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinishArgs f) {
 // ---------------------------------------------------------------------------
 // SEL = false: every chunk fully selected (batch.sel == NULL) -> a lean
 // streaming-only kernel (no selection state, high occupancy).
-// IDS: the launch covers the chunks listed in a.ids (pyas_reduce_chunks_split);
-// tile partials still land at their chunk's place, so k_finish is unchanged.
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL, bool IDS = false>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL>
 __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
     const int64_t b = blockIdx.x;
-    const int64_t cb = b / a.tpc;
-    const int64_t t = b - cb * a.tpc;
-    const int64_t c = IDS ? (int64_t)a.ids[cb] : cb;
-    pyas_partial *const tout = a.out + (IDS ? c * a.tpc + t : b);
+    const int64_t c = b / a.tpc;
+    const int64_t t = b - c * a.tpc;
+    pyas_partial *const tout = a.out + b;
     const uint8_t *base = a.data + a.offsets[c];
     MaskT<T> mk;
     if constexpr (MASKED) mk.init(a.mask);
@@ -602,18 +599,12 @@ __global__ __launch_bounds__(kBlock) PYAS_WAVES_ATTR void k_reduce(ReduceArgs a)
     reduce_body<T, SHUF, BSWAP, MASKED, false>(a);
 }
 
-// k_reduce over the whole chunks of a selection batch (pyas_reduce_chunks_split)
-template <typename T, bool SHUF, bool BSWAP, int MASKED>
-__global__ __launch_bounds__(kBlock) PYAS_WAVES_ATTR void k_reduce_ids(ReduceArgs a) {
-    reduce_body<T, SHUF, BSWAP, MASKED, false, true>(a);
-}
-
 // Uncapped: per-chunk selections (hyperslabs, strides, lists), where the cap
 // spills (C5 measured 46 % slower), and 1-/2-byte dtypes (16 or 8 values per
 // 16-B load also spill under the cap).  Keeps the compiler's allocation.
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL, bool IDS = false>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool SEL>
 __global__ __launch_bounds__(kBlock) void k_reduce_u(ReduceArgs a) {
-    reduce_body<T, SHUF, BSWAP, MASKED, SEL, IDS>(a);
+    reduce_body<T, SHUF, BSWAP, MASKED, SEL>(a);
 }
 
 // LDS writes of a wave visible to its other lanes (no block barrier)
@@ -2458,154 +2449,471 @@ __global__ __launch_bounds__(kBlock) void k_select(SelectArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// NumPy's sign of a zero min/max (pyas.h pyas_tie_rule; zerosign.py)
+// NumPy's sign of a zero min/max (pyas.h pyas_tie_*; zerosign.py restates
+// the same arithmetic and documents the measured NumPy behaviour)
 // ---------------------------------------------------------------------------
-// Flattened element e >= 1 of S (e == 0 seeds the result) falls in piece k
-// (piece 0 = [1, P), piece k = [kP, (k+1)P)), in lane (e - start) % L of the
-// piece's vector part or in its scalar remainder (slot L).
-__device__ __forceinline__ void tie_slot(int64_t e, int64_t S, const TieRule &t, int64_t &k, int &slot) {
-    const int64_t P = t.piece;
-    k = e / P;
-    const int64_t s0 = k == 0 ? 1 : k * P;
-    const int64_t e1 = (k + 1) * P < S ? (k + 1) * P : S;
-    const int64_t m = e1 - s0, nv = m - m % t.lanes, o = e - s0;
-    slot = o < nv ? (int)(o % t.lanes) : t.lanes;
-}
+// Key layouts (order-free: K1 combines by max, W by min):
+//   K1, contiguous loop : (e + 1) << 1 | sign of the seed, top-lane and
+//                         remainder zeros (0: none)
+//   W                   : (row + 1) << 32 | lane rank << 25 | (2^24-1-off) << 1 | sign
+//                         (the seed: sign alone; none: kTieWNone)
+//   K1, strided loop    : (call + 1) << 33 | remainder << 32 | acc priority << 25 | off << 1 | sign
+//                         (the seed: 2 | sign)
+constexpr uint64_t kTieWNone = ~0ull;
+constexpr int kTieOffBits = 24;
+constexpr uint32_t kTieRemRank = 127;
 
-// Thread 0, after the scan: tab[k * (L + 1) + slot] holds ((e + 1) << 1 |
-// signbit) of the last zero there (0: none).  Replays the loop's ties piece
-// by piece: with a zero already in hand every lane ties, so the rank-0 lane
-// decides (its own last zero, else the carried result); otherwise the best
-// ranked lane holding a zero; then the remainder's last zero.
-__device__ bool tie_fold(const uint64_t *tab, int64_t npieces, const TieRule &t, bool have, bool &sign) {
-    const int L = t.lanes;
-    int top = 0;
-    for (int l = 0; l < L; ++l)
-        if (t.rank[l] == 0) top = l;
-    for (int64_t k = 0; k < npieces; ++k) {
-        const uint64_t *row = tab + k * (L + 1);
-        if (have) {
-            if (row[top]) sign = row[top] & 1u;
-        } else {
-            int best = -1, br = 1 << 30;
-            for (int l = 0; l < L; ++l)
-                if (row[l] && t.rank[l] < br) { br = t.rank[l]; best = l; }
-            if (best >= 0) { sign = row[best] & 1u; have = true; }
+// Call structure (zerosign.call_structure): cnt/vstride per dim in elements,
+// perm = iteration order (outer -> inner).  lr = 1: elementwise calls.  A
+// strided call (acc) whose first buffer fill spans more than one kept
+// iteration dim: the first n_copy runs are copied, i.e. contiguous calls;
+// `block` = those kept dims.
+__device__ __forceinline__ TieCall tie_call(const int64_t *cnt, const int64_t *vstride, uint32_t red,
+                                            const int32_t *perm, int nd, bool buffered, int64_t piece) {
+    TieCall c;
+    c.acc = 0;
+    c.lr = 1;
+    c.npr = 1;
+    c.n_copy = 0;
+    c.block = 0;
+    int64_t lr = 1, prev_stride = 0, prev_cnt = 0, inner_stride = 0, first = 0, kb = 1;
+    bool one = true, any = false, chain = true;
+    int state = 0;   // 0 trailing reduced group, 1 kept block, 2 done
+#pragma unroll
+    for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
+        if (i < nd && state < 2) {
+            const int d = perm[i];
+            if (cnt[d] != 1) {
+                const bool r = (red >> d) & 1u;
+                if (state == 0 && r) {
+                    if (!any) inner_stride = vstride[d];
+                    else if (vstride[d] != prev_stride * prev_cnt) one = false;
+                    any = true;
+                    lr *= cnt[d];
+                } else if (!any || r) {
+                    state = 2;
+                } else {
+                    if (state == 0) {
+                        state = 1;
+                        first = cnt[d];
+                    } else if (chain && vstride[d] == prev_stride * prev_cnt) {
+                        first *= cnt[d];
+                    } else {
+                        chain = false;
+                    }
+                    c.block |= 1u << d;
+                    kb *= cnt[d];
+                }
+                prev_stride = vstride[d];
+                prev_cnt = cnt[d];
+            }
         }
-        if (row[L]) { sign = row[L] & 1u; have = true; }
     }
-    return have;
+    if (!any) {
+        c.block = 0;
+        return c;
+    }
+    c.lr = lr;
+    c.npr = (lr + piece - 1) / piece;
+    c.acc = (one && !buffered && inner_stride != 1) ? 1 : 0;
+    const int64_t n1 = c.acc && lr < piece ? (piece / lr < kb ? piece / lr : kb) : 0;
+    if (n1 > first) c.n_copy = n1;
+    else c.block = 0;
+    return c;
 }
 
-template <typename T>
-__device__ __forceinline__ void tie_record(uint64_t *tab, int64_t e, int64_t S, const TieRule &t, T x,
-                                           uint32_t *seed) {
-    const uint64_t sg = __builtin_signbit(x) ? 1u : 0u;
+// Keys of a zero at reduced position e (sg = its sign bit): k1/w for a
+// contiguous call, ka for a strided one (lanes: a copied strided call).
+__device__ __forceinline__ void tie_keys(int64_t e, uint64_t sg, const TieCall &c, const TieRule &t, bool lanes,
+                                         uint64_t &k1, uint64_t &w, uint64_t &ka) {
+    k1 = 0;
+    w = kTieWNone;
+    ka = 0;
+    const bool acc = c.acc && !lanes;
     if (e == 0) {
-        *seed = 1u | (uint32_t)(sg << 1);
+        if (acc) ka = 2u | sg;
+        else {
+            k1 = 2u | sg;
+            w = sg;
+        }
         return;
     }
-    int64_t k;
-    int slot;
-    tie_slot(e, S, t, k, slot);
-    atomicMax(reinterpret_cast<unsigned long long *>(tab + k * (t.lanes + 1) + slot),
-              (unsigned long long)((((uint64_t)e + 1) << 1) | sg));
+    const int64_t P = t.piece;
+    const int64_t q = e / c.lr, pos = e - q * c.lr;
+    const int64_t k = pos / P;
+    const int64_t s0 = (q == 0 && k == 0) ? 1 : k * P;
+    const int64_t e1 = (k + 1) * P < c.lr ? (k + 1) * P : c.lr;
+    const int64_t m = e1 - s0, off = pos - s0;
+    const uint64_t row1 = (uint64_t)(q * c.npr + k + 1);
+    if (acc) {
+        const int64_t nv = m - m % t.acc;
+        const bool vec = off < nv;
+        const uint64_t prio = vec ? (uint64_t)(t.acc - 1 - t.acc_rank[off % t.acc]) : 0u;
+        ka = (row1 << 33) | ((uint64_t)(vec ? 0 : 1) << 32) | (prio << 25) | ((uint64_t)off << 1) | sg;
+        return;
+    }
+    const int64_t nv = m - m % t.lanes;
+    const bool vec = off < nv;
+    const uint32_t rank = vec ? (uint32_t)t.rank[off % t.lanes] : kTieRemRank;
+    k1 = (!vec || rank == 0) ? ((((uint64_t)e + 1) << 1) | sg) : 0u;
+    w = (row1 << 32) | ((uint64_t)rank << 25) | ((uint64_t)(((int64_t)1 << kTieOffBits) - 1 - off) << 1) | sg;
 }
 
-// One workgroup per chunk; chunks whose min/max is not a zero return at once.
+// Sign bit from an output's combined keys; -1 when it holds no zero.
+__device__ __forceinline__ int tie_finalize(uint64_t k1, uint64_t w, uint64_t ka, const TieCall &c,
+                                            const TieRule &t) {
+    if (ka) return (int)(ka & 1u);   // a strided call's zero is later than a copied first call's
+    if (k1 == 0 && w == kTieWNone) return -1;
+    if (k1 == 0) return (int)(w & 1u);
+    if (w == kTieWNone) return (int)(k1 & 1u);
+    const int64_t e1 = (int64_t)(k1 >> 1) - 1;
+    int64_t ew = 0;
+    if (w >= 2) {
+        const int64_t row = (int64_t)(w >> 32) - 1;
+        const int64_t off = (((int64_t)1 << kTieOffBits) - 1) - (int64_t)((w >> 1) & ((1u << kTieOffBits) - 1));
+        const int64_t q = row / c.npr, k = row - q * c.npr;
+        const int64_t s0 = (q == 0 && k == 0) ? 1 : k * (int64_t)t.piece;
+        ew = q * c.lr + s0 + off;
+    }
+    return ew > e1 ? (int)(w & 1u) : (int)(k1 & 1u);
+}
+
 template <typename T>
-__global__ __launch_bounds__(kBlock) void k_zero_sign_chunks(ReduceArgs r, bool shuf, bool bswap, TieRule t,
-                                                             uint32_t which, pyas_partial *parts) {
-    extern __shared__ uint64_t tab[];
-    __shared__ uint32_t seed;
-    const int64_t c = blockIdx.x;
-    pyas_partial p = parts[c];
-    if (p.count <= 0) return;
-    const bool fmin = (which & 1u) && TT<T>::from(p.min) == (T)0;
-    const bool fmax = (which & 2u) && TT<T>::from(p.max) == (T)0;
-    if (!fmin && !fmax) return;   // block-uniform
+__device__ __forceinline__ bool tie_zero(const pyas_partial &p, uint32_t which) {
+    return p.count > 0 && (((which & 1u) && TT<T>::from(p.min) == (T)0) ||
+                           ((which & 2u) && TT<T>::from(p.max) == (T)0));
+}
+
+template <typename T>
+__device__ __forceinline__ void tie_put(pyas_partial *p, uint32_t which, int sg) {
+    const T z = sg ? -(T)0 : (T)0;
+    if ((which & 1u) && TT<T>::from(p->min) == (T)0) TT<T>::put(p->min, z);
+    if ((which & 2u) && TT<T>::from(p->max) == (T)0) TT<T>::put(p->max, z);
+}
+
+// Level 1 (storage.py:99-100 over chunk[sel]): workgroup = (chunk, tile of
+// kTieTile outputs).  Rewrite mode (parts): outputs whose min/max is a zero
+// get NumPy's sign.  Flag mode (flags): one byte per chunk output, bit 0 an
+// unmasked zero, bit 1 the winning zero's sign; skipped when *gate == 0.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_tie_chunks(TieChunkArgs a) {
+    __shared__ uint64_t sk1[kTieTile], sw[kTieTile], ska[kTieTile];
+    __shared__ uint8_t swant[kTieTile];
+    const ReduceArgs &r = a.r;
+    if (a.gate && *a.gate == 0u) return;
+    const int64_t c = (int64_t)blockIdx.x / a.tpc, tile = (int64_t)blockIdx.x - c * a.tpc;
     Sel s;
     load_sel(s, r.sel, c, r.ndim, r.shape);
-    int64_t S = 1;
+    int64_t cnt[PYAS_MAX_DIMS];
+    int64_t n_out = 1, R = 1;
 #pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d) S *= s.cnt[d];
-    const int64_t npieces = S > 1 ? (S - 1) / t.piece + 1 : 0;
-    for (int64_t q = threadIdx.x; q < npieces * (t.lanes + 1); q += kBlock) tab[q] = 0;
-    if (threadIdx.x == 0) seed = 0;
-    __syncthreads();
-    const uint8_t *base = r.data + r.offsets[c];
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+        cnt[d] = d < r.ndim ? (int64_t)s.cnt[d] : 1;
+        if ((a.axes >> d) & 1u) R *= cnt[d];
+        else n_out *= cnt[d];
+    }
+    const int64_t o0 = tile * kTieTile;
+    if (n_out == 0 || R == 0 || o0 >= n_out) return;   // block-uniform
+    const int no = (int)((n_out - o0) < kTieTile ? (n_out - o0) : kTieTile);
+    const int64_t ob = (a.out_offsets ? a.out_offsets[c] : c) + o0;
+    int any = 0;
+    for (int ol = threadIdx.x; ol < no; ol += kBlock) {
+        sk1[ol] = 0;
+        sw[ol] = kTieWNone;
+        ska[ol] = 0;
+        const uint8_t want = a.parts ? (tie_zero<T>(a.parts[ob + ol], a.which) ? 1 : 0) : 1;
+        swant[ol] = want;
+        any |= want;
+    }
+    if (!__syncthreads_or(any)) return;
+    int64_t vstride[PYAS_MAX_DIMS], wred[PYAS_MAX_DIMS];
+    {
+        int64_t st = 1, sr = 1;
+#pragma unroll
+        for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
+            if (i < r.ndim) {
+                const int d = a.g.perm[i];
+                vstride[d] = st;
+                st *= cnt[d];
+                if ((a.axes >> d) & 1u) {
+                    wred[d] = sr;
+                    sr *= cnt[d];
+                } else {
+                    wred[d] = 0;
+                }
+            }
+        }
+        if (a.g.flags & PYAS_TIE_VIEW) {
+#pragma unroll
+            for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+                if (d < r.ndim) vstride[d] = (int64_t)s.step[d] * r.cstride[d];
+        }
+    }
+    const TieCall call = tie_call(cnt, vstride, a.axes, a.g.perm, r.ndim, (a.g.flags & PYAS_TIE_BUFFERED) != 0,
+                                  a.t.piece);
+    int64_t bw[PYAS_MAX_DIMS];   // kept-block weights (NumPy's copied first fill), inner first
+    {
+        int64_t st = 1;
+#pragma unroll
+        for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
+            if (i < r.ndim) {
+                const int d = a.g.perm[i];
+                bw[d] = ((call.block >> d) & 1u) ? st : 0;
+                if ((call.block >> d) & 1u) st *= cnt[d];
+            }
+        }
+    }
+    // walk outputs fastest when the innermost non-1 dim is kept (adjacent lanes
+    // then read adjacent elements), else reduced positions fastest
+    bool ofast = false, found = false;
+#pragma unroll
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+        if (!found && d < r.ndim && cnt[d] != 1) {
+            found = true;
+            ofast = !((a.axes >> d) & 1u);
+        }
+    }
     MaskT<T> mk;
     mk.init(r.mask);
-    const uint32_t all = (1u << r.ndim) - 1u;
-    for (int64_t e = threadIdx.x; e < S; e += kBlock) {
+    const uint8_t *base = r.data + r.offsets[c];
+    const int64_t total = (int64_t)no * R;
+    for (int64_t f = threadIdx.x; f < total; f += kBlock) {
+        int64_t ol, rr;
+        if (ofast) {
+            rr = f / no;
+            ol = f - rr * no;
+        } else {
+            ol = f / R;
+            rr = f - ol * R;
+        }
+        if (!swant[ol]) continue;
+        int64_t oo = o0 + ol, e = 0, bidx = 0;
+        bool beyond = false;   // a kept coordinate outside the block is non-zero
         Decomp o{0, {0, 0}};
-        decompose(s, r.pool, r.cstride, r.tab, r.ndim, all, e, o);
-        const T x = load_elem_rt<T>(base, r.chunk_elems, o.mem, shuf, bswap);
-        if (x == (T)0 && !all_masked(mk, r.tab, o, x)) tie_record(tab, e, S, t, x, &seed);
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            if (d < r.ndim) {
+                int64_t k;
+                if ((a.axes >> d) & 1u) {
+                    const int64_t q = rr / cnt[d];
+                    k = rr - q * cnt[d];
+                    rr = q;
+                    e += k * wred[d];
+                } else {
+                    const int64_t q = oo / cnt[d];
+                    k = oo - q * cnt[d];
+                    oo = q;
+                    if ((call.block >> d) & 1u) bidx += k * bw[d];
+                    else beyond |= k != 0;
+                }
+                o.mem += sel_index(s, r.pool, d, k) * r.cstride[d];
+                o.v[0] += k * r.tab.stride[0][d];
+                o.v[1] += k * r.tab.stride[1][d];
+            }
+        }
+        const T x = load_elem_rt<T>(base, r.chunk_elems, o.mem, a.shuf, a.bswap);
+        if (x == (T)0 && !all_masked(mk, r.tab, o, x)) {
+            const bool lanes = call.n_copy && e < call.lr && !beyond && bidx < call.n_copy;
+            uint64_t k1, w, ka;
+            tie_keys(e, __builtin_signbit(x) ? 1u : 0u, call, a.t, lanes, k1, w, ka);
+            if (k1) atomicMax(reinterpret_cast<unsigned long long *>(&sk1[ol]), (unsigned long long)k1);
+            if (w != kTieWNone) atomicMin(reinterpret_cast<unsigned long long *>(&sw[ol]), (unsigned long long)w);
+            if (ka) atomicMax(reinterpret_cast<unsigned long long *>(&ska[ol]), (unsigned long long)ka);
+        }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        bool sign = (seed >> 1) & 1u;
-        if (tie_fold(tab, npieces, t, (seed & 1u) != 0, sign)) {
-            const T z = sign ? -(T)0 : (T)0;
-            if (fmin) TT<T>::put(parts[c].min, z);
-            if (fmax) TT<T>::put(parts[c].max, z);
+    for (int ol = threadIdx.x; ol < no; ol += kBlock) {
+        if (!swant[ol]) continue;
+        const int sg = tie_finalize(sk1[ol], sw[ol], ska[ol], call, a.t);
+        if (a.parts) {
+            if (sg >= 0) tie_put<T>(a.parts + ob + ol, a.which, sg);
+        } else {
+            a.flags[ob + ol] = sg < 0 ? (uint8_t)0 : (uint8_t)(1u | ((unsigned)sg << 1));
         }
     }
 }
 
-// One workgroup over the sequence of per-chunk values (min or max).
+// Is any final output's min/max a zero (the fold path's level-1 gate)?
 template <typename T>
-__global__ __launch_bounds__(kBlock) void k_zero_sign_seq(const pyas_partial *parts, int64_t n, TieRule t,
-                                                          bool use_max, pyas_partial *total) {
-    extern __shared__ uint64_t tab[];
-    __shared__ uint32_t seed;
-    const pyas_partial tp = *total;
-    if (tp.count <= 0 || TT<T>::from(use_max ? tp.max : tp.min) != (T)0) return;
-    const int64_t npieces = n > 1 ? (n - 1) / t.piece + 1 : 0;
-    for (int64_t q = threadIdx.x; q < npieces * (t.lanes + 1); q += kBlock) tab[q] = 0;
-    if (threadIdx.x == 0) seed = 0;
-    __syncthreads();
-    for (int64_t e = threadIdx.x; e < n; e += kBlock) {
-        const pyas_partial p = parts[e];
-        const T x = TT<T>::from(use_max ? p.max : p.min);
-        if (p.count > 0 && x == (T)0) tie_record(tab, e, n, t, x, &seed);
+__global__ __launch_bounds__(kBlock) void k_tie_gate(const pyas_partial *fin, int64_t n, uint32_t which,
+                                                     uint32_t *gate) {
+    int hit = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        hit |= tie_zero<T>(fin[i], which) ? 1 : 0;
+    if (__syncthreads_or(hit) && threadIdx.x == 0) atomicOr(gate, 1u);
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int m = kWave / 2; m >= 1; m >>= 1) {
+        const uint64_t o = shfl_xor(v, m);
+        v = o > v ? o : v;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        bool sign = (seed >> 1) & 1u;
-        if (tie_fold(tab, npieces, t, (seed & 1u) != 0, sign)) {
-            const T z = sign ? -(T)0 : (T)0;
-            if (use_max) TT<T>::put(total->max, z);
-            else TT<T>::put(total->min, z);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int m = kWave / 2; m >= 1; m >>= 1) {
+        const uint64_t o = shfl_xor(v, m);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// Level 2 (active.py:594 over the `out` array): one wave per (final output,
+// slice of its chunk layers).  Layer l of output f comes from the grid
+// tables (kind 0, pyas_combine_grid's walk), a segment list (kind 1,
+// pyas_combine_segments') or parts[l] itself (kind 2, one output); its
+// reduced position is layer_base + l.  keys == NULL: the output's sign is
+// written to fin[f] (one slice per output); else the wave's keys are folded
+// into keys[f] (max) / keys[n_out + f] (min).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_tie_grid(TieGridArgs a) {
+    const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    const int64_t gw = (int64_t)blockIdx.x * (kBlock / kWave) + w;
+    const int64_t f = gw / a.slices, sl = gw - f * a.slices;
+    if (f >= a.n_out) return;   // wave-uniform
+    if (!tie_zero<T>(a.fin[f], a.which)) return;
+    const pyas_grid &g = a.g;
+    int64_t gstride[PYAS_MAX_DIMS];
+    int64_t j = 0, nk = 0, l_lo = 0, l_n = a.n_layers;
+    if (a.kind == 0) {
+        int64_t jstride = 1, rest = f, st = 1;
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            gstride[d] = st;
+            if (d < g.ndim) {
+                st *= g.n_coords[d];
+                if (!((g.axes_mask >> d) & 1u)) {
+                    const int64_t ext = g.out_extent[d];
+                    const int64_t p = rest % ext;
+                    rest /= ext;
+                    const int64_t cc = g.pos_coord[d][p];
+                    nk += cc * gstride[d];
+                    j += (int64_t)g.pos_local[d][p] * jstride;
+                    jstride *= g.coord_count[d][cc];
+                }
+            }
         }
+    } else if (a.kind == 1) {
+        l_lo = a.seg[f];
+        l_n = a.seg[f + 1] - l_lo;
+    }
+    const int64_t per = (l_n + a.slices - 1) / a.slices;
+    const int64_t lb = sl * per, le = (lb + per) < l_n ? (lb + per) : l_n;
+    uint64_t k1 = 0, kw = kTieWNone;
+    for (int64_t l = lb + lane; l < le; l += kWave) {
+        int64_t idx;
+        if (a.kind == 0) {
+            int64_t n = nk;
+            uint32_t rr = (uint32_t)l;
+#pragma unroll
+            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+                if (d < g.ndim && ((g.axes_mask >> d) & 1u)) {
+                    const uint32_t nc = (uint32_t)g.n_coords[d], q = rr / nc;
+                    n += (int64_t)(rr - q * nc) * gstride[d];
+                    rr = q;
+                }
+            }
+            idx = g.chunk_out_offsets[n] + j;
+        } else if (a.kind == 1) {
+            idx = a.index ? a.index[l_lo + l] : l_lo + l;
+        } else {
+            idx = l;
+        }
+        bool zero;
+        uint64_t sg;
+        if (a.flags) {
+            const uint8_t b = a.flags[idx];
+            zero = (b & 1u) != 0;
+            sg = (b >> 1) & 1u;
+        } else {
+            const pyas_partial p = a.parts[idx];
+            const T v = TT<T>::from((a.which & 1u) ? p.min : p.max);
+            zero = p.count > 0 && v == (T)0;
+            sg = __builtin_signbit(v) ? 1u : 0u;
+        }
+        if (zero) {
+            uint64_t x1, xw, xa;
+            tie_keys(a.layer_base + l, sg, a.call, a.t, true, x1, xw, xa);
+            k1 = x1 > k1 ? x1 : k1;
+            kw = xw < kw ? xw : kw;
+        }
+    }
+    k1 = wave_max_u64(k1);
+    kw = wave_min_u64(kw);
+    if (lane != 0) return;
+    if (a.keys) {
+        if (k1) atomicMax(reinterpret_cast<unsigned long long *>(a.keys + f), (unsigned long long)k1);
+        if (kw != kTieWNone)
+            atomicMin(reinterpret_cast<unsigned long long *>(a.keys + a.n_out + f), (unsigned long long)kw);
+    } else {
+        const int sg = tie_finalize(k1, kw, 0, a.call, a.t);
+        if (sg >= 0) tie_put<T>(a.fin + f, a.which, sg);
     }
 }
 
+// Keys of n_sets slices or ranks ([K1[n_out], W[n_out]] each) -> fin's signs.
 template <typename T>
-hipError_t launch_zero_sign_chunks_t(const ReduceArgs &r, bool shuf, bool bswap, const TieRule &t,
-                                     uint32_t which, pyas_partial *parts, int64_t n_chunks, int64_t lds_bytes, hipStream_t st) {
+__global__ __launch_bounds__(kBlock) void k_tie_finalize(const uint64_t *keys, int64_t n_out, int32_t n_sets,
+                                                         TieCall call, TieRule t, uint32_t which,
+                                                         pyas_partial *fin) {
+    const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (f >= n_out || !tie_zero<T>(fin[f], which)) return;
+    uint64_t k1 = 0, kw = kTieWNone;
+    for (int32_t s = 0; s < n_sets; ++s) {
+        const uint64_t x1 = keys[(int64_t)s * 2 * n_out + f], xw = keys[(int64_t)s * 2 * n_out + n_out + f];
+        k1 = x1 > k1 ? x1 : k1;
+        kw = xw < kw ? xw : kw;
+    }
+    const int sg = tie_finalize(k1, kw, 0, call, t);
+    if (sg >= 0) tie_put<T>(fin + f, which, sg);
+}
+
+template <typename T>
+hipError_t launch_tie_chunks_t(const TieChunkArgs &a, int64_t grid, hipStream_t st) {
     if constexpr (TT<T>::kind != 0) {
         return hipSuccess;
     } else {
-        hipLaunchKernelGGL((k_zero_sign_chunks<T>), dim3((unsigned)n_chunks), dim3(kBlock), (size_t)lds_bytes,
-                           st, r, shuf, bswap, t, which, parts);
+        hipLaunchKernelGGL((k_tie_chunks<T>), dim3((unsigned)grid), dim3(kBlock), 0, st, a);
         return hipGetLastError();
     }
 }
 
 template <typename T>
-hipError_t launch_zero_sign_seq_t(const pyas_partial *parts, int64_t n, const TieRule &t, uint32_t which,
-                                  pyas_partial *total, int64_t lds_bytes, hipStream_t st) {
+hipError_t launch_tie_gate_t(const pyas_partial *fin, int64_t n, uint32_t which, uint32_t *gate, hipStream_t st) {
     if constexpr (TT<T>::kind != 0) {
         return hipSuccess;
     } else {
-        if (which & 1u)
-            hipLaunchKernelGGL((k_zero_sign_seq<T>), dim3(1), dim3(kBlock), (size_t)lds_bytes, st, parts, n, t,
-                               false, total);
-        if (which & 2u)
-            hipLaunchKernelGGL((k_zero_sign_seq<T>), dim3(1), dim3(kBlock), (size_t)lds_bytes, st, parts, n, t,
-                               true, total);
+        int64_t blocks = (n + kBlock - 1) / kBlock;
+        blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+        hipLaunchKernelGGL((k_tie_gate<T>), dim3((unsigned)blocks), dim3(kBlock), 0, st, fin, n, which, gate);
+        return hipGetLastError();
+    }
+}
+
+template <typename T>
+hipError_t launch_tie_grid_t(const TieGridArgs &a, hipStream_t st) {
+    if constexpr (TT<T>::kind != 0) {
+        return hipSuccess;
+    } else {
+        const int64_t waves = a.n_out * a.slices;
+        const int64_t blocks = (waves + kBlock / kWave - 1) / (kBlock / kWave);
+        hipLaunchKernelGGL((k_tie_grid<T>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a);
+        return hipGetLastError();
+    }
+}
+
+template <typename T>
+hipError_t launch_tie_finalize_t(const uint64_t *keys, int64_t n_out, int32_t n_sets, const TieCall &call,
+                                 const TieRule &t, uint32_t which, pyas_partial *fin, hipStream_t st) {
+    if constexpr (TT<T>::kind != 0) {
+        return hipSuccess;
+    } else {
+        const int64_t blocks = (n_out + kBlock - 1) / kBlock;
+        hipLaunchKernelGGL((k_tie_finalize<T>), dim3((unsigned)blocks), dim3(kBlock), 0, st, keys, n_out, n_sets,
+                           call, t, which, fin);
         return hipGetLastError();
     }
 }
@@ -2625,16 +2933,14 @@ inline int mask_mode(const pyas_mask &m, bool masked) {
     return kMaskAll;
 }
 
-template <typename T, bool SEL, bool IDS = false>
+template <typename T, bool SEL>
 static void launch_reduce_ts(const ReduceArgs &a, bool shuf, bool bsw, bool masked, dim3 g,
                              hipStream_t st) {
     const dim3 blk(kBlock);
 #define PYAS_L(S, B, M)                                                                \
     do {                                                                               \
         if constexpr (SEL || sizeof(T) < 4)                                            \
-            hipLaunchKernelGGL((k_reduce_u<T, S, B, M, SEL, IDS>), g, blk, 0, st, a);  \
-        else if constexpr (IDS)                                                        \
-            hipLaunchKernelGGL((k_reduce_ids<T, S, B, M>), g, blk, 0, st, a);          \
+            hipLaunchKernelGGL((k_reduce_u<T, S, B, M, SEL>), g, blk, 0, st, a);       \
         else hipLaunchKernelGGL((k_reduce<T, S, B, M>), g, blk, 0, st, a);             \
     } while (0)
     // the lean kernel also has variants with fewer rules (mask_mode)
@@ -2673,10 +2979,7 @@ hipError_t launch_reduce_t(const ReduceArgs &a, bool shuf, bool bsw, bool masked
     // vector fill/missing tables are applied by the selection-aware path only
     // (a NULL table there means every chunk whole)
     const bool sel = a.sel || a.tab.on[0] || a.tab.on[1];
-    if (a.ids) {   // one half of pyas_reduce_chunks_split
-        if (sel) launch_reduce_ts<T, true, true>(a, shuf, bsw, masked, g, st);
-        else launch_reduce_ts<T, false, true>(a, shuf, bsw, masked, g, st);
-    } else if (sel) {
+    if (sel) {
         launch_reduce_ts<T, true>(a, shuf, bsw, masked, g, st);
     } else {
         launch_reduce_ts<T, false>(a, shuf, bsw, masked, g, st);
@@ -2957,10 +3260,12 @@ hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, vo
     template hipError_t launch_select_t<T>(const SelectArgs &, int64_t, hipStream_t);         \
     template hipError_t launch_format_t<T>(const pyas_partial *, int64_t, int32_t, void *,    \
                                            uint8_t *, int64_t *, hipStream_t);                \
-    template hipError_t launch_zero_sign_chunks_t<T>(const ReduceArgs &, bool, bool, const TieRule &, \
-                                                     uint32_t, pyas_partial *, int64_t, int64_t, hipStream_t); \
-    template hipError_t launch_zero_sign_seq_t<T>(const pyas_partial *, int64_t, const TieRule &,   \
-                                                  uint32_t, pyas_partial *, int64_t, hipStream_t);
+    template hipError_t launch_tie_chunks_t<T>(const TieChunkArgs &, int64_t, hipStream_t);      \
+    template hipError_t launch_tie_gate_t<T>(const pyas_partial *, int64_t, uint32_t, uint32_t *,  \
+                                             hipStream_t);                                       \
+    template hipError_t launch_tie_grid_t<T>(const TieGridArgs &, hipStream_t);                   \
+    template hipError_t launch_tie_finalize_t<T>(const uint64_t *, int64_t, int32_t, const TieCall &, \
+                                                 const TieRule &, uint32_t, pyas_partial *, hipStream_t);
 #define PYAS_INSTANTIATE_PART2(T)                                                              \
     template hipError_t launch_axes_dense_t<T>(const AxesArgs &, bool, int64_t, hipStream_t);
 #define PYAS_INSTANTIATE_PART3(T)                                                              \

@@ -173,9 +173,11 @@ class Context:
             if rule is None:
                 continue
             r = _lib.TieRule()
-            r.lanes, r.piece = rule.lanes, rule.piece
+            r.lanes, r.piece, r.acc = rule.lanes, rule.piece, rule.acc
             for lane, rank in enumerate(rule.rank):
                 r.rank[lane] = rank
+            for k, rank in enumerate(rule.acc_rank):
+                r.acc_rank[k] = rank
             _lib.check(self.lib.pyas_ctx_set_tie_rule(self.handle, code, ctypes.byref(r)), "set_tie_rule")
 
     def _count(self, streams=0, pinned=0):

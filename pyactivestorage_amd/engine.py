@@ -86,40 +86,51 @@ def reduce_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, chunk_out_pt
                "pyas_reduce_chunks")
 
 
-def reduce_chunks_split(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, whole_ptr, n_whole: int,
-                        part_ptr, n_part: int, chunk_out_ptr, total_ptr, round_to_var: bool,
-                        stream) -> None:
-    """reduce_chunks as two launches: whole chunks on the lean kernel, the
-    rest on the selection-aware one (pyas_reduce_chunks_split)."""
-    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
-    _lib.check(ctx.lib.pyas_reduce_chunks_split(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
-                                                whole_ptr, int(n_whole), part_ptr, int(n_part),
-                                                chunk_out_ptr, total_ptr, flags, stream),
-               "pyas_reduce_chunks_split")
+def tie_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, geom: _lib.TieGeom, axes_mask: int,
+               which: int, out_offsets_ptr, partials_ptr, stream) -> None:
+    """NumPy's sign of every zero min (which 1) / max (which 2) among the
+    chunks' partials (pyas_tie_chunks, storage.py:99-100)."""
+    _lib.check(ctx.lib.pyas_tie_chunks(ctx.handle, ctypes.byref(batch), ctypes.byref(mask), ctypes.byref(geom),
+                                       int(axes_mask), int(which), out_offsets_ptr, partials_ptr, stream),
+               "pyas_tie_chunks")
 
 
-def zero_sign_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, which: int, partials_ptr,
-                     stream) -> bool:
-    """NumPy's sign of each chunk's zero min (which & 1) / max (which & 2)
-    (pyas_zero_sign_chunks); False when a chunk is too large for the table
-    (the sign is then the reduction's own)."""
-    rc = ctx.lib.pyas_zero_sign_chunks(ctx.handle, ctypes.byref(batch), ctypes.byref(mask), int(which),
-                                       partials_ptr, stream)
-    if rc == _lib.ENOTSUP:
-        return False
-    _lib.check(rc, "pyas_zero_sign_chunks")
-    return True
+def tie_chunk_flags(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, geom: _lib.TieGeom, axes_mask: int,
+                    which: int, out_offsets_ptr, final_ptr, n_final: int, flags_ptr, stream) -> None:
+    """Per chunk output: zero held / NumPy's sign, when a final min/max is a
+    zero (pyas_tie_chunk_flags; for results folded in the reduce kernel)."""
+    _lib.check(ctx.lib.pyas_tie_chunk_flags(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
+                                            ctypes.byref(geom), int(axes_mask), int(which), out_offsets_ptr,
+                                            final_ptr, int(n_final), flags_ptr, stream),
+               "pyas_tie_chunk_flags")
 
 
-def zero_sign_seq(ctx: Context, dt, partials_ptr, n, which: int, total_ptr, stream) -> bool:
-    """NumPy's sign of the combined zero min/max over per-chunk partials in
-    the reference's `out` order (pyas_zero_sign_seq)."""
-    rc = ctx.lib.pyas_zero_sign_seq(ctx.handle, dtype_code(dt), partials_ptr, int(n), int(which), total_ptr,
-                                    stream)
-    if rc == _lib.ENOTSUP:
-        return False
-    _lib.check(rc, "pyas_zero_sign_seq")
-    return True
+def tie_grid(ctx: Context, dt, grid: _lib.Grid, parts_ptr, flags_ptr, lr: int, which: int, final_ptr,
+             keys_ptr, stream) -> None:
+    """NumPy's sign of the zero min/max of the `out` reduction over chunk
+    layers (pyas_tie_grid, active.py:594)."""
+    _lib.check(ctx.lib.pyas_tie_grid(ctx.handle, dtype_code(dt), ctypes.byref(grid), parts_ptr, flags_ptr,
+                                     int(lr), int(which), final_ptr, keys_ptr, stream), "pyas_tie_grid")
+
+
+def tie_segments(ctx: Context, dt, parts_ptr, index_ptr, seg_ptr, n_seg: int, n_layers: int, layer_base: int,
+                 lr: int, which: int, final_ptr, keys_ptr, stream) -> None:
+    """pyas_tie_segments: the level-2 sign over segment lists (or one
+    output over parts[0, n_layers) when index/seg are None)."""
+    _lib.check(ctx.lib.pyas_tie_segments(ctx.handle, dtype_code(dt), parts_ptr, index_ptr, seg_ptr, int(n_seg),
+                                         int(n_layers), int(layer_base), int(lr), int(which), final_ptr,
+                                         keys_ptr, stream), "pyas_tie_segments")
+
+
+def tie_keys_reset(ctx: Context, keys_ptr, n_out: int, stream) -> None:
+    _lib.check(ctx.lib.pyas_tie_keys_reset(ctx.handle, keys_ptr, int(n_out), stream), "pyas_tie_keys_reset")
+
+
+def tie_finalize(ctx: Context, dt, keys_ptr, n_out: int, n_sets: int, lr: int, which: int, final_ptr,
+                 stream) -> None:
+    """Combine gathered keys (ranks) and write the signs (pyas_tie_finalize)."""
+    _lib.check(ctx.lib.pyas_tie_finalize(ctx.handle, dtype_code(dt), keys_ptr, int(n_out), int(n_sets), int(lr),
+                                         int(which), final_ptr, stream), "pyas_tie_finalize")
 
 
 def reduce_axes(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, axes_mask: int, out_offsets_ptr,

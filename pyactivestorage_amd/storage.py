@@ -26,7 +26,7 @@ import zlib
 
 import numpy as np
 
-from . import _lib, engine, results, selection
+from . import _lib, engine, results, selection, zerosign
 from .device import get_context
 from .dtypes import dtype_code, native, needs_byteswap, sum_dtype
 from .inflate import inflate_chunk, is_zlib
@@ -177,7 +177,7 @@ class _Layout:
     pyas_chunk_desc / pyas_mask pair and the per-(selection, axis) plans."""
 
     __slots__ = ("refs", "ok", "dt", "pdt", "cm", "mask", "mask_ref", "desc_base", "rev", "shape",
-                 "zlib", "sels")
+                 "zlib", "sels", "order")
 
     def __init__(self, refs, compression, filters, missing, dtype, shape, order):
         self.refs = refs
@@ -185,6 +185,7 @@ class _Layout:
         self.sels = {}
         dt = self.dt = np.dtype(dtype)
         self.shape = shape
+        self.order = order
         if order not in ("C", "F") or dt.kind not in "iuf":
             return
         try:
@@ -222,14 +223,15 @@ class _Layout:
         self.pdt = engine.partial_dtype(dt)
         self.ok = True
 
-    def plan(self, chunk_selection, axis):
+    def plan(self, chunk_selection, axis, which=0):
         """(desc, sel_ptr, pool_ptr, pool_len, n_out, keep_shape, n_red, n_sel,
-        keepalive) for one selection + axis, cached when the selection is
-        made of slices (what pyfive's indexer produces)."""
+        keepalive) for one selection + axis (+ the min (1) / max (2) whose
+        zero sign the batch fixes, pyas_tie_chunks), cached when the
+        selection is made of slices (what pyfive's indexer produces)."""
         sel = chunk_selection if chunk_selection.__class__ is tuple else (chunk_selection,)
         try:   # slices only (ints, lists and arrays have no .start): cacheable
             key = (tuple([(s.start, s.stop, s.step) for s in sel]),
-                   axis if axis is None or axis.__class__ is int else tuple(axis))
+                   axis if axis is None or axis.__class__ is int else tuple(axis), which)
         except (AttributeError, TypeError):
             key = None
         if key is not None:
@@ -259,6 +261,9 @@ class _Layout:
         desc = _lib.ChunkDesc()
         ctypes.pointer(desc)[0] = self.desc_base
         desc.axes_mask = mask_bits
+        if which and self.dt.kind == "f":
+            desc.tie_which = which
+            desc.tie = zerosign.geometry(shape, self.order, cs, self.cm.masked, self.dt)
         dev_dims = cs.dims[::-1] if rev else cs.dims
         full = all(ds.step == 1 and ds.start == 0 and ds.count == n and not ds.dropped
                    for ds, n in zip(dev_dims, shape[::-1] if rev else shape))
@@ -310,7 +315,7 @@ def _coalesced(rfile, offset, size, compression, filters, missing, dtype, shape,
         if not lay.ok:
             return None
         desc, desc_ref, sel_ptr, pool_ptr, pool_len, n_out, keep_shape, n_red, n_sel, _ = \
-            lay.plan(chunk_selection, axis)
+            lay.plan(chunk_selection, axis, _TIE_WHICH.get(kind, 0))
     except Exception:
         return None
     if n_out == 0 or n_sel == 0:
@@ -369,13 +374,15 @@ def _get_ctx0():
 
 
 _KIND = {"sum": 0, "min": 1, "max": 2}
+_TIE_WHICH = {"min": 1, "max": 2}
 _VCLASS = {"f": 0, "i": 1, "u": 2}
 
 
 def _register_fast(lay, compression, filters, missing, dtype, shape, order, chunk_selection, axis,
                    method, kind, is_ma, keep_shape, n_sel):
     """Hand one call shape's plan to the C hot path (pyas_fastpath.cpp)."""
-    desc, _, sel_ptr, _, pool_len, _, _, _, _, (table, pool) = lay.plan(chunk_selection, axis)
+    desc, _, sel_ptr, _, pool_len, _, _, _, _, (table, pool) = lay.plan(chunk_selection, axis,
+                                                                        _TIE_WHICH.get(kind, 0))
     if not keep_shape:
         return
     rdt = sum_dtype(lay.dt) if kind == "sum" else native(lay.dt)
@@ -499,7 +506,8 @@ def reduce_chunk_bytes(raw, compression, filters, missing, dtype, shape, order,
         out = ctx.thread_buffer("out", _lib.PARTIAL_NBYTES)
         engine.reduce_chunks(ctx, batch, mup.struct, out.ptr, None, False, st)
         if kind in ("min", "max"):   # NumPy's +0.0/-0.0 when the extreme is zero
-            engine.zero_sign_chunks(ctx, batch, mup.struct, 1 if kind == "min" else 2, out.ptr, st)
+            engine.tie_chunks(ctx, batch, mup.struct, zerosign.geometry(shape, order, cs, cm.masked, dt),
+                              (1 << len(shape)) - 1, 1 if kind == "min" else 2, None, out.ptr, st)
         host = np.zeros(1, dtype=pdt)
         ctx.d2h(host, out.ptr, st)
         ctx.synchronize(st)
@@ -516,6 +524,12 @@ def reduce_chunk_bytes(raw, compression, filters, missing, dtype, shape, order,
         ctx.h2d(off_ptr, zero, st)
         if n_out:
             engine.reduce_axes(ctx, batch, mup.struct, mask_bits, off_ptr, out.ptr, st)
+            if kind in ("min", "max"):
+                for k, ds in enumerate(dev_dims):   # integer-indexed dims are reduced too (extent 1)
+                    if ds.dropped:
+                        mask_bits |= 1 << k
+                engine.tie_chunks(ctx, batch, mup.struct, zerosign.geometry(shape, order, cs, cm.masked, dt),
+                                  mask_bits, 1 if kind == "min" else 2, off_ptr, out.ptr, st)
         host = np.zeros(max(n_out, 1), dtype=pdt)
         ctx.d2h(host, out.ptr, st)
         ctx.synchronize(st)

@@ -20,12 +20,28 @@ QUERIES = [
     ("mean", ([1, 5, 20, 33], slice(None), slice(10, 40)), (1,)),
     ("sum", (slice(0, 8), slice(0, 12), slice(0, 10)), None),      # a single chunk
 ]
+# min/max of data holding both signed zeros: the result's zero sign must be
+# NumPy's over the whole `out` array (zero-sign keys gathered with the grids)
+ZQUERIES = [
+    ("min", (slice(None),) * 3, None),
+    ("min", (slice(3, 37), slice(5, 30, 2), slice(None)), (0,)),
+    ("min", (slice(None), slice(None), slice(7, 45)), (1, 2)),
+    ("min", (slice(None),) * 3, (0, 2)),
+    ("max", (slice(None),) * 3, None),
+    ("max", (slice(3, 37), slice(None), slice(None)), (2,)),
+]
 
 
-def make_variable():
+def make_variable(zeros=0):
+    """zeros = 0: the plain variable; +1 / -1: values >= 0 / <= 0 with 20 %
+    signed zeros (min / max outputs are zeros)."""
     from pyactivestorage_amd.variable import ChunkedVariable
-    rng = np.random.default_rng(3)
+    rng = np.random.default_rng(3 + zeros)
     a = rng.uniform(0, 100, size=SHAPE).astype("<f4")
+    if zeros:
+        a *= zeros
+        z = rng.random(a.size) < 0.2
+        a.reshape(-1)[z] = np.where(rng.random(int(z.sum())) < 0.5, -0.0, 0.0)
     a.reshape(-1)[::17] = -999.0
     grid = [s // c for s, c in zip(SHAPE, CHUNKS)]
     blobs, index, pos = [], {}, 0
@@ -36,7 +52,9 @@ def make_variable():
         blobs.append(b)
         pos += len(b)
     data = b"".join(blobs)
-    attrs = {"_FillValue": np.array([-999.0], dtype="<f4"), "valid_max": np.array([95.0], dtype="<f4")}
+    attrs = {"_FillValue": np.array([-999.0], dtype="<f4")}
+    if not zeros:
+        attrs["valid_max"] = np.array([95.0], dtype="<f4")
     return ChunkedVariable(name="v", shape=SHAPE, chunks=CHUNKS, dtype="<f4", chunk_index=index,
                            attrs=attrs, reader=lambda off, size: data[off:off + size])
 
@@ -53,6 +71,13 @@ def run_queries(group=None):
         r = act[index]
         out[f"q{k}_data"] = np.ma.getdata(r)
         out[f"q{k}_mask"] = np.ma.getmaskarray(r)
+    zvar = {"min": make_variable(1), "max": make_variable(-1)}
+    for k, (method, index, axis) in enumerate(ZQUERIES):
+        act = Active(zvar[method], axis=axis, group=group)
+        act.method = method
+        r = act[index]
+        out[f"z{k}_data"] = np.ma.getdata(r)
+        out[f"z{k}_mask"] = np.ma.getmaskarray(r)
     return out
 
 

@@ -292,9 +292,62 @@ def main():
                                 axis=[0, 1, 2], method=meth, missing=miss,
                                 codecs={"shuffle": es} if shuffle else {})
 
+    # 5. signed zeros over axis subsets and strided / listed selections: per
+    #    output NumPy visits the reduced elements in its iterator's order
+    #    (elementwise when the innermost dim is kept, reduce calls over the
+    #    trailing reduced dims otherwise), and an unmasked selection is
+    #    reduced as the strided view itself (zerosign.py).  Dense signed
+    #    zeros so most outputs are a zero.
+    axsets = [[0], [1], [2], [0, 1], [1, 2], [0, 2], [0, 1, 2]]
+    zsels = [(slice(None),) * 3, (slice(1, 7), slice(0, 11, 2), slice(3, 37)),
+             (slice(7, 0, -2), slice(None), slice(38, 2, -3)), (slice(None), [0, 3, 4, 9], slice(5, 30)),
+             (slice(2, 5), slice(None), slice(None, None, 4))]
+    zshape2 = (8, 12, 40)
+    for dt in ("<f4", "<f8", ">f8", "<f4s"):
+        shuffle = dt.endswith("s")
+        ndt = np.dtype(dt.rstrip("s"))
+        for pattern in ("min0", "max0", "zeros"):
+            n = int(np.prod(zshape2))
+            arr = np.zeros(n, dtype=ndt) if pattern == "zeros" else \
+                rng.uniform(0.5, 400.0, n).astype(ndt) * (1 if pattern == "min0" else -1)
+            z = rng.random(n) < 0.3
+            arr[z] = np.where(rng.random(int(z.sum())) < 0.5, -0.0, 0.0)
+            arr[rng.choice(n, 25, replace=False)] = -999.0
+            arr = arr.reshape(zshape2)
+            raw = arr.tobytes()
+            es = ndt.itemsize
+            if shuffle:
+                raw = np.frombuffer(raw, dtype=np.uint8).reshape(-1, es).T.reshape(-1).tobytes()
+            for miss in ([None, None, None, None], [-999.0, None, -500.0, 500.0]):
+                for sel in zsels:
+                    for axis in axsets:
+                        for meth in (("ma.min", "max") if pattern != "max0" else ("ma.max", "min")):
+                            add(raw, source="zero-sign-axes", dtype=dt.rstrip("s"), shape=list(zshape2), order="C",
+                                sel=sel, axis=axis, method=meth, missing=miss,
+                                codecs={"shuffle": es} if shuffle else {})
+    # reduce calls longer than np.getbufsize() (pieces inside a call)
+    zshape3 = (3, 40, 300)
+    for dt in ("<f4", ">f8"):
+        ndt = np.dtype(dt)
+        for pattern in ("min0", "zeros"):
+            n = int(np.prod(zshape3))
+            arr = np.zeros(n, dtype=ndt) if pattern == "zeros" else rng.uniform(0.5, 400.0, n).astype(ndt)
+            k = 60 if pattern == "min0" else n // 3
+            pos = rng.choice(n, k, replace=False)
+            arr[pos] = np.where(rng.random(k) < 0.5, -0.0, 0.0)
+            if pattern == "zeros":
+                arr[:] = np.where(rng.random(n) < 0.5, -0.0, 0.0)
+            raw = arr.reshape(zshape3).tobytes()
+            for miss in ([None, None, None, None], [-999.0, None, None, None]):
+                for sel in ((slice(None),) * 3, (slice(None), slice(0, 40, 3), slice(None))):
+                    for axis in ([1, 2], [2], [0, 2], [0, 1, 2]):
+                        for meth in ("ma.min", "min"):
+                            add(raw, source="zero-sign-axes", dtype=dt, shape=list(zshape3), order="C", sel=sel,
+                                axis=axis, method=meth, missing=miss)
+
     sys.path.insert(0, ROOT)
     from pyactivestorage_amd.zerosign import tie_rule
-    rules = {dt: {"lanes": r.lanes, "order": r.order, "piece": r.piece}
+    rules = {dt: {"lanes": r.lanes, "order": r.order, "piece": r.piece, "acc": r.acc, "acc_order": r.acc_order}
              for dt, r in (("f4", tie_rule("f4")), ("f8", tie_rule("f8"))) if r is not None}
     with open(os.path.join(HERE, "reference_cases.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "reference": REF_STORAGE,

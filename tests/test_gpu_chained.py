@@ -109,32 +109,3 @@ def test_chained_hyperslab(gpu, dtype):
     finally:
         gpu.set_chained_combine(True)
         gpu.set_tile_bytes(0)
-
-
-@pytest.mark.parametrize("dtype", ["<f4", "<f8", ">f4", "<i4", ">i2"])
-@pytest.mark.parametrize("tile_bytes", [0, 512])
-@pytest.mark.parametrize("masked", [False, True])
-def test_split_whole_equals_one_launch(gpu, dtype, tile_bytes, masked, monkeypatch):
-    """pyas_reduce_chunks_split (whole chunks on the lean kernel, the rest on
-    the selection-aware one, one k_finish) against one pyas_reduce_chunks
-    launch (PYAS_SPLIT_WHOLE=0, the default), bit for bit: totals and chunk partials,
-    for a box query's mix of whole interior and partial boundary chunks."""
-    n = 1500
-    rng = np.random.default_rng(7 + len(dtype) + tile_bytes)
-    data = _variable(n, dtype, rng)
-    whole = rng.random(n) < 0.7
-    sels = [selection.normalize((slice(None),) * 3 if w else
-                                (slice(int(rng.integers(0, 4)), 8), slice(1, 15, 2), slice(0, 16)), CHUNK)
-            for w in whole]
-    try:
-        monkeypatch.setenv("PYAS_SPLIT_WHOLE", "1")
-        p1, a = _run(gpu, data, dtype, True, tile_bytes, sels, masked, True, True)
-        _, a2 = _run(gpu, data, dtype, True, tile_bytes, sels, masked, True, False)
-        monkeypatch.setenv("PYAS_SPLIT_WHOLE", "0")
-        p0, b = _run(gpu, data, dtype, True, tile_bytes, sels, masked, True, True)
-        assert p1.split is not None and p1.split[1] == int(whole.sum()) and p0.split is None
-        _same(a, b, "split != one launch")
-        _same(a2[:1], b[:1], "split total without chunk_out differs")
-    finally:
-        gpu.set_chained_combine(True)
-        gpu.set_tile_bytes(0)

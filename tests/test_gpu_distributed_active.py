@@ -52,3 +52,9 @@ def test_distributed_active_matches_local(gpu, tmp_path, world):
             np.testing.assert_array_equal(gd[~wm], wd[~wm], err_msg=f"query {k}")
         else:
             np.testing.assert_allclose(gd[~wm], wd[~wm], rtol=1e-6, err_msg=f"query {k}")
+    for k in range(len(D.ZQUERIES)):
+        wd, wm = want[f"z{k}_data"], want[f"z{k}_mask"]
+        gd, gm = got[f"z{k}_data"], got[f"z{k}_mask"]
+        np.testing.assert_array_equal(gm, wm, err_msg=f"zero query {k} mask")
+        assert (wd[~wm] == 0).sum() > 0, k
+        assert gd[~wm].tobytes() == wd[~wm].tobytes(), f"zero query {k}: bytes (zero signs) differ"

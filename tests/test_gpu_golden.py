@@ -46,6 +46,11 @@ def test_report_cancelling_sum_fallbacks(gpu):
     4e-7 * sum|x| (cancelling sums only; see tests/_golden.py check_gpu)."""
     n_float_sums = sum(1 for c in G.cases() if "raises" not in c and c["dtype"].lstrip("<>=|")[0] == "f"
                        and c["method"] in ("ma.sum", "sum", "ma.mean", "mean"))
+    n_zero = sum(1 for i, c in enumerate(G.cases()) if "raises" not in c and c["method"].endswith(("min", "max"))
+                 and c["dtype"].lstrip("<>=|")[0] == "f" and (G.expected(i)[1] == 0).any())
     print(f"\ngolden float sum/mean cases: {n_float_sums}; needing the cancelling-sum bound: "
-          f"{len(FALLBACKS)} {FALLBACKS}; zero min/max sign bits compared: {G.signs_comparable()}")
+          f"{len(FALLBACKS)} {FALLBACKS}; min/max cases with a zero result: {n_zero}; "
+          f"zero sign bits compared: {G.signs_comparable()}")
     assert len(FALLBACKS) <= n_float_sums
+    if not G.signs_comparable():
+        pytest.skip("this host's NumPy breaks zero ties unlike the golden host: zero signs compared by value")

@@ -1,18 +1,27 @@
-"""NumPy's sign of a zero min/max on the device (pyas_zero_sign_chunks /
-pyas_zero_sign_seq, rule from zerosign.py).
+"""NumPy's sign of a zero min/max on the device (pyas_tie_chunks /
+pyas_tie_grid / pyas_tie_segments / pyas_tie_finalize; the rule and its
+host restatement are in zerosign.py, checked against NumPy by
+tests/test_zero_sign.py).
 
-Per chunk (``storage.py:99-100``): the drop-in's per-call path and the
-coalesced pool path return the reference's +0.0 / -0.0 (the golden cases of
-``tests/golden`` hold 420 such chunks made by the reference itself).  Across
-chunks (``active.py:575-598``): ``Active`` reduces the per-chunk results in
-the ``out`` array's C order with ``np.ma.min/max``, so the final zero's sign
-follows the same rule over the chunk sequence; here it is checked against a
-NumPy restatement of that combine.
+Per chunk (``storage.py:95-100``): the drop-in returns the reference's +0.0
+/ -0.0 for every axis subset and selection: masked chunks (``np.ma`` reduces
+a filled copy), unmasked strided and reversed views (NumPy reduces the view
+itself), index lists (a copy laid out with the listed dim outermost),
+big-endian and F-ordered chunks.  Across chunks (``active.py:575-598``):
+``Active`` stores the per-chunk results in the ``out`` array and reduces it
+with ``np.ma.min/max`` again, here restated with the oracle's own
+``reduce_chunk`` and ``combine_partials`` for full and partial-axis queries,
+resident or not, folded in the kernel or in two steps, and under a group of
+ranks (gloo, sharing this GPU).  Every comparison is of bytes: a zero's
+sign bit included.
 """
+import threading
+
 import numpy as np
 import pytest
 
 from oracle import storage_ref as ref
+from pyactivestorage_amd import active as active_mod
 from pyactivestorage_amd import storage as pas
 from pyactivestorage_amd.active import Active
 from pyactivestorage_amd.variable import ChunkedVariable
@@ -21,83 +30,180 @@ from pyactivestorage_amd.zerosign import tie_rule
 pytestmark = pytest.mark.gpu
 
 
-def _chunk(rng, shape, dt, pattern, n_zero=25):
+def _same_bytes(want, got, what):
+    w = np.asarray(np.ma.getdata(want))
+    g = np.asarray(np.ma.getdata(got))
+    assert w.shape == g.shape and w.dtype == g.dtype, (what, w.shape, g.shape, w.dtype, g.dtype)
+    assert np.array_equal(np.ma.getmaskarray(want), np.ma.getmaskarray(got)), what
+    keep = ~np.ma.getmaskarray(want)
+    wk, gk = w[keep], g[keep]
+    nan = np.isnan(wk)
+    assert np.array_equal(nan, np.isnan(gk)), what
+    assert wk[~nan].tobytes() == gk[~nan].tobytes(), (what, wk[~nan][wk[~nan] != gk[~nan]],
+                                                     np.signbit(wk[~nan]).sum(), np.signbit(gk[~nan]).sum())
+
+
+def _chunk(rng, shape, dt, pattern, dens=0.3, n_fill=10):
     n = int(np.prod(shape))
     if pattern == "zeros":
         a = np.zeros(n, dtype=dt)
     else:
         a = rng.uniform(0.5, 9.0, n).astype(dt) * (1 if pattern == "min0" else -1)
-    a[rng.choice(n, n_zero, replace=False)] = np.where(rng.random(n_zero) < 0.5, -0.0, 0.0)
-    a[rng.choice(n, 10, replace=False)] = -999.0
+    z = rng.random(n) < dens
+    a[z] = np.where(rng.random(int(z.sum())) < 0.5, -0.0, 0.0)
+    a[rng.choice(n, n_fill, replace=False)] = -999.0
     return a.reshape(shape)
+
+
+SELS = [(slice(None),) * 3, (slice(1, 11), slice(2, 19), slice(0, 66, 3)),
+        (slice(11, 0, -2), slice(None), slice(60, 3, -1)), (slice(None), [0, 3, 4, 17], slice(5, 50)),
+        (2, slice(None), slice(None, None, 4))]
+AXES = [(0,), (1,), (2,), (0, 1), (1, 2), (0, 2), (0, 1, 2)]
 
 
 @pytest.mark.parametrize("dt", ["<f4", ">f8"])
 @pytest.mark.parametrize("pattern", ["min0", "max0", "zeros"])
-def test_per_call_chunk_sign(gpu, dt, pattern):
-    rng = np.random.default_rng(len(dt) * 7 + len(pattern))
+@pytest.mark.parametrize("order", ["C", "F"])
+def test_per_call_chunk_sign(gpu, dt, pattern, order):
+    """storage.py:95-100 per call: every selection kind x axis subset, with
+    and without a mask attribute, against the oracle byte for byte."""
+    if tie_rule(dt) is None:
+        pytest.skip("no NumPy tie rule derived on this host")
+    rng = np.random.default_rng(len(dt) * 7 + len(pattern) + len(order))
     shape = (12, 20, 70)                               # > one 8192-element iterator piece
-    full = (slice(None),) * 3
-    box = (slice(1, 11), slice(2, 19), slice(0, 66, 3))
-    for trial in range(6):
-        a = _chunk(rng, shape, np.dtype(dt), pattern)
-        raw = a.tobytes()
-        for miss in ((None, None, None, None), (np.dtype(dt).type(-999.0), None, None, None)):
-            for sel in ((full,) if miss[0] is None else (full, box)):
-                for method in (np.ma.min, np.ma.max, np.min, np.max):
-                    want, _ = ref.reduce_chunk_bytes(raw, None, None, miss, dt, shape, "C", sel, (0, 1, 2), method)
-                    got, _ = pas.reduce_chunk_bytes(raw, None, None, miss, dt, shape, "C", sel, (0, 1, 2), method)
-                    w, g = np.ma.getdata(want).reshape(-1)[0], np.ma.getdata(got).reshape(-1)[0]
-                    assert w == g or (np.isnan(w) and np.isnan(g)), (trial, method, w, g)
-                    if w == 0:
-                        assert np.signbit(w) == np.signbit(g), (trial, miss, sel, method.__name__, w, g)
+    a = _chunk(rng, shape, np.dtype(dt), pattern)
+    raw = (np.asfortranarray(a) if order == "F" else a).tobytes(order="A")
+    methods = (np.ma.min, np.min) if pattern != "max0" else (np.ma.max, np.max)
+    for miss in ((None, None, None, None), (np.dtype(dt).type(-999.0), None, None, None)):
+        for sel in SELS:
+            for axis in AXES:
+                if isinstance(sel[0], int):   # dim 0 dropped: a 2-D result
+                    axis = tuple(sorted({min(x, 1) for x in axis}))
+                for method in methods:
+                    want, wn = ref.reduce_chunk_bytes(raw, None, None, miss, dt, shape, order, sel, axis, method)
+                    got, gn = pas.reduce_chunk_bytes(raw, None, None, miss, dt, shape, order, sel, axis, method)
+                    _same_bytes(want, got, (miss[0], sel, axis, method.__name__))
+                    assert np.array_equal(wn, gn)
 
 
-def _reference_combine(arr, chunks, miss_fill, method):
-    """active.py:575-598 over storage.py's per-chunk results: per-chunk
-    np.ma.min/max into `out` (the variable dtype, masked where a chunk is
-    all masked), then np.ma.min/max over `out`."""
-    grid = tuple(s // c for s, c in zip(arr.shape, chunks))
-    out = np.ma.masked_all(grid, dtype=arr.dtype)
+def _variable(a, chunks, attrs):
+    shape = a.shape
+    grid = [-(-s // c) for s, c in zip(shape, chunks)]
+    blobs, index, pos = [], {}, 0
     for cc in np.ndindex(*grid):
-        sl = tuple(slice(i * c, (i + 1) * c) for i, c in zip(cc, chunks))
-        tmp = np.ma.masked_equal(arr[sl], miss_fill)
-        r = method(tmp, axis=(0, 1, 2), keepdims=True)
-        out[cc] = r.reshape(())
-    return method(out, axis=(0, 1, 2), keepdims=True)
+        blk = np.full(chunks, -999.0, dtype=a.dtype)   # edge chunks padded like HDF5
+        sl = tuple(slice(i * c, min((i + 1) * c, s)) for i, c, s in zip(cc, chunks, shape))
+        blk[tuple(slice(0, x.stop - x.start) for x in sl)] = a[sl]
+        b = blk.tobytes()
+        index[cc] = (pos, len(b))
+        blobs.append(b)
+        pos += len(b)
+    data = b"".join(blobs)
+    return ChunkedVariable(name="v", shape=shape, chunks=chunks, dtype=a.dtype.str, chunk_index=index,
+                           attrs=attrs, reader=lambda off, size: data[off:off + size]), data
+
+
+def _reference_active(a, chunks, index, axis, kind, missing, data_of):
+    """active.py:487-630 over storage.py's reduce_chunk (the oracle's),
+    for an index of positive-step slices."""
+    shape = a.shape
+    picks, per_dim = [], []
+    for d, s in enumerate(index):
+        idx = np.arange(shape[d])[s]
+        c = chunks[d]
+        coords = sorted(set((idx // c).tolist()))
+        per_dim.append([(k, idx[idx // c == k]) for k in coords])
+    out_shape = [len(per_dim[d]) if d in axis else sum(len(x) for _, x in per_dim[d]) for d in range(a.ndim)]
+    method = np.ma.min if kind == "min" else np.ma.max
+    parts = []
+    for combo in np.ndindex(*[len(p) for p in per_dim]):
+        cc, csel, osel = [], [], []
+        for d, j in enumerate(combo):
+            k, ids = per_dim[d][j]
+            cc.append(k)
+            step = index[d].step or 1
+            local = ids - k * chunks[d]
+            csel.append(slice(int(local[0]), int(local[-1]) + 1, step))
+            if d in axis:
+                osel.append(slice(j, j + 1))
+            else:
+                before = sum(len(x) for _, x in per_dim[d][:j])
+                osel.append(slice(before, before + len(ids)))
+        raw = data_of(tuple(cc))
+        tmp, n = ref.reduce_chunk_bytes(raw, None, None, missing, a.dtype.str, chunks, "C", tuple(csel),
+                                        tuple(axis), method)
+        parts.append((tmp, n, tuple(osel)))
+    return ref.combine_partials(parts, out_shape, a.dtype, tuple(axis), kind)
+
+
+QUERIES = [(slice(None),) * 3, (slice(1, 15), slice(3, 21), slice(2, 75)), (slice(0, 16, 3), slice(None), slice(7, 80, 2))]
 
 
 @pytest.mark.parametrize("dt", ["<f4", "<f8"])
 @pytest.mark.parametrize("kind", ["min", "max"])
-@pytest.mark.parametrize("resident", [False, True])
-def test_active_combine_sign(gpu, dt, kind, resident):
+@pytest.mark.parametrize("fill", [True, False])
+def test_active_sign(gpu, dt, kind, fill):
+    """Active full and partial-axis min/max (fold and two-step paths,
+    resident and not) against active.py's combine over storage.py's
+    per-chunk results: the zero's sign bit included."""
     if tie_rule(dt) is None:
         pytest.skip("no NumPy tie rule derived on this host")
-    rng = np.random.default_rng(3 + len(kind) + resident)
-    shape, chunks = (8, 12, 40), (4, 4, 10)
-    method = np.ma.min if kind == "min" else np.ma.max
-    for trial in range(5):
-        a = np.full(shape, 5.0 if kind == "min" else -5.0, dtype=dt)
-        n = a.size
-        z = rng.choice(n, 30, replace=False)
-        a.reshape(-1)[z] = np.where(rng.random(30) < 0.5, -0.0, 0.0)
-        a.reshape(-1)[rng.choice(n, 10, replace=False)] = -999.0
-        blobs, index, pos = [], {}, 0
-        grid = [s // c for s, c in zip(shape, chunks)]
-        for cc in np.ndindex(*grid):
-            sl = tuple(slice(i * c, (i + 1) * c) for i, c in zip(cc, chunks))
-            b = np.ascontiguousarray(a[sl]).tobytes()
-            index[cc] = (pos, len(b))
-            blobs.append(b)
-            pos += len(b)
-        data = b"".join(blobs)
-        var = ChunkedVariable(name="v", shape=shape, chunks=chunks, dtype=dt, chunk_index=index,
-                              attrs={"_FillValue": np.array([-999.0], dtype=dt)},
-                              reader=lambda off, size: data[off:off + size])
-        act = Active(var, resident=resident)
-        act.method = kind
-        got = act[...]
-        want = _reference_combine(a, chunks, np.dtype(dt).type(-999.0), method)
-        w, g = np.ma.getdata(want).reshape(-1)[0], np.ma.getdata(got).reshape(-1)[0]
-        assert w == g == 0, (trial, w, g)
-        assert np.signbit(w) == np.signbit(g), (trial, kind, w, g)
+    rng = np.random.default_rng(3 + len(kind) + fill + len(dt))
+    shape, chunks = (16, 24, 80), (4, 8, 20)
+    a = _chunk(rng, shape, np.dtype(dt), "min0" if kind == "min" else "max0", dens=0.2, n_fill=10 if fill else 0)
+    attrs = {"_FillValue": np.array([-999.0], dtype=dt)} if fill else {}
+    missing = (np.dtype(dt).type(-999.0), None, None, None) if fill else (None, None, None, None)
+    var, data = _variable(a, chunks, attrs)
+    data_of = lambda cc: data[var.chunk_index[cc][0]: var.chunk_index[cc][0] + var.chunk_index[cc][1]]
+    for q in QUERIES:
+        for axis in [(0, 1, 2)] + AXES[:6]:
+            want = _reference_active(a, chunks, q, axis, kind, missing, data_of)
+            for resident in (False, True):
+                for fold in (True, False):
+                    old = active_mod._AXES_FOLD
+                    active_mod._AXES_FOLD = fold
+                    try:
+                        act = Active(var, axis=axis, resident=resident)
+                        act.method = kind
+                        got = act[q]
+                        act.method = kind                    # (reset after each query, active.py:633)
+                        got2 = act[q] if resident else got   # a cached replay
+                    finally:
+                        active_mod._AXES_FOLD = old
+                    _same_bytes(want, got, (q, axis, resident, fold))
+                    _same_bytes(want, got2, (q, axis, "replay"))
+            active_mod.release_resident(var)
+
+
+def test_replay_threads_share_a_query(gpu):
+    """8 threads replaying ONE cached resident min query on data
+    with mixed signed zeros all get the reference's sign (the replay holds
+    the query's lock across its launches and copies)."""
+    rng = np.random.default_rng(77)
+    shape, chunks = (16, 24, 80), (4, 8, 20)
+    a = _chunk(rng, shape, np.dtype("<f4"), "min0", dens=0.1)
+    var, data = _variable(a, chunks, {"_FillValue": np.array([-999.0], dtype="<f4")})
+    data_of = lambda cc: data[var.chunk_index[cc][0]: var.chunk_index[cc][0] + var.chunk_index[cc][1]]
+    missing = (np.float32(-999.0), None, None, None)
+    for axis in ((0, 1, 2), (0,), (0, 2)):
+        want = _reference_active(a, chunks, (slice(None),) * 3, axis, "min", missing, data_of)
+        act = Active(var, axis=axis, resident=True)
+        act.method = "min"
+        act[...]
+        errors = []
+
+        def worker():
+            try:
+                for _ in range(20):
+                    x = Active(var, axis=axis, resident=True)
+                    x.method = "min"
+                    _same_bytes(want, x[...], axis)
+            except Exception as exc:   # noqa: BLE001 - reported below
+                errors.append(exc)
+        ts = [threading.Thread(target=worker) for _ in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors[0]
+    active_mod.release_resident(var)

@@ -223,7 +223,11 @@ def test_capi_struct_layouts():
     assert ctypes.sizeof(_lib.Scalar) == 8
     assert _lib.Batch.data.offset == 4 * 4 + 8 * _lib.MAX_DIMS + 8
     assert ctypes.sizeof(_lib.Mask) == 4 + 8 + 16 + 16 + 8 + 8 + 16 + 16 + 2 * 8 * _lib.MAX_DIMS + 4  # padding
-    assert ctypes.sizeof(_lib.ChunkDesc) == 4 * 4 + 8 * _lib.MAX_DIMS + 4 + 4
+    assert ctypes.sizeof(_lib.TieGeom) == 4 * _lib.MAX_DIMS + 4
+    assert ctypes.sizeof(_lib.TieRule) == 3 * 4 + 64 + 64
+    assert ctypes.sizeof(_lib.ChunkDesc) == 4 * 4 + 8 * _lib.MAX_DIMS + 4 + 4 + 4 + ctypes.sizeof(_lib.TieGeom)
+    from pyactivestorage_amd import _fastpath   # the C side's own sizeof
+    assert _fastpath.CHUNK_DESC_SIZE == ctypes.sizeof(_lib.ChunkDesc)
 
 
 def test_capi_errors_without_gpu_are_reported():
