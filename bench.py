@@ -54,6 +54,13 @@ CONFIGS = {
     "c5": dict(shape=(4096, 2048, 1024), chunks=(32, 32, 32), dtype="f8", shuffle=False,
                masked=True, hyperslab=16,
                desc="4096x2048x1024 f64, 32^3 chunks, hyperslab [16:-16]^3, masked mean"),
+    # small shapes of C3 / C4 / C5 for the N-rank rehearsal tests (not bench lines)
+    "t3": dict(shape=(256, 256, 256), chunks=(64, 64, 64), dtype="f4", shuffle=False,
+               masked=True, hyperslab=None, desc="test: 256^3 f32, 64^3 chunks, masked"),
+    "t4": dict(shape=(256, 256, 256), chunks=(128, 128, 128), dtype="f4", shuffle=True,
+               masked=True, hyperslab=None, desc="test: 256^3 f32, 128^3 chunks, shuffle + mask"),
+    "t5": dict(shape=(256, 128, 128), chunks=(32, 32, 32), dtype="f8", shuffle=False,
+               masked=True, hyperslab=16, desc="test: 256x128x128 f64, 32^3 chunks, hyperslab, masked"),
 }
 FILL = -999.0
 VMIN = 1000.0
@@ -80,6 +87,10 @@ def parse(argv=None):
     p.add_argument("--force-dist", action="store_true",
                    help="rehearsal: run the RCCL branch (init, all-gather, device combine) "
                         "even at world size 1 (launch under torch.distributed.run)")
+    p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                   help="nccl (= RCCL, one GPU per rank); gloo: the same N-rank body with the "
+                        "exchange staged through host memory, ranks may share a GPU (rehearsal "
+                        "of --gpus N on a smaller box)")
     p.add_argument("--host-inclusive", type=int, default=1,
                    help="also time pinned host -> H2D -> reduce -> D2H (rank 0, N=1)")
     p.add_argument("--file-inclusive", type=int, default=1,
@@ -104,18 +115,40 @@ def _free_port() -> int:
     return port
 
 
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without any HIP call: the KFD
+    topology in sysfs (nodes with a non-zero gpu_id), narrowed by the
+    *_VISIBLE_DEVICES variables.  -1 when sysfs cannot be read."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for node in os.listdir(root):
+            with open(os.path.join(root, node, "gpu_id")) as f:
+                n += int(f.read().strip() or 0) != 0
+    except (OSError, ValueError):
+        return -1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks(n: int, argv, check_devices: bool = True, timeout: float | None = None) -> int:
     """Start ``n`` rank processes of this script (one per GPU) and wait.
 
-    Runs in a process that has not touched the GPU (counting devices does
-    not initialise it), and starts children rather than exec'ing, so no
+    Runs in a process that has not touched the GPU (it counts devices from
+    sysfs, :func:`visible_gpus`, and every rank checks the count again once
+    its runtime is up), and starts children rather than exec'ing, so no
     GPU-initialised process is ever replaced.  Exits non-zero if fewer than
     ``n`` devices are visible: the bench never silently runs fewer ranks.
     If one rank fails the others are stopped (they would wait forever in
     the next collective)."""
     if check_devices:
-        import torch
-        have = torch.cuda.device_count()
+        have = visible_gpus()
+        if have < 0:   # no KFD topology readable: the runtime's count (amdsmi; no HIP init here)
+            import torch
+            have = torch.cuda.device_count()
         if have < n:
             print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
             return 2
@@ -220,10 +253,12 @@ def chunk_selections(cfg, gshape, lo, hi):
     return table, cnt.prod(axis=1)
 
 
-def cpu_baseline(cfg, host_chunks: np.ndarray, n_chunks: int, missing, threads: int):
+def cpu_baseline(cfg, host_chunks: np.ndarray, n_chunks: int, missing, threads: int, check_minmax=False):
     """Time the oracle (NumPy restatement of storage.reduce_chunk + the
     Active combine) on a page-cache-hot chunk-major file, fanned out over a
-    ThreadPoolExecutor like active.py:557-572."""
+    ThreadPoolExecutor like active.py:557-572.  Returns (seconds, the
+    oracle's mean components {"sum", "n"}, and with ``check_minmax`` its
+    min and max over the same chunks, untimed)."""
     import concurrent.futures
 
     from oracle import storage_ref as ref
@@ -250,9 +285,41 @@ def cpu_baseline(cfg, host_chunks: np.ndarray, n_chunks: int, missing, threads: 
                 parts.append((tmp, cnt, (slice(c, c + 1), slice(0, 1), slice(0, 1))))
         out = ref.combine_partials(parts, (n_chunks, 1, 1), dt, axis, "mean", components=True)
         dt_s = time.perf_counter() - t0
+        if check_minmax:
+            for kind, fn in (("min", np.ma.min), ("max", np.ma.max)):
+                with concurrent.futures.ThreadPoolExecutor(max_workers=threads) as ex:
+                    futs = [ex.submit(ref.reduce_chunk, path, c * chunk_bytes, chunk_bytes, None, filters,
+                                      missing, dt, cfg["chunks"], "C", sel, axis, fn)
+                            for c in range(n_chunks)]
+                    mp = [(fu.result()[0], None, (slice(c, c + 1), slice(0, 1), slice(0, 1)))
+                          for c, fu in enumerate(futs)]
+                out[kind] = ref.combine_partials(mp, (n_chunks, 1, 1), dt, axis, kind)
     finally:
         os.unlink(path)
     return dt_s, out
+
+
+def oracle_check(gpu_result, oracle, dt):
+    """The GPU's full-size result against the oracle's storage.py +
+    _from_storage combine over the same chunks (active.py:575-630): count,
+    min and max exact (bytes, a zero's sign included), mean within 1e-6
+    relative."""
+    n = int(np.asarray(oracle["n"]).reshape(-1)[0])
+    osum = np.asarray(np.ma.getdata(oracle["sum"])).reshape(-1)[0]
+    omean = float(osum) / n if n else float("nan")
+    gmean = float(np.asarray(gpu_result["sum"], dtype=dt).astype(np.float64)) / gpu_result["count"] \
+        if gpu_result["count"] else float("nan")
+    rep = {"count": [gpu_result["count"], n], "mean": [gmean, omean]}
+    ok = gpu_result["count"] == n and abs(gmean - omean) <= 1e-6 * abs(omean)
+    for kind in ("min", "max"):
+        if kind in oracle:
+            ov = np.asarray(np.ma.getdata(oracle[kind])).reshape(-1)[0]
+            gv = np.asarray(gpu_result[kind], dtype=dt)
+            rep[kind] = [float(gv), float(ov)]
+            ok = ok and gv.tobytes() == np.asarray(ov, dtype=dt).tobytes()
+    rep["ok"] = bool(ok)
+    rep["bar"] = "count/min/max bit-exact, mean <= 1e-6 relative"
+    return rep
 
 
 def host_inclusive(torch, ctx, data, cfg, dt, missing, reps=3, groups=16):
@@ -367,9 +434,10 @@ def run_config(env, name, scaling, steps, warmup, args, full_check=False):
     partials.  Returns the per-config report (on every rank)."""
     torch, dist, ctx, dev, stream = env["torch"], env["dist"], env["ctx"], env["dev"], env["stream"]
     rank, world, use_dist = env["rank"], env["world"], env["use_dist"]
+    coll_dev = env["coll_dev"]   # where collective tensors live (the GPU for RCCL, the host for gloo)
     from pyactivestorage_amd import _lib, engine
     from pyactivestorage_amd.batch import ReductionPlan
-    from pyactivestorage_amd.distributed import reduce_sharded, shard_ranges
+    from pyactivestorage_amd.distributed import all_gather_bytes, reduce_sharded, shard_ranges
     from pyactivestorage_amd.synthetic import chunk_major_device
 
     cfg = CONFIGS[name]
@@ -452,8 +520,8 @@ def run_config(env, name, scaling, steps, warmup, args, full_check=False):
     mine = [elapsed, kern_ms, ex_ms if ex_ms is not None else -1.0, float(bytes_per_launch),
             float(n_chunks), t_gen]
     if use_dist:
-        t = torch.tensor(mine, dtype=torch.float64, device=dev)
-        allr = torch.empty(world * len(mine), dtype=torch.float64, device=dev)
+        t = torch.tensor(mine, dtype=torch.float64, device=coll_dev)
+        allr = torch.empty(world * len(mine), dtype=torch.float64, device=coll_dev)
         dist.all_gather_into_tensor(allr, t)
         per = allr.view(world, len(mine)).cpu().numpy()
     else:
@@ -475,10 +543,8 @@ def run_config(env, name, scaling, steps, warmup, args, full_check=False):
     else:
         result = local_total
     cparts = plan.read_chunk_partials(stream)
-    if use_dist:
-        allparts = [None] * world
-        dist.all_gather_object(allparts, cparts.tobytes())
-        cat = b"".join(allparts)
+    if use_dist:   # every rank's chunk partials (32 B each), as tensors
+        cat = b"".join(all_gather_bytes(torch, cparts.tobytes(), coll_dev))
     else:
         cat = cparts.tobytes()
     selfcheck = None
@@ -527,7 +593,8 @@ def main():
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         # plain `python bench.py --gpus N`: become the launcher of N ranks
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:], check_devices=not args.selftest_launch))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:],
+                              check_devices=not args.selftest_launch and args.dist_backend == "nccl"))
     world = int(world_env or 1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -542,21 +609,29 @@ def main():
     import torch.distributed as dist
 
     use_dist = world > 1 or args.force_dist
+    ndev = torch.cuda.device_count()
+    gloo = args.dist_backend == "gloo"
+    if not gloo and ndev < world:   # each rank checks the launcher's sysfs count
+        print(f"bench.py: rank {rank}: WORLD_SIZE {world} but {ndev} GPU(s) visible", file=sys.stderr)
+        sys.exit(2)
+    gpu = local % max(ndev, 1) if gloo else local   # gloo rehearsal: ranks may share a GPU
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from pyactivestorage_amd.device import get_context
 
-    ctx = get_context(local)
+    ctx = get_context(gpu)
     if args.tile_bytes:
         ctx.set_tile_bytes(args.tile_bytes)
     env = dict(torch=torch, dist=dist, ctx=ctx, dev=dev, stream=torch.cuda.current_stream().cuda_stream,
-               rank=rank, world=world, use_dist=use_dist)
+               rank=rank, world=world, use_dist=use_dist,
+               coll_dev=torch.device("cpu") if gloo else dev)
 
     cfg = CONFIGS[args.config]
     dt = np.dtype(cfg["dtype"])
@@ -574,7 +649,7 @@ def main():
         pass
 
     # CPU baseline and host/file-inclusive legs: rank 0 at N=1 only
-    cpu = hostinc = fileinc = None
+    cpu = hostinc = fileinc = ocheck = None
     if rank == 0 and world == 1 and (args.cpu_chunks > 0 or args.host_inclusive or args.file_inclusive):
         from pyactivestorage_amd.synthetic import chunk_major_device
         data, _, _ = chunk_major_device(torch, cfg["shape"], cfg["chunks"], dt, dev,
@@ -588,7 +663,11 @@ def main():
         if args.cpu_chunks > 0:
             nc = min(args.cpu_chunks, n_chunks)
             host = data[: nc * cb].cpu().numpy()
-            secs, _ = cpu_baseline(cfg, host, nc, missing, args.cpu_threads)
+            full = nc == n_chunks and args.scaling == "weak" and cfg["hyperslab"] is None
+            secs, oracle = cpu_baseline(cfg, host, nc, missing, args.cpu_threads, check_minmax=full)
+            if full:   # the GPU's full-size result against the oracle's (not timed)
+                ocheck = oracle_check(head["result"], oracle, dt)
+                ocheck["chunks"] = nc
             ncores = len(os.sched_getaffinity(0))
             cpu = {"value": round(nc * cb / secs / 1e9, 4), "unit": "GB/s",
                    "cores": min(args.cpu_threads, ncores), "kind": "port",
@@ -628,6 +707,7 @@ def main():
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": head["dtype"], "data": "synthetic",
             "config": {"workload": f"{args.config}: {cfg['desc']}", "variable": head["variable"],
+                       "exchange": (args.dist_backend if use_dist else None),
                        "chunk_shape": head["chunk_shape"], "chunks_total": head["chunks_total"],
                        "chunks_rank0": head["chunks_rank0"], "bytes_rank0": head["bytes_rank0"],
                        "parallelism": f"chunk-shard x{world}",
@@ -636,12 +716,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "traffic_source": "profiles/traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
-                                           "pass of this config, per launch)",
+                         "traffic_source": "profile figure, not measured in this run: profiles/traffic.json "
+                                           "(rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of this config's "
+                                           "k_reduce, per launch)",
                          "kernel": "pyas::k_reduce", "kernel_ms_avg": head["kernel_ms_rank0"],
                          "bytes_per_launch": head["bytes_rank0"]},
             "per_rank": head["per_rank"],
             "cpu_baseline": cpu,
+            "oracle_check": ocheck,
             "result": head["result"], "check": head["check"], "selfcheck": head["selfcheck"],
             "host_inclusive": hostinc, "file_inclusive": fileinc,
             "extra": extra or None,

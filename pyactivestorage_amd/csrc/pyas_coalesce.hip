@@ -49,6 +49,7 @@
 
 #include "pyas.h"
 #include "pyas_internal.hpp"
+#include "pyas_queue.hpp"
 
 namespace {
 
@@ -72,7 +73,7 @@ int es_of(int dtype) {
     }
 }
 
-enum State { RESERVED = 0, FILLED = 1, SKIP = 2, SUBMITTED = 3, DONE = 4 };
+constexpr int SKIP = pyas::kSkip, SUBMITTED = pyas::kSubmitted;
 
 // What one launch group shares; compared bytewise (zero-initialised).
 struct Key {
@@ -80,21 +81,20 @@ struct Key {
     pyas_mask mask;
 };
 
-struct Req {
+// ring_off / span / state / cv: pyas::QItem (pyas_queue.hpp)
+struct Req : pyas::QItem {
     Key key;
     int32_t sel[PYAS_MAX_DIMS * 3];
     bool has_sel = false;
     const int32_t *pool = nullptr;  // caller memory, valid while it waits
     int32_t pool_len = 0;
-    int64_t ring_off = 0, nbytes = 0, span = 0;
+    int64_t nbytes = 0;
     int64_t n_out = 0;
     int64_t chunk_bytes = 0;        // decoded bytes
     pyas_partial *out = nullptr;    // caller memory
     int64_t *info = nullptr;
-    int state = RESERVED;
     int rc = PYAS_OK;
     std::string err;
-    std::condition_variable cv;     // DONE (waited on with the coalescer's mutex)
 };
 
 struct Group {
@@ -172,13 +172,8 @@ struct pyas_coalescer {
     int32_t max_batch = 4096;
     uint8_t *hring = nullptr;   // pinned
     uint8_t *dring = nullptr;   // device mirror (same offsets)
-    int64_t head = 0;           // next free byte
-    std::deque<Req *> fifo;     // reservation order == ring order
-    std::mutex mu;
-    std::condition_variable cv_disp, cv_space;
+    pyas::BatchQueue<Req, Slot> *q = nullptr;   // ring, FIFO and hand-offs; its mutex guards the stats
     std::thread disp, comp;
-    bool stop = false;
-    bool disp_done = false;
     hipStream_t cst = nullptr;   // H2D chunk copies (callers' in caller-copy mode; the
                                  // dispatcher's unless PYAS_COALESCE_COPYSTREAM=0)
     bool copy_stream = true;
@@ -190,9 +185,6 @@ struct pyas_coalescer {
     // stream's inflate latency), so one batch runs while the next gathers.
     int32_t depth = 1;
     std::vector<Slot *> slots;
-    std::deque<Slot *> free_slots, inflight;
-    int64_t n_sub = 0;           // fifo[0, n_sub) are submitted, in flight
-    std::condition_variable cv_comp, cv_slot;
     // Measured on the box (tools/bench_dropin.py): with 30 reader threads on a
     // 16-CPU host share, the dispatcher copying the batch's prefix and
     // sleeping on its completion event leaves the most CPU to the readers.
@@ -205,38 +197,6 @@ struct pyas_coalescer {
 };
 
 namespace {
-
-// Reserve `span` ring bytes (lock held).  Returns the offset or -1 if the
-// request can never fit.
-int64_t ring_reserve(pyas_coalescer *c, std::unique_lock<std::mutex> &lk, int64_t span) {
-    if (span > c->ring_bytes) return -1;
-    for (;;) {
-        if (c->stop) return -1;
-        if (c->fifo.empty()) {       // everything free: restart at 0
-            c->head = span;
-            return 0;
-        }
-        // in use: [front, head) when head > front, else [front, R) + [0, head)
-        // (head == front with requests queued means full)
-        const int64_t front = c->fifo.front()->ring_off;
-        if (c->head > front) {       // free: [head, R) and [0, front)
-            if (c->ring_bytes - c->head >= span) {
-                const int64_t off = c->head;
-                c->head += span;
-                return off;
-            }
-            if (front >= span) {     // wrap
-                c->head = span;
-                return 0;
-            }
-        } else if (c->head < front && front - c->head >= span) {   // free: [head, front)
-            const int64_t off = c->head;
-            c->head += span;
-            return off;
-        }
-        c->cv_space.wait(lk);
-    }
-}
 
 // Host bounds check of one selection row (the device trusts it).
 bool sel_ok(const pyas_chunk_desc &d, const int32_t *sel, const int32_t *pool, int32_t pool_len,
@@ -544,75 +504,37 @@ void finish_batch(pyas_coalescer *c, Slot *sl) {
 
 void dispatcher(pyas_coalescer *c) {
     (void)hipSetDevice(c->device);
-    std::unique_lock<std::mutex> lk(c->mu);
-    for (;;) {
-        auto ready = [&] {
-            return (int64_t)c->fifo.size() > c->n_sub && c->fifo[c->n_sub]->state != RESERVED;
-        };
-        c->cv_disp.wait(lk, [&] { return ready() || (c->stop && (int64_t)c->fifo.size() == c->n_sub); });
-        if (!ready()) break;   // stopping, nothing unsubmitted
-        c->cv_slot.wait(lk, [&] { return !c->free_slots.empty(); });
-        Slot *sl = c->free_slots.front();
-        c->free_slots.pop_front();
-        sl->batch.clear();
-        for (int64_t i = c->n_sub; i < (int64_t)c->fifo.size(); ++i) {
-            Req *r = c->fifo[i];
-            if ((int32_t)sl->batch.size() >= c->max_batch) break;
-            if (r->state != FILLED && r->state != SKIP) break;
-            sl->batch.push_back(r);
-        }
-        for (Req *r : sl->batch)
-            if (r->state == FILLED) r->state = SUBMITTED;
-        c->n_sub += (int64_t)sl->batch.size();
-        lk.unlock();
+    Slot *sl = nullptr;
+    while (c->q->next_batch(sl)) {
         const int64_t t0 = now_ns();
         launch_batch(c, sl);
         const int64_t t1 = now_ns();
         sl->t_launched = t1;
-        lk.lock();
-        c->busy_ns += t1 - t0;
-        c->inflight.push_back(sl);
-        c->cv_comp.notify_one();
+        c->q->launched(sl, [&] { c->busy_ns += t1 - t0; });
     }
-    c->disp_done = true;
-    c->cv_comp.notify_one();
+    c->q->dispatcher_done();
 }
 
 void completer(pyas_coalescer *c) {
     (void)hipSetDevice(c->device);
-    std::unique_lock<std::mutex> lk(c->mu);
-    for (;;) {
-        c->cv_comp.wait(lk, [&] { return !c->inflight.empty() || c->disp_done; });
-        if (c->inflight.empty()) break;   // the dispatcher has stopped and everything completed
-        Slot *sl = c->inflight.front();
-        c->inflight.pop_front();
-        lk.unlock();
+    Slot *sl = nullptr;
+    while (c->q->next_done(sl)) {
         finish_batch(c, sl);
         const int64_t t_done = now_ns();
-        lk.lock();
-        // time this batch held the device queue: from its launch (or the
-        // previous batch's completion, if later) to its completion
-        c->gpu_ns += t_done - (sl->t_launched > c->t_last_done ? sl->t_launched : c->t_last_done);
-        c->t_last_done = t_done;
-        int64_t nch = 0;
-        for (Req *r : sl->batch) {
-            if (r->state == SUBMITTED) ++nch;
-            if (r->rc != PYAS_OK) ++c->n_back;
-            r->state = DONE;
-        }
-        // batches complete in submission order == the fifo's order
-        for (size_t i = 0; i < sl->batch.size(); ++i) c->fifo.pop_front();
-        c->n_sub -= (int64_t)sl->batch.size();
-        c->n_batches += 1;
-        c->n_chunks += nch;
-        if (nch > c->max_seen) c->max_seen = nch;
-        // wake exactly this batch's callers (one condition variable each:
-        // a shared notify_all would wake every waiting caller per batch)
-        for (Req *r : sl->batch) r->cv.notify_one();
-        sl->batch.clear();
-        c->free_slots.push_back(sl);
-        c->cv_slot.notify_one();
-        c->cv_space.notify_all();
+        c->q->complete(sl, [&] {
+            // time this batch held the device queue: from its launch (or the
+            // previous batch's completion, if later) to its completion
+            c->gpu_ns += t_done - (sl->t_launched > c->t_last_done ? sl->t_launched : c->t_last_done);
+            c->t_last_done = t_done;
+            int64_t nch = 0;
+            for (Req *r : sl->batch) {
+                if (r->state == SUBMITTED) ++nch;
+                if (r->rc != PYAS_OK) ++c->n_back;
+            }
+            c->n_batches += 1;
+            c->n_chunks += nch;
+            if (nch > c->max_seen) c->max_seen = nch;
+        });
     }
 }
 
@@ -628,6 +550,7 @@ int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch, 
     c->device = pyas::ctx_device(ctx);
     c->ring_bytes = align_up(ring_bytes > 0 ? ring_bytes : kDefaultRing, kAlign);
     c->max_batch = max_batch > 0 ? max_batch : 4096;
+    c->q = new pyas::BatchQueue<Req, Slot>(c->ring_bytes, c->max_batch);
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->hring, (size_t)c->ring_bytes, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc((void **)&c->dring, (size_t)c->ring_bytes);
@@ -645,7 +568,7 @@ int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch, 
         if (e == hipSuccess) e = hipEventCreateWithFlags(&sl->ev_copy, hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&sl->st, hipStreamNonBlocking);
         c->slots.push_back(sl);
-        c->free_slots.push_back(sl);
+        c->q->add_slot(sl);
     }
     if (e != hipSuccess) {
         for (Slot *sl : c->slots) {
@@ -657,6 +580,7 @@ int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch, 
         if (c->cst) (void)hipStreamDestroy(c->cst);
         if (c->hring) (void)hipHostFree(c->hring);
         if (c->dring) (void)hipFree(c->dring);
+        delete c->q;
         delete c;
         return pyas::set_error(e == hipErrorOutOfMemory ? PYAS_ENOMEM : PYAS_EDEVICE, hipGetErrorString(e));
     }
@@ -668,12 +592,7 @@ int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch, 
 
 int pyas_coalescer_destroy(pyas_coalescer *c) {
     if (!c) return PYAS_OK;
-    {
-        std::lock_guard<std::mutex> lk(c->mu);
-        c->stop = true;
-    }
-    c->cv_disp.notify_all();
-    c->cv_space.notify_all();
+    c->q->stop();
     if (c->disp.joinable()) c->disp.join();
     if (c->comp.joinable()) c->comp.join();
     (void)hipSetDevice(c->device);
@@ -694,13 +613,14 @@ int pyas_coalescer_destroy(pyas_coalescer *c) {
     }
     (void)hipHostFree(c->hring);
     (void)hipFree(c->dring);
+    delete c->q;
     delete c;
     return PYAS_OK;
 }
 
 int pyas_coalescer_stats(pyas_coalescer *c, int64_t *stats) {
     if (!c || !stats) return pyas::set_error(PYAS_EINVAL, "NULL argument");
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::mutex> lk(c->q->mu);
     stats[0] = c->n_batches;
     stats[1] = c->n_chunks;
     stats[2] = c->max_seen;
@@ -762,17 +682,11 @@ int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, i
         info[0] = -errno;
         return pyas::set_error(PYAS_EIO, "open failed: %s", strerror(errno));
     }
-    std::unique_lock<std::mutex> lk(c->mu);
-    const int64_t off = ring_reserve(c, lk, r.span);
-    if (off < 0) {
-        lk.unlock();
+    if (!c->q->reserve(&r)) {
         close(fd);
         return pyas::set_error(PYAS_EDEVICE, "coalescer stopped");
     }
-    r.ring_off = off;
-    r.state = RESERVED;
-    c->fifo.push_back(&r);
-    lk.unlock();
+    const int64_t off = r.ring_off;
 
     const int64_t t_read = now_ns();
     int64_t got = 0;
@@ -799,15 +713,13 @@ int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, i
     }
 
     const int64_t t_wait = now_ns();
-    lk.lock();
-    r.state = (got == size && !read_errno && ce == hipSuccess) ? FILLED : SKIP;
-    if (r.state == SKIP) r.rc = ce == hipSuccess ? PYAS_EIO : PYAS_EDEVICE;
+    const bool ok = got == size && !read_errno && ce == hipSuccess;
+    if (!ok) r.rc = ce == hipSuccess ? PYAS_EIO : PYAS_EDEVICE;
     if (ce != hipSuccess) r.err = hipGetErrorString(ce);
-    c->cv_disp.notify_one();
-    r.cv.wait(lk, [&] { return r.state == DONE; });
-    c->read_ns += t_wait - t_read;
-    c->wait_ns += now_ns() - t_wait;
-    lk.unlock();
+    c->q->finish(&r, ok, [&] {
+        c->read_ns += t_wait - t_read;
+        c->wait_ns += now_ns() - t_wait;
+    });
     if (r.rc != PYAS_OK) {
         if (r.err.empty()) r.err = read_errno ? strerror(read_errno) : "short read";
         return pyas::set_error(r.rc, "%s", r.err.c_str());

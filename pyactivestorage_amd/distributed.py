@@ -68,9 +68,35 @@ def exchange_partials(torch, local_total, group=None):
     (world * 32,) uint8 tensor in rank order."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    out = torch.empty(world * _lib.PARTIAL_NBYTES, dtype=torch.uint8, device=local_total.device)
-    dist.all_gather_into_tensor(out, local_total.reshape(-1), group=group)
-    return out
+    src = local_total.reshape(-1)
+    staged = dist.get_backend(group) == "gloo" and src.device.type != "cpu"
+    if staged:   # gloo moves host memory: stage the 32 bytes through it
+        src = src.cpu()
+    out = torch.empty(world * _lib.PARTIAL_NBYTES, dtype=torch.uint8, device=src.device)
+    dist.all_gather_into_tensor(out, src, group=group)
+    return out.to(local_total.device) if staged else out
+
+
+def all_gather_bytes(torch, data: bytes, device, group=None) -> list:
+    """All-gather one variable-length byte string per rank as tensors (two
+    collectives: the lengths, then the payloads padded to the longest);
+    returns the ranks' strings in rank order.  ``device``: where the
+    tensors live (the GPU for RCCL, the host for gloo)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([len(data)], dtype=torch.int64, device=device)
+    lens = torch.empty(world, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(lens, n, group=group)
+    lens = [int(x) for x in lens.cpu()]
+    m = max(max(lens), 1)
+    buf = torch.zeros(m, dtype=torch.uint8)
+    if data:
+        buf[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    buf = buf.to(device)
+    out = torch.empty(world * m, dtype=torch.uint8, device=device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    host = out.cpu().numpy()
+    return [host[r * m: r * m + lens[r]].tobytes() for r in range(world)]
 
 
 def device_combine(ctx, dtype, gathered, out, stream):

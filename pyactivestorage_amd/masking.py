@@ -23,6 +23,7 @@ NEP-50 weak Python scalars, integer/float cross-kind promotion).
 from __future__ import annotations
 
 import math
+import threading
 
 import numpy as np
 
@@ -224,6 +225,7 @@ class CompiledMask:
 
 
 _cache: dict = {}
+_cache_lock = threading.Lock()
 _CACHE_CAP = 512   # compiled masks kept; keys can come from clients (reductionist_server)
 
 
@@ -295,9 +297,10 @@ def compile_missing(missing, dt) -> CompiledMask:
         nxt = space.value(space.lo + 1)
         cm.lt = nxt if cm.lt is None or cm.lt < nxt else cm.lt
         cm.flags |= _lib.MASK_LT
-    if len(_cache) >= _CACHE_CAP:
-        _cache.pop(next(iter(_cache)))   # oldest first (dicts keep insertion order)
-    _cache[key] = cm
+    with _cache_lock:   # callers: the 30-thread drop-in pool, Reductionist request threads
+        while len(_cache) >= _CACHE_CAP:
+            _cache.pop(next(iter(_cache)))   # oldest first (dicts keep insertion order)
+        _cache[key] = cm
     return cm
 
 
