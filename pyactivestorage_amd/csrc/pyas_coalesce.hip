@@ -38,6 +38,8 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <zlib.h>
+
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -61,6 +63,29 @@ int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(
                std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// zlib.decompress of one stream (RFC 1950) into exactly `cap` bytes of dst
+// (storage.py:119-120 through numcodecs.Zlib): a pyas_inflate_status; any
+// failure sends the call back to the per-call path, which raises zlib's own
+// error.  Bytes after the stream's end are ignored, as zlib.decompress does.
+int host_inflate(const uint8_t *src, int64_t n_src, uint8_t *dst, int64_t cap, int64_t &n_out) {
+    z_stream zs;
+    std::memset(&zs, 0, sizeof(zs));
+    n_out = 0;
+    if (inflateInit(&zs) != Z_OK) return PYAS_INFLATE_BAD_HEADER;
+    zs.next_in = const_cast<Bytef *>(src);
+    zs.avail_in = (uInt)n_src;
+    zs.next_out = dst;
+    zs.avail_out = (uInt)cap;
+    const int r = inflate(&zs, Z_FINISH);
+    n_out = (int64_t)zs.total_out;
+    int st = PYAS_INFLATE_OK;
+    if (r == Z_NEED_DICT) st = PYAS_INFLATE_NEED_DICT;
+    else if (r == Z_DATA_ERROR) st = PYAS_INFLATE_BAD_CODE;
+    else if (r != Z_STREAM_END) st = zs.avail_out == 0 ? PYAS_INFLATE_OVERFLOW : PYAS_INFLATE_TRUNCATED;
+    inflateEnd(&zs);
+    return st;
 }
 
 int es_of(int dtype) {
@@ -184,6 +209,14 @@ struct pyas_coalescer {
     // batches in flight are smaller, and each zlib batch is bounded by one
     // stream's inflate latency), so one batch runs while the next gathers.
     int32_t depth = 1;
+    // Where a zlib chunk is inflated (PYAS_COALESCE_INFLATE=host|device).
+    // The device inflates one stream per wave at ~55 MB/s, so a batch of the
+    // pool's <= 30 streams takes ~20 ms; a caller thread inflates its own
+    // stream with zlib at several hundred MB/s, and the 30 callers do so in
+    // parallel.  The device wins only with thousands of streams in flight
+    // (Active's batched path, pyas_inflate), which the per-chunk pattern never
+    // has: the callers inflate, the device reduces.
+    bool host_inflate = true;
     std::vector<Slot *> slots;
     // Measured on the box (tools/bench_dropin.py): with 30 reader threads on a
     // 16-CPU host share, the dispatcher copying the batch's prefix and
@@ -559,6 +592,7 @@ int pyas_coalescer_create(pyas_ctx *ctx, int64_t ring_bytes, int32_t max_batch, 
     if (const char *v = getenv("PYAS_COALESCE_SYNC")) c->blocking_sync = std::strcmp(v, "spin") != 0;
     if (const char *v = getenv("PYAS_COALESCE_DEPTH")) c->depth = atoi(v) > 0 ? atoi(v) : 1;
     if (const char *v = getenv("PYAS_COALESCE_ZEROCOPY")) c->zero_copy = std::strcmp(v, "0") != 0;
+    if (const char *v = getenv("PYAS_COALESCE_INFLATE")) c->host_inflate = std::strcmp(v, "device") != 0;
     if (const char *v = getenv("PYAS_COALESCE_COPYSTREAM")) c->copy_stream = std::strcmp(v, "0") != 0;
     for (int i = 0; e == hipSuccess && i < c->depth; ++i) {
         Slot *sl = new Slot();
@@ -674,7 +708,14 @@ int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, i
     r.out = out;
     r.info = info;
     r.nbytes = size;
-    r.span = align_up(size > 0 ? size : 1, kAlign);
+    // a zlib chunk inflated by this thread lands decoded in the ring and joins
+    // the uncompressed requests of its layout
+    const bool inflate_here = desc->zlib && c->host_inflate;
+    if (inflate_here) {
+        r.key.desc.zlib = 0;
+        r.nbytes = r.chunk_bytes;
+    }
+    r.span = align_up(r.nbytes > 0 ? r.nbytes : 1, kAlign);
     if (r.span > c->ring_bytes) return pyas::set_error(PYAS_ENOTSUP, "chunk larger than the coalescing ring");
 
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
@@ -691,8 +732,11 @@ int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, i
     const int64_t t_read = now_ns();
     int64_t got = 0;
     int read_errno = 0;
+    thread_local std::vector<uint8_t> zbuf;   // this caller's compressed bytes
+    if (inflate_here && (int64_t)zbuf.size() < size) zbuf.resize((size_t)size);
+    uint8_t *const dst = inflate_here ? zbuf.data() : c->hring + off;
     while (got < size) {
-        const ssize_t k = pread(fd, c->hring + off + got, (size_t)(size - got), (off_t)(offset + got));
+        const ssize_t k = pread(fd, dst + got, (size_t)(size - got), (off_t)(offset + got));
         if (k < 0) {
             if (errno == EINTR) continue;
             read_errno = errno;
@@ -703,17 +747,26 @@ int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, i
     }
     close(fd);
     info[0] = got;
+    bool inflated = true;
+    if (inflate_here && got == size && !read_errno) {
+        int64_t n_dec = 0;
+        const int zst = host_inflate(zbuf.data(), size, c->hring + off, r.chunk_bytes, n_dec);
+        info[1] = zst;
+        info[2] = n_dec;
+        inflated = zst == PYAS_INFLATE_OK && n_dec == r.chunk_bytes;
+        if (!inflated) r.err = "inflate failed or size mismatch";
+    }
     hipError_t ce = hipSuccess;
-    if (c->caller_copy && got == size && !read_errno && size > 0) {
+    if (c->caller_copy && got == size && !read_errno && inflated && r.nbytes > 0) {
         // this chunk's H2D copy, issued by the caller so that copies overlap
         // other callers' reads; ordered before the batch's launches by its ev_copy
         ce = hipSetDevice(c->device);
         if (ce == hipSuccess)
-            ce = hipMemcpyAsync(c->dring + off, c->hring + off, (size_t)size, hipMemcpyHostToDevice, c->cst);
+            ce = hipMemcpyAsync(c->dring + off, c->hring + off, (size_t)r.nbytes, hipMemcpyHostToDevice, c->cst);
     }
 
     const int64_t t_wait = now_ns();
-    const bool ok = got == size && !read_errno && ce == hipSuccess;
+    const bool ok = got == size && !read_errno && inflated && ce == hipSuccess;
     if (!ok) r.rc = ce == hipSuccess ? PYAS_EIO : PYAS_EDEVICE;
     if (ce != hipSuccess) r.err = hipGetErrorString(ce);
     c->q->finish(&r, ok, [&] {
