@@ -71,6 +71,7 @@ struct pyas_ctx {
     int32_t inflate_wbits = 13;   // LDS history ring of pyas_inflate: 2^13 B per stream
     bool chained = true;          // k_finish folds the total itself (arrival counter)
     int64_t fold_min_blocks = 2048;   // pyas_reduce_axes_grid: fewest workgroups worth folding
+    int64_t col_stream_blocks = 2048; // pyas_reduce_axes: workgroups k_axes_col_stream aims for
     pyas::TieRule tie[2];             // NumPy's zero-sign rule for f32, f64 (lanes 0: unset)
     pyas::Ingest *ingest = nullptr;   // pinned staging ring of pyas_read_ranges (lazy)
     std::mutex mu;
@@ -913,8 +914,26 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *ma
     dense_geometry(x.d, batch, axes_mask, es, shuf ? es : 1, x.r.tab.on[0] || x.r.tab.on[1]);
     // Fully selected chunks go to k_axes_dense, the rest to k_reduce_axes
     // (each kernel skips the other's chunks); sel == NULL means all full.
+    // Streamed column layout (k_axes_col_stream): every chunk whole, one lane
+    // per item (split 1), rows in whole 4-row groups; each workgroup walks
+    // cpb chunks as one ring of loads.  PYAS_COL_STREAM: 0 off, N > 0 chunks
+    // per workgroup, unset auto (about col_stream_blocks workgroups).
+    if (x.d.mode == 1 && !batch->sel && es >= 4 && x.d.split == 1 && x.d.it == pyas::kBlock &&
+        (x.d.RO * x.d.RI) % 4 == 0) {
+        const char *e = getenv("PYAS_COL_STREAM");   // per call: tests and benches switch it
+        const int64_t forced = e ? atoll(e) : -1;
+        const int64_t units = batch->n_chunks * x.d.bpc;
+        int64_t cpb = forced >= 0 ? forced : units / ctx->col_stream_blocks;
+        if (cpb > batch->n_chunks) cpb = batch->n_chunks;
+        if (cpb >= 2 || forced > 0) {
+            const int64_t items = x.d.KO * (x.d.KI / (16 / es)), per_block = pyas::kBlock * PYAS_STREAM_NV;
+            x.d.cpb = cpb;
+            x.d.n_chunks = batch->n_chunks;
+            x.d.bpc = (items + per_block - 1) / per_block;
+        }
+    }
     if (x.d.mode) {
-        const int64_t g = batch->n_chunks * x.d.bpc;
+        const int64_t g = (x.d.cpb > 0 ? (batch->n_chunks + x.d.cpb - 1) / x.d.cpb : batch->n_chunks) * x.d.bpc;
         if (g >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
         PYAS_HIP(pyas::launch_axes_dense(batch->dtype, x, masked, g, (hipStream_t)stream));
     }

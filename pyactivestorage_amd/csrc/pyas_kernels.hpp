@@ -1355,6 +1355,9 @@ __device__ __forceinline__ void store_group(const TileAcc<T> &a, uint32_t cnt, u
 #ifndef PYAS_LDS_WAVES
 #define PYAS_LDS_WAVES 0
 #endif
+#ifndef PYAS_STREAM_WAVES
+#define PYAS_STREAM_WAVES 0
+#endif
 #ifndef PYAS_FOLD_COL_WAVES
 #define PYAS_FOLD_COL_WAVES 0
 #endif
@@ -2018,13 +2021,85 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes
 #define PYAS_LEAN_WAVES 4   // occupancy floor: <= 128 VGPRs, 16 waves per CU
 #endif
 
-// One lane's row walk of k_axes_fold_lean over every layer of its column:
-// groups of 4 rows (the two-step path's PYAS_COL_U grouping, so the sums are
-// bit-identical), DEPTH groups of 16-B loads in flight while the oldest is
-// consumed.  The fetch cursor runs ahead of the consume cursor across layer
-// boundaries; a layer's partial is merged into w[] when its last group is
-// consumed (tile_store_lane + merge, as k_combine_grid would).  The walk
-// covers layers [l0, l0 + n_layers); with `sink` set, each layer's rounded
+// One lane's row walk over a run of layers (chunks) that share one column
+// geometry: groups of 4 rows (the two-step path's PYAS_COL_U grouping, so
+// the sums are bit-identical), DEPTH groups of 16-B loads in flight while
+// the oldest is consumed.  The fetch cursor runs ahead of the consume cursor
+// across layer boundaries, so a layer's first loads are in flight while the
+// previous layer's last group is summed.  The walk covers layers
+// [l0, l0 + n_layers) at layer_base(l) + off0; when a layer's last group has
+// been consumed, layer_end(cl, acc) runs (cl = layers done before it) with
+// the layer's sum / min / max in acc[] (counts: masked mode counts per
+// element; unmasked, the walk adds the layer's R rows first).
+// NV > 1: the lane walks NV items at once (row-0 byte offsets offs[s],
+// partials in acc[s * N ...]), so a wave's loads of one row cover NV KiB
+// when its items are adjacent.
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, bool NT, int NV, typename LB,
+          typename LE>
+__device__ __forceinline__ void col_walk_layers(const AxesDense &d, int64_t n, const int64_t *offs, int64_t l0,
+                                                int64_t n_layers, const MaskT<T> &mk, const LB &layer_base,
+                                                TileAcc<T> *acc, const LE &layer_end) {
+    constexpr int N = 16 / sizeof(T), ES = sizeof(T), U = 4;
+    const int64_t R = d.RO * d.RI;                      // rows per layer, a multiple of U
+    const int64_t step = d.KI * ES;                     // next ri
+    const int64_t wrap = (d.KO * d.RI * d.KI - d.RI * d.KI) * ES;   // ri wrapped: next ro
+    const int64_t gpl = R / U, total = n_layers * gpl;  // groups per layer, in all
+    // fetch cursor
+    const uint8_t *fb = layer_base(l0);
+    int64_t foff = 0, fl = 0;   // row offset from the items' row 0
+    int64_t fri = 0, fg = 0;
+    auto fetch = [&](uint4 *buf) {   // buf[v * U + u]: item set v, row u of the group
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) buf[v * U + u] = ldv<T, SHUF, AL, NT>(fb, fb + offs[v] + foff, n);
+            foff += step;
+            if (++fri == d.RI) { fri = 0; foff += wrap; }
+        }
+        if (++fg == gpl) {   // next layer (wave-uniform)
+            fg = 0;
+            if (++fl < n_layers) {
+                fb = layer_base(l0 + fl);
+                foff = 0;
+                fri = 0;
+            }
+        }
+    };
+    int64_t cg = 0, cl = 0;   // consumed groups of the current layer, consumed layers
+    auto consume = [&](const uint4 *buf) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) col_consume<T, BSWAP, MASKED, U>(buf + v * U, acc + v * N, mk);
+        if (++cg == gpl) {
+            cg = 0;
+            if constexpr (!MASKED) {
+#pragma unroll
+                for (int k = 0; k < NV * N; ++k) acc[k].count += (uint32_t)R;
+            }
+            layer_end(cl, acc);
+            ++cl;
+        }
+    };
+    uint4 buf[DEPTH][NV * U];
+#pragma unroll
+    for (int s = 0; s < DEPTH; ++s)
+        if (s < total) fetch(buf[s]);
+    for (int64_t t = 0; t < total; t += DEPTH) {   // wave-uniform
+#pragma unroll
+        for (int s = 0; s < DEPTH; ++s) {
+            if (t + s < total) {
+                uint4 cur[NV * U];
+#pragma unroll
+                for (int u = 0; u < NV * U; ++u) cur[u] = buf[s][u];
+                if (t + s + DEPTH < total) fetch(buf[s]);
+                consume(cur);
+            }
+        }
+    }
+}
+
+// k_axes_fold_lean's walk over every layer of its column: each layer's
+// partial is merged into w[] when its last group is consumed (tile_store_lane
+// + merge, as k_combine_grid would).  With `sink` set, each layer's rounded
 // sum is stored at sink[(layer - l0) * sstride + k * IB] instead of being
 // added to w[k].sum (the second half of a split column, added in order by
 // the first half's lane).
@@ -2033,31 +2108,7 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
                                           int64_t n_layers, bool round, const MaskT<T> &mk,
                                           const LB &layer_base, WAcc<T> *w,
                                           typename TT<T>::Acc *sink, int sstride, int IB) {
-    constexpr int N = 16 / sizeof(T), ES = sizeof(T), U = 4;
-    const int64_t R = d.RO * d.RI;                      // rows per layer, a multiple of U
-    const int64_t step = d.KI * ES;                     // next ri
-    const int64_t wrap = (d.KO * d.RI * d.KI - d.RI * d.KI) * ES;   // ri wrapped: next ro
-    const int64_t gpl = R / U, total = n_layers * gpl;  // groups per layer, in all
-    // fetch cursor
-    const uint8_t *fb = layer_base(l0);
-    int64_t foff = off0, fl = 0;
-    int64_t fri = 0, fg = 0;
-    auto fetch = [&](uint4 *buf) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            buf[u] = ldv<T, SHUF, AL, NT>(fb, fb + foff, n);
-            foff += step;
-            if (++fri == d.RI) { fri = 0; foff += wrap; }
-        }
-        if (++fg == gpl) {   // next layer (wave-uniform)
-            fg = 0;
-            if (++fl < n_layers) {
-                fb = layer_base(l0 + fl);
-                foff = off0;
-                fri = 0;
-            }
-        }
-    };
+    constexpr int N = 16 / sizeof(T);
     // acc[k]: the current layer's sum / min / max; its count and NaN flag run
     // over every layer (merge adds counts, and a NaN layer min/max stays NaN
     // through pmin/pmax).  A layer's sum is rounded and added to w[k].sum and
@@ -2068,43 +2119,22 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
     TileAcc<T> acc[N];
 #pragma unroll
     for (int k = 0; k < N; ++k) acc[k].init();
-    int64_t cg = 0, cl = 0;   // consumed groups of the current layer, consumed layers
-    auto consume = [&](const uint4 *buf) {
-        col_consume<T, BSWAP, MASKED, U>(buf, acc, mk);
-        if (++cg == gpl) {
-            cg = 0;
+    auto merge_layer = [&](int64_t cl, TileAcc<T> *ac) {
 #pragma unroll
-            for (int k = 0; k < N; ++k) {
-                if constexpr (!MASKED) acc[k].count += (uint32_t)R;
-                pyas_scalar s;
-                TT<T>::put_acc(s, acc[k].sum);
-                if constexpr (SINK) sink[cl * sstride + k * IB] = sum_of<T>(s, round);
-                else w[k].sum += sum_of<T>(s, round);
-                w[k].mn = pmin(w[k].mn, acc[k].mn);
-                w[k].mx = pmax(w[k].mx, acc[k].mx);
-                acc[k].sum = 0;
-                acc[k].mn = TT<T>::highest();
-                acc[k].mx = TT<T>::lowest();
-            }
-            ++cl;
+        for (int k = 0; k < N; ++k) {
+            pyas_scalar s;
+            TT<T>::put_acc(s, ac[k].sum);
+            if constexpr (SINK) sink[cl * sstride + k * IB] = sum_of<T>(s, round);
+            else w[k].sum += sum_of<T>(s, round);
+            w[k].mn = pmin(w[k].mn, ac[k].mn);
+            w[k].mx = pmax(w[k].mx, ac[k].mx);
+            ac[k].sum = 0;
+            ac[k].mn = TT<T>::highest();
+            ac[k].mx = TT<T>::lowest();
         }
     };
-    uint4 buf[DEPTH][U];
-#pragma unroll
-    for (int s = 0; s < DEPTH; ++s)
-        if (s < total) fetch(buf[s]);
-    for (int64_t t = 0; t < total; t += DEPTH) {   // wave-uniform
-#pragma unroll
-        for (int s = 0; s < DEPTH; ++s) {
-            if (t + s < total) {
-                uint4 cur[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) cur[u] = buf[s][u];
-                if (t + s + DEPTH < total) fetch(buf[s]);
-                consume(cur);
-            }
-        }
-    }
+    col_walk_layers<T, SHUF, BSWAP, MASKED, AL, DEPTH, NT, 1>(d, n, &off0, l0, n_layers, mk, layer_base, acc,
+                                                             merge_layer);
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         w[k].count = (int64_t)acc[k].count;   // host: n_layers * rows < 2^31
@@ -2254,6 +2284,98 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
         }
         store_wpartial(a.out + f, w[k]);
     }
+}
+
+#ifndef PYAS_STREAM_DEPTH
+#define PYAS_STREAM_DEPTH 2   // 4-row load groups in flight per lane (k_axes_col_stream)
+#endif
+// PYAS_STREAM_NV (pyas_internal.hpp): items per lane of k_axes_col_stream
+
+// Per-chunk column layout streamed over several chunks (pyas_reduce_axes
+// with every chunk whole, dense_geometry's split 1, rows per chunk a
+// multiple of 4).  Block (g, j) owns items j * kBlock + t of chunks
+// g * cpb ... g * cpb + cpb - 1 and walks them as ONE ring of loads
+// (col_walk_layers: a chunk's first rows are in flight while the previous
+// chunk's last group is summed), instead of one short walk per chunk with a
+// fill and a drain each (dense_col: 64 KiB per wave on C3).  When a chunk's
+// last group is in, each wave stages its lanes' partials in its own 8-KiB
+// LDS area and writes them as consecutive 16-B stores (no block barrier).
+// Same 4-row groups, order and count as col_rows_ring: bit-identical to
+// dense_col.  A block whose chunks are not all 16-B aligned runs dense_col
+// per chunk instead (block-uniform).
+template <typename T, bool SHUF, bool BSWAP, int MASKED>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_col_stream(AxesArgs a) {
+    constexpr int N = 16 / sizeof(T);
+    const AxesDense &d = a.d;
+    const ReduceArgs &r = a.r;
+    const int64_t g = blockIdx.x / d.bpc;
+    const int64_t j = blockIdx.x - g * d.bpc;
+    const int64_t c0 = g * d.cpb;
+    const int64_t nc = d.n_chunks - c0 < d.cpb ? d.n_chunks - c0 : d.cpb;
+    auto layer_base = [&](int64_t l) { return r.data + r.offsets[c0 + l]; };
+    MaskT<T> mk;
+    mk.init(r.mask);
+    __shared__ uint4 stage[kBlock * 2 * N > col_units_lds<T>() ? kBlock * 2 * N : col_units_lds<T>()];
+    bool al = true;   // block-uniform
+    for (int64_t l = 0; al && l < nc; ++l) al = ldv_aligned<T, SHUF>(layer_base(l), r.chunk_elems);
+    if (!al) {
+        for (int64_t l = 0; l < nc; ++l)
+            dense_col<T, SHUF, BSWAP, MASKED, false>(a, c0 + l, j, layer_base(l), mk, stage);
+        return;
+    }
+    // wave w of block j owns items j * kBlock * NV + w * kWave * NV + v * kWave + lane, v < NV
+    constexpr int NV = PYAS_STREAM_NV;
+    const int64_t items = d.KO * (d.KI / N);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t iw = j * kBlock * NV + (threadIdx.x / kWave) * (kWave * NV);   // the wave's first item
+    if (iw + lane >= items) return;                   // no block barrier below
+    const int nv = (int)(items - iw < kWave ? items - iw : kWave);   // active lanes (a prefix)
+    uint4 *ws = stage + (threadIdx.x / kWave) * (kWave * 2 * N);
+    const int64_t KIV = d.KI / N;
+    int64_t offs[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {   // row 0 of each item; a missing item re-reads item set 0's
+        const int64_t it = iw + v * kWave + lane < items ? iw + v * kWave + lane : iw + lane;
+        const int64_t ko = it / KIV, vv = it - ko * KIV;
+        offs[v] = (ko * d.RI * d.KI + vv * N) * sizeof(T);
+    }
+    auto chunk_end = [&](int64_t cl, TileAcc<T> *acc) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        pyas_partial *cout = a.out + a.out_offsets[c0 + cl];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int64_t iv = iw + v * kWave;
+            const int64_t nvv = items - iv < kWave ? items - iv : kWave;   // items of set v (may be <= 0)
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                pyas_partial pp;
+                tile_store_lane(acc[v * N + k], &pp);
+                uint4 h[2];
+                __builtin_memcpy(h, &pp, 32);
+                ws[(lane * N + k) * 2] = h[0];
+                ws[(lane * N + k) * 2 + 1] = h[1];
+                acc[v * N + k].init();
+            }
+            wave_sync_lds();
+            u32x4 *dst = reinterpret_cast<u32x4 *>(cout + iv * N);
+            for (int64_t q = lane; q < nvv * 2 * N; q += nv) {
+                const uint4 h = ws[q];
+                u32x4 x = {h.x, h.y, h.z, h.w};
+                __builtin_nontemporal_store(x, dst + q);
+            }
+            wave_sync_lds();   // the area is rewritten next
+        }
+    };
+    TileAcc<T> acc[NV * N];
+#pragma unroll
+    for (int k = 0; k < NV * N; ++k) acc[k].init();
+    // shuffled rows under 128 elements: plain plane loads (k_axes_fold_lean's rule)
+    if (SHUF && d.KI < 128)
+        col_walk_layers<T, SHUF, BSWAP, MASKED, true, PYAS_STREAM_DEPTH, false, NV>(
+            d, r.chunk_elems, offs, 0, nc, mk, layer_base, acc, chunk_end);
+    else
+        col_walk_layers<T, SHUF, BSWAP, MASKED, true, PYAS_STREAM_DEPTH, true, NV>(
+            d, r.chunk_elems, offs, 0, nc, mk, layer_base, acc, chunk_end);
 }
 
 // Whole-chunk box query, LDS row layout (modes 4/5/6), chunk layers folded
@@ -3062,9 +3184,33 @@ static void launch_dense_m(const AxesArgs &a, bool masked, dim3 g, hipStream_t s
     launch_dense_ms<T, false, MODE>(a, masked, g, st);
 }
 
+template <typename T, bool SHUF>
+static void launch_col_stream(const AxesArgs &a, bool masked, dim3 gr, hipStream_t st) {
+    const dim3 blk(kBlock);
+    const int mm = mask_mode(a.r.mask, masked);
+    if (a.bswap) {
+        if (mm) hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, true, kMaskAll>), gr, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, true, 0>), gr, blk, 0, st, a);
+    } else if (mm == kMaskRange) {
+        hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, kMaskRange>), gr, blk, 0, st, a);
+    } else if (mm == kMaskNoEq1) {
+        hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, kMaskNoEq1>), gr, blk, 0, st, a);
+    } else {
+        if (mm) hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, kMaskAll>), gr, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, 0>), gr, blk, 0, st, a);
+    }
+}
+
 template <typename T>
 hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st) {
     const dim3 g((unsigned)grid);
+    if constexpr (sizeof(T) >= 4) {
+        if (a.d.mode == 1 && a.d.cpb > 0) {   // k_axes_col_stream (host: split 1, whole chunks)
+            if (a.shuf) launch_col_stream<T, true>(a, masked, g, st);
+            else launch_col_stream<T, false>(a, masked, g, st);
+            return hipGetLastError();
+        }
+    }
     if (a.d.mode == 1) launch_dense_m<T, 1>(a, masked, g, st);
     else if (a.d.mode == 2) launch_dense_m<T, 2>(a, masked, g, st);
     else if (a.d.mode == 4) launch_dense_m<T, 4>(a, masked, g, st);
