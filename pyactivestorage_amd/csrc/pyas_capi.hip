@@ -71,7 +71,6 @@ struct pyas_ctx {
     int32_t inflate_wbits = 13;   // LDS history ring of pyas_inflate: 2^13 B per stream
     bool chained = true;          // k_finish folds the total itself (arrival counter)
     int64_t fold_min_blocks = 2048;   // pyas_reduce_axes_grid: fewest workgroups worth folding
-    int64_t col_stream_blocks = 2048; // pyas_reduce_axes: workgroups k_axes_col_stream aims for
     pyas::TieRule tie[2];             // NumPy's zero-sign rule for f32, f64 (lanes 0: unset)
     pyas::Ingest *ingest = nullptr;   // pinned staging ring of pyas_read_ranges (lazy)
     std::mutex mu;
@@ -914,22 +913,39 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *ma
     dense_geometry(x.d, batch, axes_mask, es, shuf ? es : 1, x.r.tab.on[0] || x.r.tab.on[1]);
     // Fully selected chunks go to k_axes_dense, the rest to k_reduce_axes
     // (each kernel skips the other's chunks); sel == NULL means all full.
-    // Streamed column layout (k_axes_col_stream): every chunk whole, one lane
-    // per item (split 1), rows in whole 4-row groups; each workgroup walks
-    // cpb chunks as one ring of loads.  PYAS_COL_STREAM: 0 off, N > 0 chunks
-    // per workgroup, unset auto (about col_stream_blocks workgroups).
+    // Streamed column layout (k_axes_col_stream): every chunk whole, one
+    // lane per item column (split 1), rows in whole 4-row groups; each
+    // workgroup walks cpb chunks as one ring of loads.  Measured on C3
+    // (tools/bench_axes.py, profiles/r03/axes_stream_sweep.txt), per
+    // geometry:
+    //  - plain, kept inner run >= 4 KiB (axis (0,)): 4 items per lane, about
+    //    1024 workgroups (0.884 -> 0.795 ms);
+    //  - plain otherwise (axis (1,)): 2 items per lane, about 256 workgroups
+    //    (0.90 -> 0.805 ms);
+    //  - shuffled, kept inner run under 128 elements (axis (1,)): 1 item per
+    //    lane, about 512 workgroups (0.975 -> 0.927 ms); other shuffled
+    //    geometries measured slower streamed ((0,): 0.846 -> 0.88-1.0 ms) and
+    //    keep dense_col.
+    // PYAS_COL_STREAM: 0 off, N > 0 forces N chunks per workgroup wherever
+    // the kernel can run (tests), unset auto.
+    const int64_t col_items = x.d.mode == 1 ? x.d.KO * (x.d.KI / (16 / es)) : 0;
     if (x.d.mode == 1 && !batch->sel && es >= 4 && x.d.split == 1 && x.d.it == pyas::kBlock &&
         (x.d.RO * x.d.RI) % 4 == 0) {
         const char *e = getenv("PYAS_COL_STREAM");   // per call: tests and benches switch it
         const int64_t forced = e ? atoll(e) : -1;
-        const int64_t units = batch->n_chunks * x.d.bpc;
-        int64_t cpb = forced >= 0 ? forced : units / ctx->col_stream_blocks;
+        const int64_t kiv = x.d.KI / (16 / es);     // vectors per kept inner run
+        const int nv = shuf ? 1 : (kiv % 256 == 0 && col_items >= 4 * pyas::kBlock) ? 4 : 2;
+        const int64_t target = shuf ? 512 : nv == 4 ? 1024 : 256;   // workgroups
+        // auto: the measured geometries, with every lane's NV items present
+        const bool auto_ok = shuf ? x.d.KI < 128 : col_items >= nv * pyas::kBlock;
+        const int64_t bpc = (col_items + nv * pyas::kBlock - 1) / (nv * pyas::kBlock);
+        int64_t cpb = forced >= 0 ? forced : auto_ok ? batch->n_chunks * bpc / target : 0;
         if (cpb > batch->n_chunks) cpb = batch->n_chunks;
         if (cpb >= 2 || forced > 0) {
-            const int64_t items = x.d.KO * (x.d.KI / (16 / es)), per_block = pyas::kBlock * PYAS_STREAM_NV;
             x.d.cpb = cpb;
+            x.d.nv = nv;
             x.d.n_chunks = batch->n_chunks;
-            x.d.bpc = (items + per_block - 1) / per_block;
+            x.d.bpc = bpc;
         }
     }
     if (x.d.mode) {

@@ -47,10 +47,6 @@ constexpr int kAxesLds = 8192;   // reduced-index offsets kept in LDS (int32, 32
 
 // Dense partial-axis geometry (k_axes_dense): the chunk dims merged into
 // (RO, KO, RI, KI) = (reduced outer, kept outer, reduced inner, kept inner).
-#ifndef PYAS_STREAM_NV
-#define PYAS_STREAM_NV 1   // k_axes_col_stream: items per lane (a wave reads NV KiB of a row)
-#endif
-
 struct AxesDense {
     int32_t mode;                     // 0 off, 1 column, 2 row, 3 row with 4 outputs per lane,
                                       // 4/5/6 row through LDS with 1/2/4 lanes per output
@@ -59,6 +55,7 @@ struct AxesDense {
     int64_t RO, KO, RI, KI;
     int64_t bpc;                      // workgroups per chunk of the dense launch
     int64_t cpb;                      // column layout: chunks per workgroup of k_axes_col_stream (0: off)
+    int32_t nv;                       // k_axes_col_stream: items per lane (1, 2 or 4)
     int64_t n_chunks;                 // k_axes_col_stream: chunks in the batch
 };
 

@@ -2286,10 +2286,6 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
     }
 }
 
-#ifndef PYAS_STREAM_DEPTH
-#define PYAS_STREAM_DEPTH 2   // 4-row load groups in flight per lane (k_axes_col_stream)
-#endif
-// PYAS_STREAM_NV (pyas_internal.hpp): items per lane of k_axes_col_stream
 
 // Per-chunk column layout streamed over several chunks (pyas_reduce_axes
 // with every chunk whole, dense_geometry's split 1, rows per chunk a
@@ -2303,7 +2299,10 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
 // Same 4-row groups, order and count as col_rows_ring: bit-identical to
 // dense_col.  A block whose chunks are not all 16-B aligned runs dense_col
 // per chunk instead (block-uniform).
-template <typename T, bool SHUF, bool BSWAP, int MASKED>
+// NV items per lane, kWave apart: with adjacent items (a kept inner run of
+// >= NV KiB, C3 axis (0,)) a wave's loads of one row cover NV KiB; NV > 1
+// keeps one 4-row group in flight per item instead of two.
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int NV>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_col_stream(AxesArgs a) {
     constexpr int N = 16 / sizeof(T);
     const AxesDense &d = a.d;
@@ -2324,7 +2323,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_c
         return;
     }
     // wave w of block j owns items j * kBlock * NV + w * kWave * NV + v * kWave + lane, v < NV
-    constexpr int NV = PYAS_STREAM_NV;
+    constexpr int DEPTH = NV == 1 ? 2 : 1;
     const int64_t items = d.KO * (d.KI / N);
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t iw = j * kBlock * NV + (threadIdx.x / kWave) * (kWave * NV);   // the wave's first item
@@ -2371,10 +2370,10 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_c
     for (int k = 0; k < NV * N; ++k) acc[k].init();
     // shuffled rows under 128 elements: plain plane loads (k_axes_fold_lean's rule)
     if (SHUF && d.KI < 128)
-        col_walk_layers<T, SHUF, BSWAP, MASKED, true, PYAS_STREAM_DEPTH, false, NV>(
+        col_walk_layers<T, SHUF, BSWAP, MASKED, true, DEPTH, false, NV>(
             d, r.chunk_elems, offs, 0, nc, mk, layer_base, acc, chunk_end);
     else
-        col_walk_layers<T, SHUF, BSWAP, MASKED, true, PYAS_STREAM_DEPTH, true, NV>(
+        col_walk_layers<T, SHUF, BSWAP, MASKED, true, DEPTH, true, NV>(
             d, r.chunk_elems, offs, 0, nc, mk, layer_base, acc, chunk_end);
 }
 
@@ -3184,20 +3183,20 @@ static void launch_dense_m(const AxesArgs &a, bool masked, dim3 g, hipStream_t s
     launch_dense_ms<T, false, MODE>(a, masked, g, st);
 }
 
-template <typename T, bool SHUF>
+template <typename T, bool SHUF, int NV>
 static void launch_col_stream(const AxesArgs &a, bool masked, dim3 gr, hipStream_t st) {
     const dim3 blk(kBlock);
     const int mm = mask_mode(a.r.mask, masked);
     if (a.bswap) {
-        if (mm) hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, true, kMaskAll>), gr, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, true, 0>), gr, blk, 0, st, a);
+        if (mm) hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, true, kMaskAll, NV>), gr, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, true, 0, NV>), gr, blk, 0, st, a);
     } else if (mm == kMaskRange) {
-        hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, kMaskRange>), gr, blk, 0, st, a);
+        hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, kMaskRange, NV>), gr, blk, 0, st, a);
     } else if (mm == kMaskNoEq1) {
-        hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, kMaskNoEq1>), gr, blk, 0, st, a);
+        hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, kMaskNoEq1, NV>), gr, blk, 0, st, a);
     } else {
-        if (mm) hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, kMaskAll>), gr, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, 0>), gr, blk, 0, st, a);
+        if (mm) hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, kMaskAll, NV>), gr, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_col_stream<T, SHUF, false, 0, NV>), gr, blk, 0, st, a);
     }
 }
 
@@ -3206,8 +3205,11 @@ hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hip
     const dim3 g((unsigned)grid);
     if constexpr (sizeof(T) >= 4) {
         if (a.d.mode == 1 && a.d.cpb > 0) {   // k_axes_col_stream (host: split 1, whole chunks)
-            if (a.shuf) launch_col_stream<T, true>(a, masked, g, st);
-            else launch_col_stream<T, false>(a, masked, g, st);
+            // host: shuffled chunks stream with one item per lane, plain
+            // ones with 2 or 4
+            if (a.shuf) launch_col_stream<T, true, 1>(a, masked, g, st);
+            else if (a.d.nv == 4) launch_col_stream<T, false, 4>(a, masked, g, st);
+            else launch_col_stream<T, false, 2>(a, masked, g, st);
             return hipGetLastError();
         }
     }

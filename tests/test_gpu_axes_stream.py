@@ -22,8 +22,12 @@ from tests._compare import shuffle_bytes
 pytestmark = pytest.mark.gpu
 
 # (shape, axes): shapes whose column layout has >= 256 items per chunk
-# (one lane per item, split 1) and rows in whole 4-row groups
-GEOMS = [((8, 32, 64), (0,)), ((16, 8, 128), (1,)), ((4, 4, 1024), (0, 1)), ((12, 16, 64), (0,))]
+# (one lane per item column, split 1) and rows in whole 4-row groups.
+# Plain f4 chunks of (8, 64, 64) / (4, 5, 1024) over (0,) take 4 items per
+# lane (the second with a ragged last workgroup), the others 2 (f8 ones
+# with item sets left empty); shuffled chunks take 1.
+GEOMS = [((8, 32, 64), (0,)), ((16, 8, 128), (1,)), ((4, 4, 1024), (0, 1)), ((12, 16, 64), (0,)),
+         ((8, 64, 64), (0,)), ((4, 5, 1024), (0,))]
 DTYPES = ["<f4", ">f4", "<f8", "<i4", "<u8"]
 MISSING = [None, (-999, None, -50, 140), (None, None, -1e30, None)]
 
