@@ -1779,7 +1779,30 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
         if constexpr (!MASKED) acc.count += (uint32_t)(VH * N);
         uint32_t cnt, nan;
         group_reduce(acc, H, cnt, nan);
-        if (h == 0 && o0 + r < d.KO) store_group(acc, cnt, nan, out + o0 + r);
+        // the tile's partials go out as consecutive 16-B non-temporal stores,
+        // staged in the (now read) tile area, instead of store_group's
+        // per-lane 32-B writes that half fill each store instruction's span
+        // (C3 (2,): plain unchanged at 0.85 ms, shuffled 0.85 -> 0.84 ms)
+        wave_sync_lds();
+        if (h == 0) {
+            pyas_partial pp;
+            store_group(acc, cnt, nan, &pp);
+            uint4 hv[2];
+            __builtin_memcpy(hv, &pp, 32);
+            t[r * 2] = hv[0];
+            t[r * 2 + 1] = hv[1];
+        }
+        wave_sync_lds();
+        {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const int nq = (int)(nvec / V) * 2;   // runs in this tile x 2 uint4
+            u32x4 *dst = reinterpret_cast<u32x4 *>(out + o0);
+            for (int q = lane; q < nq; q += kWave) {
+                const uint4 hv = t[q];
+                u32x4 x = {hv.x, hv.y, hv.z, hv.w};
+                __builtin_nontemporal_store(x, dst + q);
+            }
+        }
         wave_sync_lds();
     }
 }

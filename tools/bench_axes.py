@@ -3,7 +3,8 @@
 Reports GB/s of pyas_reduce_axes for several axis sets (per chunk, keepdims),
 or with --fold of pyas_reduce_axes_grid (the whole-variable box query with
 the chunk layers folded in the kernel, what Active runs on resident data).
---shuffle stores the chunks HDF5-byte-shuffled."""
+--shuffle stores the chunks HDF5-byte-shuffled; --only AXES (e.g. "0" or
+"0,2") runs one axis set (for per-axis rocprofv3 passes)."""
 import json
 import os
 import sys
@@ -25,6 +26,9 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     shape, chunks = (1024, 1024, 1024), (64, 64, 64)
     shuffled = "--shuffle" in sys.argv   # chunks stored HDF5-byte-shuffled
+    axis_sets = ((0,), (1,), (2,), (0, 1), (1, 2), (0, 2))
+    if "--only" in sys.argv:
+        axis_sets = (tuple(int(x) for x in sys.argv[sys.argv.index("--only") + 1].split(",")),)
     for k, arg in enumerate(sys.argv):     # --fold-blocks N: workgroup floor of the in-kernel fold
         if arg == "--fold-blocks":
             ctx.set_fold_min_blocks(int(sys.argv[k + 1]))
@@ -54,7 +58,7 @@ def main():
         return ms[len(ms) // 2] * 1e-3, ms[0] * 1e-3
     if "--fold" in sys.argv:
         grid_n = [s // c for s, c in zip(shape, chunks)]
-        for axes in ((0,), (1,), (2,), (0, 1), (1, 2), (0, 2)):
+        for axes in axis_sets:
             g = _lib.Grid()
             g.ndim = 3
             g.axes_mask = sum(1 << a for a in axes)
@@ -76,7 +80,7 @@ def main():
         print(json.dumps({"workload": "c3 box query, chunk layers folded in-kernel (pyas_reduce_axes_grid)"
                           + (", byte-shuffled chunks" if shuffled else ""), "results": res}))
         return
-    for axes in ((0,), (1,), (2,), (0, 1), (1, 2), (0, 2)):
+    for axes in axis_sets:
         n_out = int(np.prod([1 if d in axes else chunks[d] for d in range(3)]))
         out = DeviceBuffer(ctx, len(offsets) * n_out * _lib.PARTIAL_NBYTES)
         offs = torch.from_numpy(np.arange(len(offsets), dtype=np.int64) * n_out).to(dev)
