@@ -299,6 +299,18 @@ def cpu_baseline(cfg, host_chunks: np.ndarray, n_chunks: int, missing, threads: 
     return dt_s, out
 
 
+def _cpu_model():
+    """The host CPU's model name (/proc/cpuinfo, as lscpu reports it)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def oracle_check(gpu_result, oracle, dt):
     """The GPU's full-size result against the oracle's storage.py +
     _from_storage combine over the same chunks (active.py:575-630): count,
@@ -676,7 +688,7 @@ def main():
                              f"file on a {args.cpu_threads}-thread pool (active.py:557), "
                              f"{secs:.2f} s; 'cores' = pool threads used, the host has {ncores} "
                              f"usable cores",
-                   "chunks_per_s": round(nc / secs, 1)}
+                   "chunks_per_s": round(nc / secs, 1), "cpu_model": _cpu_model()}
             del host
         if args.host_inclusive and data.numel() <= (8 << 30):
             ser, ovl = host_inclusive(torch, ctx, data, cfg, dt, missing)
