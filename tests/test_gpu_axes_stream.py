@@ -124,3 +124,19 @@ def test_stream_matches_oracle(gpu, monkeypatch, geom):
             np.testing.assert_array_equal(got[k][f][ok].astype(np.float32), w, err_msg=f"chunk {k} {f}")
         wsum = np.ma.filled(vm.astype(np.float64), 0).sum(axis=axes, keepdims=True).reshape(-1)
         np.testing.assert_allclose(got[k]["sum"][ok], wsum[ok], rtol=1e-6, atol=1e-3)
+
+
+def test_auto_choice_at_size(gpu):
+    """The configurations pyas_reduce_axes picks by itself at a C3-like size
+    against the one-chunk-per-workgroup kernel and the oracle
+    (tests/_axes_stream_auto.py in a fresh process: torch initialises the
+    GPU first there; this process already holds libpyas_hip's context)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-u", "-m", "tests._axes_stream_auto"], cwd=root,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, f"rc={r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-4000:]}"
+    assert "axes-stream-auto OK" in r.stdout
+    print(r.stdout.strip())
