@@ -819,8 +819,11 @@ static void dense_geometry(pyas::AxesDense &d, const pyas_batch *b, uint32_t axe
         // per output (PYAS_ROW_LDS: 0 off, else the most lanes allowed; default 2)
         const char *e_lds = getenv("PYAS_ROW_LDS");     // per call: tests switch it
         const int row_lds = e_lds ? atoi(e_lds) : 2;
-        const char *e_tpw = getenv("PYAS_ROW_LDS_TPW");   // tiles per wave; measured on (2,): 2 best
-        const int64_t row_tpw = e_tpw && atoi(e_tpw) > 0 ? (int64_t)atoi(e_tpw) : (int64_t)2;
+        // tiles per wave: 2 measured best in round 1; with the staged partial
+        // stores (round 3) 1 is: C3 (2,) 0.80-0.81 ms against 0.82 (4: 0.87,
+        // 8: 0.89; profiles/r03/axes_row_tpw.txt)
+        const char *e_tpw = getenv("PYAS_ROW_LDS_TPW");
+        const int64_t row_tpw = e_tpw && atoi(e_tpw) > 0 ? (int64_t)atoi(e_tpw) : (int64_t)1;
         if (row_lds && d.RO == 1 && V <= 16) {
             int h = 1;
             while (h < row_lds && h < 4 && V % (h * 2) == 0) h *= 2;
