@@ -19,7 +19,7 @@ save_logs() {   # on success and on failure: the bench logs, prefixed by config
 }
 trap save_logs EXIT
 cd /tmp
-bench=("$root/bench.py" --config "$cfg" --cpu-chunks 0 --host-inclusive 0 --file-inclusive 0 "$@")
+bench=("$root/bench.py" --config "$cfg" --extra none --cpu-chunks 0 --host-inclusive 0 --file-inclusive 0 "$@")
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
     python3 "${bench[@]}" --steps 20 --warmup 5 > "$out/bench_trace.log" 2>&1
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- \
