@@ -2312,7 +2312,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
 
 // Per-chunk column layout streamed over several chunks (pyas_reduce_axes
 // with every chunk whole, dense_geometry's split 1, rows per chunk a
-// multiple of 4).  Block (g, j) owns items j * kBlock + t of chunks
+// multiple of 4).  Block (g, j) owns items j * kBlock * NV ... of chunks
 // g * cpb ... g * cpb + cpb - 1 and walks them as ONE ring of loads
 // (col_walk_layers: a chunk's first rows are in flight while the previous
 // chunk's last group is summed), instead of one short walk per chunk with a
