@@ -71,6 +71,7 @@ struct pyas_ctx {
     int32_t inflate_wbits = 13;   // LDS history ring of pyas_inflate: 2^13 B per stream
     bool chained = true;          // k_finish folds the total itself (arrival counter)
     int64_t fold_min_blocks = 2048;   // pyas_reduce_axes_grid: fewest workgroups worth folding
+    int32_t n_cu = 256;               // compute units (hipDeviceProp_t; sizes k_axes_col_stream's grid)
     pyas::TieRule tie[2];             // NumPy's zero-sign rule for f32, f64 (lanes 0: unset)
     pyas::Ingest *ingest = nullptr;   // pinned staging ring of pyas_read_ranges (lazy)
     std::mutex mu;
@@ -281,6 +282,9 @@ int pyas_ctx_create(int device, pyas_ctx **out) {
     PYAS_HIP(hipSetDevice(device));
     pyas_ctx *c = new pyas_ctx();
     c->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        c->n_cu = cus;
     *out = c;
     return PYAS_OK;
 }
@@ -938,11 +942,16 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *ma
         const int64_t forced = e ? atoll(e) : -1;
         const int64_t kiv = x.d.KI / (16 / es);     // vectors per kept inner run
         const int nv = shuf ? 1 : (kiv % 256 == 0 && col_items >= 4 * pyas::kBlock) ? 4 : 2;
-        const int64_t target = shuf ? 512 : nv == 4 ? 1024 : 256;   // workgroups
+        // workgroups per CU aimed at (C3: 1024 / 256 / 512 on 256 CUs).  The
+        // chunks per workgroup are rounded up, so the grid never exceeds the
+        // target: one workgroup past a round of the CUs would take a second
+        // round nearly alone (C3 (1,) at 24 or 48 chunks per workgroup:
+        // 0.86-0.89 ms against 0.79 at 32; profiles/r03/axes_stream_cpb.txt)
+        const int64_t target = (int64_t)ctx->n_cu * (shuf ? 2 : nv == 4 ? 4 : 1);
         // auto: the measured geometries, with every lane's NV items present
         const bool auto_ok = shuf ? x.d.KI < 128 : col_items >= nv * pyas::kBlock;
         const int64_t bpc = (col_items + nv * pyas::kBlock - 1) / (nv * pyas::kBlock);
-        int64_t cpb = forced >= 0 ? forced : auto_ok ? batch->n_chunks * bpc / target : 0;
+        int64_t cpb = forced >= 0 ? forced : auto_ok ? (batch->n_chunks * bpc + target - 1) / target : 0;
         if (cpb > batch->n_chunks) cpb = batch->n_chunks;
         if (cpb >= 2 || forced > 0) {
             x.d.cpb = cpb;
