@@ -101,6 +101,17 @@ def parse(argv=None):
                    help="CPU-only rehearsal of the N-rank launcher (gloo, no GPU): each rank "
                         "reduces its shard of a small variable with NumPy, the partials are "
                         "all-gathered and folded in rank order, rank 0 prints the wiring")
+    p.add_argument("--selftest-hang-rank", type=int, default=-1,
+                   help="with --selftest-launch: this rank sleeps instead of joining the "
+                        "all-gather (the launcher's wall limit must end the run)")
+    p.add_argument("--selftest-fail-rank", type=int, default=-1,
+                   help="with --selftest-launch: this rank exits with status 3 after joining")
+    p.add_argument("--launch-timeout", type=float, default=900.0,
+                   help="N > 1 launcher: wall limit in seconds for all ranks together; past it "
+                        "the ranks still running are named, stopped, and the launch exits 124")
+    p.add_argument("--dist-timeout", type=float, default=300.0,
+                   help="seconds a collective may wait before torch.distributed aborts it "
+                        "(init_process_group timeout)")
     return p.parse_args(argv)
 
 
@@ -134,7 +145,7 @@ def visible_gpus() -> int:
     return n
 
 
-def launch_ranks(n: int, argv, check_devices: bool = True, timeout: float | None = None) -> int:
+def launch_ranks(n: int, argv, check_devices: bool = True, timeout: float | None = 900.0) -> int:
     """Start ``n`` rank processes of this script (one per GPU) and wait.
 
     Runs in a process that has not touched the GPU (it counts devices from
@@ -143,7 +154,9 @@ def launch_ranks(n: int, argv, check_devices: bool = True, timeout: float | None
     GPU-initialised process is ever replaced.  Exits non-zero if fewer than
     ``n`` devices are visible: the bench never silently runs fewer ranks.
     If one rank fails the others are stopped (they would wait forever in
-    the next collective)."""
+    the next collective), and the failing rank is named on stderr.  Past
+    ``timeout`` seconds the ranks still running are named, stopped
+    (SIGTERM, then SIGKILL after 10 s) and the launch returns 124."""
     if check_devices:
         have = visible_gpus()
         if have < 0:   # no KFD topology readable: the runtime's count (amdsmi; no HIP init here)
@@ -162,33 +175,52 @@ def launch_ranks(n: int, argv, check_devices: bool = True, timeout: float | None
                                       env=env))
     t0 = time.monotonic()
     rc = 0
-    live = list(procs)
+    live = dict(enumerate(procs))
     while live:
-        for p in list(live):
+        for r, p in list(live.items()):
             code = p.poll()
             if code is None:
                 continue
-            live.remove(p)
+            del live[r]
             if code != 0 and rc == 0:
                 rc = code if code > 0 else 1
-                for q in live:
+                print(f"bench.py: rank {r} exited with status {code}; stopping ranks "
+                      f"{sorted(live)}", file=sys.stderr, flush=True)
+                for q in live.values():
                     q.terminate()
-        if timeout is not None and time.monotonic() - t0 > timeout and live:
-            rc = rc or 124
-            for q in live:
+        if timeout is not None and live and time.monotonic() - t0 > timeout:
+            if rc == 0:
+                rc = 124
+                print(f"bench.py: wall limit {timeout:.0f} s passed; ranks {sorted(live)} still "
+                      f"running (hung or slow), stopping them", file=sys.stderr, flush=True)
+            for q in live.values():
                 q.terminate()
+            t_stop = time.monotonic()
+            while live and time.monotonic() - t_stop < 10:
+                for r, p in list(live.items()):
+                    if p.poll() is not None:
+                        del live[r]
+                time.sleep(0.05)
+            for q in live.values():
+                q.kill()
+            live = {}
         time.sleep(0.05)
     for p in procs:
         try:
             p.wait(timeout=10)
         except subprocess.TimeoutExpired:
             p.kill()
+            p.wait()
     return rc
 
 
-def selftest_launch(rank: int, world: int) -> None:
+def selftest_launch(rank: int, world: int, hang_rank: int = -1, dist_timeout: float = 300.0,
+                    fail_rank: int = -1) -> None:
     """Rank body of ``--selftest-launch`` (CPU, gloo): the sharding and the
-    rank-order fold of the GPU path, with NumPy per-chunk partials."""
+    rank-order fold of the GPU path, with NumPy per-chunk partials.
+    ``hang_rank`` sleeps instead of joining the exchange (launcher test)."""
+    import datetime
+
     import torch
     import torch.distributed as dist
 
@@ -196,7 +228,12 @@ def selftest_launch(rank: int, world: int) -> None:
     from pyactivestorage_amd.engine import partial_dtype
     from pyactivestorage_amd.synthetic import chunk_major_host
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=dist_timeout))
+    if rank == hang_rank:
+        time.sleep(3600)
+    if rank == fail_rank:
+        sys.exit(3)
     shape, chunks = (32, 16, 24), (8, 8, 8)
     buf, offsets = chunk_major_host(shape, chunks, np.float32)
     vals = buf.view(np.float32).reshape(len(offsets), -1)
@@ -591,7 +628,9 @@ def run_config(env, name, scaling, steps, warmup, args, full_check=False):
                                              if use_dist else None),
                      "chunks": [int(x) for x in per[:, 4]],
                      "gen_s": [round(float(x), 2) for x in per[:, 5]]},
-        "kernel": "pyas::k_reduce", "kernel_ms_rank0": round(kern_ms, 5),
+        # k_reduce: every chunk whole, 4-/8-byte dtypes; k_reduce_u: selections (C5's hyperslab)
+        "kernel": "pyas::k_reduce" if sels is None and dt.itemsize >= 4 else "pyas::k_reduce_u",
+        "kernel_ms_rank0": round(kern_ms, 5),
         "bytes_rank0": bytes_per_launch, "chunks_rank0": n_chunks,
         "frac_rank0": round(achieved / HBM_PEAK_GBS, 4),
         "frac_min_rank": round(float((per[:, 3] / (per[:, 1] * 1e-3) / 1e9).min()) / HBM_PEAK_GBS, 4),
@@ -606,7 +645,8 @@ def main():
     if world_env is None and args.gpus > 1:
         # plain `python bench.py --gpus N`: become the launcher of N ranks
         sys.exit(launch_ranks(args.gpus, sys.argv[1:],
-                              check_devices=not args.selftest_launch and args.dist_backend == "nccl"))
+                              check_devices=not args.selftest_launch and args.dist_backend == "nccl",
+                              timeout=args.launch_timeout if args.launch_timeout > 0 else None))
     world = int(world_env or 1)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -614,7 +654,7 @@ def main():
         print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
         sys.exit(2)
     if args.selftest_launch:
-        selftest_launch(rank, world)
+        selftest_launch(rank, world, args.selftest_hang_rank, args.dist_timeout, args.selftest_fail_rank)
         return
 
     import torch
@@ -630,11 +670,15 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     if use_dist:
+        import datetime
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # a bounded timeout: a rank stuck in a collective aborts with an error
+        # instead of hanging the whole run (torch's nccl watchdog enforces it)
+        limit = datetime.timedelta(seconds=args.dist_timeout)
         if gloo:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=limit)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=limit)
 
     from pyactivestorage_amd.device import get_context
 
@@ -731,7 +775,7 @@ def main():
                          "traffic_source": "profile figure, not measured in this run: profiles/traffic.json "
                                            "(rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of this config's "
                                            "k_reduce, per launch)",
-                         "kernel": "pyas::k_reduce", "kernel_ms_avg": head["kernel_ms_rank0"],
+                         "kernel": head["kernel"], "kernel_ms_avg": head["kernel_ms_rank0"],
                          "bytes_per_launch": head["bytes_rank0"]},
             "per_rank": head["per_rank"],
             "cpu_baseline": cpu,

@@ -423,21 +423,28 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
 }
 
 // Per-stream gate word and key scratch of the tie passes.
+// Growing swaps the pointer under the context lock; the old buffer is freed
+// after the stream's queued work is done, outside the lock, so
+// other threads never wait on this stream.
 int tie_scratch(pyas_ctx *ctx, void *stream, size_t bytes, void **out) {
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    Scratch &s = ctx->tie_scratch[stream];
-    if (s.bytes < bytes) {
-        if (s.ptr) {
-            PYAS_HIP(hipStreamSynchronize((hipStream_t)stream));
-            PYAS_HIP(hipFree(s.ptr));
-            s.ptr = nullptr;
-            s.bytes = 0;
+    void *old = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        Scratch &s = ctx->tie_scratch[stream];
+        if (s.bytes < bytes) {
+            const size_t want = bytes < 4096 ? 4096 : bytes;
+            void *p = nullptr;
+            PYAS_HIP(hipMalloc(&p, want));
+            old = s.ptr;
+            s.ptr = p;
+            s.bytes = want;
         }
-        const size_t want = bytes < 4096 ? 4096 : bytes;
-        PYAS_HIP(hipMalloc(&s.ptr, want));
-        s.bytes = want;
+        *out = s.ptr;
     }
-    *out = s.ptr;
+    if (old) {
+        PYAS_HIP(hipStreamSynchronize((hipStream_t)stream));
+        PYAS_HIP(hipFree(old));
+    }
     return PYAS_OK;
 }
 

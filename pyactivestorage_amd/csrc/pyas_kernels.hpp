@@ -2660,7 +2660,9 @@ __device__ __forceinline__ TieCall tie_call(const int64_t *cnt, const int64_t *v
     c.lr = lr;
     c.npr = (lr + piece - 1) / piece;
     c.acc = (one && !buffered && inner_stride != 1) ? 1 : 0;
-    const int64_t n1 = c.acc && lr < piece ? (piece / lr < kb ? piece / lr : kb) : 0;
+    // only a non-empty kept block right outside the group can be copied
+    // (call_structure's `if block and piece`)
+    const int64_t n1 = c.acc && c.block && lr < piece ? (piece / lr < kb ? piece / lr : kb) : 0;
     if (n1 > first) c.n_copy = n1;
     else c.block = 0;
     return c;

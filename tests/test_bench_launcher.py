@@ -57,3 +57,27 @@ def test_failing_rank_fails_the_launch():
                         "--config", "no-such-config"], env=_env(), capture_output=True, text=True,
                        timeout=120)
     assert r.returncode != 0
+
+
+def test_hung_rank_ends_the_launch_within_the_wall_limit():
+    """one rank that never joins the exchange (it sleeps
+    an hour) must not hang the run.  The launcher's wall limit stops every
+    rank, names the ones still running and exits 124 well inside the bound."""
+    import time
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--selftest-launch", "--selftest-hang-rank", "1",
+                        "--launch-timeout", "25", "--dist-timeout", "600"],
+                       env=_env(), capture_output=True, text=True, timeout=200)
+    took = time.monotonic() - t0
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])
+    assert "wall limit" in r.stderr and "1" in r.stderr.split("ranks", 1)[1].split("still", 1)[0]
+    assert took < 25 + 60, took
+
+
+def test_failing_rank_is_named():
+    """A rank that exits non-zero fails the launch with its status, is named,
+    and the ranks left waiting in the exchange are stopped."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--selftest-launch", "--selftest-fail-rank", "2",
+                        "--launch-timeout", "100"], env=_env(), capture_output=True, text=True, timeout=200)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "bench.py: rank 2 exited with status 3" in r.stderr

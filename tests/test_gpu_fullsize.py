@@ -41,7 +41,7 @@ def test_full_size_config(gpu, name):
 
 @pytest.mark.parametrize("name", ["c4", "c5"])
 def test_full_size_samples_against_oracle(gpu, name):
-    """Real-size chunks of C4 (64 x 128^3 f32, shuffled, masked) and C5 (512 x
+    """Real-size chunks of C4 (64 x 128^3 f32, shuffled, masked) and C5 (256 x
     32^3 f64, boundary-heavy hyperslab) against the oracle's storage.py and
     _from_storage combine (tests/_fullsize_oracle.py, fresh process)."""
     r = subprocess.run([sys.executable, "-u", "-m", "tests._fullsize_oracle", name], cwd=ROOT,

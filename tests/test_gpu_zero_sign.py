@@ -207,3 +207,48 @@ def test_replay_threads_share_a_query(gpu):
             t.join()
         assert not errors, errors[0]
     active_mod.release_resident(var)
+
+
+def test_strided_full_reduction_sign(gpu):
+    """a full reduction of an unmasked strided view whose
+    kept block is empty (a 1-D chunk[::k], or (8,12,40)[2:5,:,::4] reduced
+    over every dim) is one strided call per run (NumPy's acc loop), not a
+    copied contiguous call.  Dense signed zeros, compared byte for byte with
+    NumPy through the oracle."""
+    if tie_rule("<f4") is None or tie_rule("<f8") is None:
+        pytest.skip("no NumPy tie rule derived on this host")
+    rng = np.random.default_rng(590)
+    none = (None, None, None, None)
+    n_cases = 0
+    for dt in ("<f4", "<f8"):
+        for n in (7, 64, 300, 4100, 20000):
+            for step in (2, 3, 5, -2, 16):
+                for dens in (0.3, 0.9):
+                    a = rng.uniform(0.5, 9.0, n).astype(dt)
+                    z = rng.random(n) < dens
+                    a[z] = np.where(rng.random(int(z.sum())) < 0.5, -0.0, 0.0)
+                    for sel in ((slice(None, None, step),), (slice(1, n - 1, step),)):
+                        for method in (np.ma.min, np.min):
+                            want, wn = ref.reduce_chunk_bytes(a.tobytes(), None, None, none, dt, (n,), "C", sel,
+                                                              (0,), method)
+                            got, gn = pas.reduce_chunk_bytes(a.tobytes(), None, None, none, dt, (n,), "C", sel,
+                                                             (0,), method)
+                            _same_bytes(want, got, (dt, n, sel, method.__name__))
+                            assert np.array_equal(wn, gn)
+                            n_cases += 1
+        shape = (8, 12, 40)
+        for rep in range(24):
+            a = rng.uniform(0.5, 9.0, shape).astype(dt)
+            z = rng.random(shape) < 0.6
+            a[z] = np.where(rng.random(int(z.sum())) < 0.5, -0.0, 0.0)
+            for sel in ((slice(2, 5), slice(None), slice(None, None, 4)),
+                        (slice(None), slice(3, 9), slice(1, None, 3)),
+                        (slice(None, None, 2), slice(None), slice(None, None, 8))):
+                for axis in ((0, 1, 2), (1, 2), (0, 2)):
+                    want, _ = ref.reduce_chunk_bytes(a.tobytes(), None, None, none, dt, shape, "C", sel, axis,
+                                                     np.min)
+                    got, _ = pas.reduce_chunk_bytes(a.tobytes(), None, None, none, dt, shape, "C", sel, axis,
+                                                    np.min)
+                    _same_bytes(want, got, (dt, rep, sel, axis))
+                    n_cases += 1
+    assert n_cases > 1000

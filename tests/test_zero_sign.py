@@ -223,3 +223,23 @@ def test_keys_match_numpy_copied_first_fill(dt):
             a = _dense(rng, shape, dt, np.min)
             n += _check_predict(a[key], axis, np.min)
     assert n > 500
+
+
+def test_missing_tie_rule_is_reported_once(monkeypatch):
+    """when no rule reproduces the host's NumPy, the
+    context says so (RuntimeWarning once per dtype and process, and the
+    per-dtype flag Context.tie_signs_exact is built from the same list)."""
+    import warnings
+
+    from pyactivestorage_amd import device, zerosign
+    real = zerosign.tie_rule
+    monkeypatch.setattr(zerosign, "tie_rule", lambda dt: None if np.dtype(dt).itemsize == 8 else real(dt))
+    monkeypatch.setattr(device, "_TIE_WARNED", set())
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        first = device.host_tie_rules()
+        again = device.host_tie_rules()
+    msgs = [str(w.message) for w in rec if issubclass(w.category, RuntimeWarning)]
+    assert len(msgs) == 1 and "f8" in msgs[0], msgs
+    assert [(dt, r is None) for _, dt, r in first] == [("f4", real("f4") is None), ("f8", True)]
+    assert [(dt, r is None) for _, dt, r in again] == [(dt, r is None) for _, dt, r in first]
