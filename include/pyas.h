@@ -299,6 +299,25 @@ int pyas_combine_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
                           int64_t n, uint32_t combine_flags, pyas_partial *out,
                           void *stream);
 
+/* ---- several GPUs in one process (active.py:557-598 across devices) ------
+ * Each of the ndev contexts (distinct devices) reduces its own batch of the
+ * SAME variable on its own stream (pyas_reduce_chunks, combine_flags as
+ * there); the per-device totals then travel in ONE RCCL all-gather over
+ * xGMI (communicators over the listed devices, created with
+ * ncclCommInitAll on first use of a device list and kept until
+ * pyas_shard_release) and every device folds them in list order.
+ * out[k] (device memory of ctx[k], ndev + 1 partials): out[k][0] receives
+ * the global total, identical on every device; out[k][1 + j] the total of
+ * device j.  mask may be NULL (unmasked) or hold one mask per device.
+ * Asynchronous like every launch: synchronise streams[k] before reading.
+ * The multi-process equivalent (one process per GPU) is
+ * pyactivestorage_amd.distributed over torch.distributed. */
+int pyas_reduce_sharded(pyas_ctx *const *ctx, const pyas_batch *const *per_dev,
+                        const pyas_mask *const *mask, int32_t ndev, uint32_t combine_flags,
+                        pyas_partial *const *out, void *const *streams);
+/* Destroy the cached RCCL communicators of pyas_reduce_sharded. */
+int pyas_shard_release(void);
+
 /* Segmented fixed-order combine: out[s] = fold of in[index[k]] for k in
  * [seg_offsets[s], seg_offsets[s+1]) in order (device arrays).  This is the
  * partial-axis form of the Active combine (active.py:575-598): `in` holds

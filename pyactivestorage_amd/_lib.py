@@ -168,6 +168,8 @@ SIGNATURES = {
     "pyas_select_scatter": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(Scatter),
                             _vp, _vp, _vp],
     "pyas_combine_partials": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
+    "pyas_reduce_sharded": [_vp, _vp, _vp, _i32, _u32, _vp, _vp],
+    "pyas_shard_release": [],
     "pyas_combine_segments": [_vp, _i32, _vp, _vp, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_grid": [_vp, _i32, _vp, ctypes.POINTER(Grid), _u32, _vp, _vp],
     "pyas_reduce_axes_grid": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(Grid), _u32,

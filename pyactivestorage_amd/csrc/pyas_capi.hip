@@ -401,9 +401,28 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
     if ((axes_mask & ~full) != 0) return fail(PYAS_EINVAL, "axes_mask 0x%x outside the chunk rank", axes_mask);
     if ((axes_mask & full) != full && !out_offsets)
         return fail(PYAS_EINVAL, "out_offsets is NULL for a partial-axis reduction");
-    int64_t kept = 1;
-    for (int d = 0; d < batch->ndim; ++d)
+    int64_t kept = 1, red = 1;
+    for (int d = 0; d < batch->ndim; ++d) {
         if (!((axes_mask >> d) & 1u)) kept *= batch->chunk_shape[d];
+        else red *= batch->chunk_shape[d];
+    }
+    if (red >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "tie pass: 2^31 or more reduced elements per output");
+    // lanes per output of the backward scan (k_tie_scan): one when the
+    // innermost visited dim is kept (elementwise calls: adjacent lanes hold
+    // adjacent outputs, and each lane stops at its last zero), else by the
+    // reduced count per output
+    int inner_kept = -1;
+    for (int i = batch->ndim - 1; i >= 0 && inner_kept < 0; --i) {
+        const int d = geom->perm[i];
+        if (batch->chunk_shape[d] != 1) inner_kept = ((axes_mask >> d) & 1u) ? 0 : 1;
+    }
+    int group = inner_kept == 1 ? 1 : red >= 16384 ? pyas::kBlock : red >= 1024 ? 64 : 16;
+    const char *e_group = getenv("PYAS_TIE_GROUP");   // per call: tests force each layout
+    if (e_group && *e_group) {
+        const int g = atoi(e_group);
+        if (g == 1 || g == 16 || g == 64 || g == pyas::kBlock) group = g;
+    }
+    a.group = group;
     a.t = *t;
     a.g = *geom;
     a.axes = axes_mask;
@@ -414,7 +433,8 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
     a.parts = partials;
     a.flags = flags;
     a.gate = gate;
-    a.tpc = (kept + pyas::kTieTile - 1) / pyas::kTieTile;
+    const int64_t per_wg = pyas::kBlock / group;   // outputs per workgroup
+    a.tpc = (kept + per_wg - 1) / per_wg;
     const int64_t grid = batch->n_chunks * a.tpc;
     if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "tie grid too large");
     PYAS_HIP(hipSetDevice(ctx->device));

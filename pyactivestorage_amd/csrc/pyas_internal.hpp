@@ -150,7 +150,6 @@ struct TieCall {
     int64_t lr, npr;                  // call length (1: elementwise), pieces per call
     int64_t n_copy;                   // acc: runs of that fill (contiguous calls), 0: none
 };
-constexpr int kTieTile = 2048;        // chunk outputs per k_tie_chunks workgroup (32 KiB of keys)
 struct TieChunkArgs {
     ReduceArgs r;
     TieRule t;
@@ -161,7 +160,8 @@ struct TieChunkArgs {
     pyas_partial *parts;              // rewrite mode, or NULL and:
     uint8_t *flags;                   //   flag mode (one byte per chunk output)
     const uint32_t *gate;             //   flag mode: skip when *gate == 0
-    int64_t tpc;                      // output tiles per chunk
+    int64_t tpc;                      // output tiles per chunk (kBlock / group outputs each)
+    int32_t group;                    // lanes per output: 1, 16, 64 or kBlock (k_tie_scan)
 };
 struct TieGridArgs {
     pyas_grid g;                      // kind 0: layers from the grid tables

@@ -2737,14 +2737,66 @@ __device__ __forceinline__ void tie_put(pyas_partial *p, uint32_t which, int sg)
     if ((which & 2u) && TT<T>::from(p->max) == (T)0) TT<T>::put(p->max, z);
 }
 
-// Level 1 (storage.py:99-100 over chunk[sel]): workgroup = (chunk, tile of
-// kTieTile outputs).  Rewrite mode (parts): outputs whose min/max is a zero
-// get NumPy's sign.  Flag mode (flags): one byte per chunk output, bit 0 an
+// Group reductions over G consecutive lanes: G = 1 (none), 16 or 64 (inside
+// a wave, DPP/bpermute butterflies that never leave the group), kBlock (the
+// workgroup, through LDS; every thread of the block must call it).
+template <int G>
+__device__ __forceinline__ uint64_t grp_max_u64(uint64_t v, uint64_t *lds) {
+    if constexpr (G == 1) {
+        return v;
+    } else if constexpr (G <= kWave) {
+#pragma unroll
+        for (int m = G / 2; m >= 1; m >>= 1) {
+            const uint64_t o = shfl_xor(v, m);
+            v = o > v ? o : v;
+        }
+        return v;
+    } else {
+        static_assert(G == kBlock, "group = lanes of a wave or the workgroup");
+#pragma unroll
+        for (int m = kWave / 2; m >= 1; m >>= 1) {
+            const uint64_t o = shfl_xor(v, m);
+            v = o > v ? o : v;
+        }
+        __syncthreads();
+        if ((threadIdx.x & (kWave - 1)) == 0) lds[threadIdx.x / kWave] = v;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kBlock / kWave; ++i) v = lds[i] > v ? lds[i] : v;
+        return v;
+    }
+}
+
+template <int G>
+__device__ __forceinline__ uint64_t grp_min_u64(uint64_t v, uint64_t *lds) {
+    return ~grp_max_u64<G>(~v, lds);
+}
+
+// Level 1 (storage.py:99-100 over chunk[sel]): the sign NumPy gives each zero
+// min/max output of a chunk, from ONE backward scan over the output's reduced
+// positions e (its visiting order) that stops early.  Every key combines by
+// max except W, and:
+//  - a significant zero of a contiguous call (the seed aside: a top-lane or
+//    remainder zero, K1 != 0) at e1 decides the output on its own: W's zero is
+//    never later than e1 (it sits in e1's row or an earlier one, and in e1's
+//    row it has rank 0 (then it is e1) or precedes the remainder);
+//  - a strided call's zero (KA) in row r beats every zero of earlier rows and
+//    every copied (contiguous) call; the rest of row r decides among them.
+// So the scan walks e downwards in steps of G*V elements and stops after the
+// step holding the first significant zero, or once it has finished the row of
+// the first strided zero; only an output with neither is scanned to e = 0, and
+// then its keys are complete.  tie_finalize of the scanned suffix's keys
+// equals that of all keys (zerosign.finalize; tests compare with NumPy).
+// G lanes share an output (1: one output per lane, for elementwise calls,
+// where adjacent lanes hold adjacent outputs), NG = kBlock/G outputs per
+// workgroup.  Rewrite mode (parts): outputs whose min/max is a zero get
+// NumPy's sign.  Flag mode (flags): one byte per chunk output, bit 0 an
 // unmasked zero, bit 1 the winning zero's sign; skipped when *gate == 0.
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_tie_chunks(TieChunkArgs a) {
-    __shared__ uint64_t sk1[kTieTile], sw[kTieTile], ska[kTieTile];
-    __shared__ uint8_t swant[kTieTile];
+template <typename T, int G>
+__global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
+    constexpr int NG = kBlock / G;
+    constexpr int V = G >= kWave ? 4 : 1;     // elements per lane per step
+    __shared__ uint64_t lds[kBlock / kWave];
     const ReduceArgs &r = a.r;
     if (a.gate && *a.gate == 0u) return;
     const int64_t c = (int64_t)blockIdx.x / a.tpc, tile = (int64_t)blockIdx.x - c * a.tpc;
@@ -2758,35 +2810,22 @@ __global__ __launch_bounds__(kBlock) void k_tie_chunks(TieChunkArgs a) {
         if ((a.axes >> d) & 1u) R *= cnt[d];
         else n_out *= cnt[d];
     }
-    const int64_t o0 = tile * kTieTile;
-    if (n_out == 0 || R == 0 || o0 >= n_out) return;   // block-uniform
-    const int no = (int)((n_out - o0) < kTieTile ? (n_out - o0) : kTieTile);
-    const int64_t ob = (a.out_offsets ? a.out_offsets[c] : c) + o0;
-    int any = 0;
-    for (int ol = threadIdx.x; ol < no; ol += kBlock) {
-        sk1[ol] = 0;
-        sw[ol] = kTieWNone;
-        ska[ol] = 0;
-        const uint8_t want = a.parts ? (tie_zero<T>(a.parts[ob + ol], a.which) ? 1 : 0) : 1;
-        swant[ol] = want;
-        any |= want;
-    }
-    if (!__syncthreads_or(any)) return;
-    int64_t vstride[PYAS_MAX_DIMS], wred[PYAS_MAX_DIMS];
+    if (n_out == 0 || R == 0 || tile * NG >= n_out) return;   // block-uniform
+    const int grp = (int)threadIdx.x / G, gl = (int)threadIdx.x % G;
+    const int64_t ol = tile * NG + grp;
+    // group-uniform from here; G == kBlock: NG == 1, so ol < n_out
+    if (ol >= n_out) return;
+    const int64_t ob = (a.out_offsets ? a.out_offsets[c] : c) + ol;
+    if (a.parts && !tie_zero<T>(a.parts[ob], a.which)) return;
+    int64_t vstride[PYAS_MAX_DIMS];
     {
-        int64_t st = 1, sr = 1;
+        int64_t st = 1;
 #pragma unroll
         for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
             if (i < r.ndim) {
                 const int d = a.g.perm[i];
                 vstride[d] = st;
                 st *= cnt[d];
-                if ((a.axes >> d) & 1u) {
-                    wred[d] = sr;
-                    sr *= cnt[d];
-                } else {
-                    wred[d] = 0;
-                }
             }
         }
         if (a.g.flags & PYAS_TIE_VIEW) {
@@ -2797,8 +2836,12 @@ __global__ __launch_bounds__(kBlock) void k_tie_chunks(TieChunkArgs a) {
     }
     const TieCall call = tie_call(cnt, vstride, a.axes, a.g.perm, r.ndim, (a.g.flags & PYAS_TIE_BUFFERED) != 0,
                                   a.t.piece);
-    int64_t bw[PYAS_MAX_DIMS];   // kept-block weights (NumPy's copied first fill), inner first
+    // the output's kept coordinates: memory / table base, and whether its
+    // first run is a copied (contiguous) call of a strided reduction
+    Decomp base{0, {0, 0}};
+    bool olanes = false;
     {
+        int64_t bw[PYAS_MAX_DIMS];   // kept-block weights (NumPy's copied first fill), inner first
         int64_t st = 1;
 #pragma unroll
         for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
@@ -2808,74 +2851,113 @@ __global__ __launch_bounds__(kBlock) void k_tie_chunks(TieChunkArgs a) {
                 if ((call.block >> d) & 1u) st *= cnt[d];
             }
         }
-    }
-    // walk outputs fastest when the innermost non-1 dim is kept (adjacent lanes
-    // then read adjacent elements), else reduced positions fastest
-    bool ofast = false, found = false;
+        int64_t oo = ol, bidx = 0;
+        bool beyond = false;   // a kept coordinate outside the block is non-zero
 #pragma unroll
-    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-        if (!found && d < r.ndim && cnt[d] != 1) {
-            found = true;
-            ofast = !((a.axes >> d) & 1u);
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            if (d < r.ndim && !((a.axes >> d) & 1u)) {
+                const int64_t q = oo / cnt[d], k = oo - q * cnt[d];
+                oo = q;
+                if ((call.block >> d) & 1u) bidx += k * bw[d];
+                else beyond |= k != 0;
+                base.mem += sel_index(s, r.pool, d, k) * r.cstride[d];
+                base.v[0] += k * r.tab.stride[0][d];
+                base.v[1] += k * r.tab.stride[1][d];
+            }
+        }
+        olanes = call.n_copy && !beyond && bidx < call.n_copy;
+    }
+    // reduced dims in visiting order, innermost first (slot i = perm[nd-1-i])
+    uint32_t rc[PYAS_MAX_DIMS];
+    int32_t rst[PYAS_MAX_DIMS], rsp[PYAS_MAX_DIMS];
+    int64_t rcs[PYAS_MAX_DIMS], rt0[PYAS_MAX_DIMS], rt1[PYAS_MAX_DIMS];
+    int nr = 0;
+#pragma unroll
+    for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
+        if (i < r.ndim) {
+            const int d = a.g.perm[i];
+            if (((a.axes >> d) & 1u) && cnt[d] != 1) {
+#pragma unroll
+                for (int j = 0; j < PYAS_MAX_DIMS; ++j) {
+                    if (j == nr) {
+                        rc[j] = (uint32_t)cnt[d];
+                        rst[j] = s.start[d];
+                        rsp[j] = s.step[d];
+                        rcs[j] = r.cstride[d];
+                        rt0[j] = r.tab.stride[0][d];
+                        rt1[j] = r.tab.stride[1][d];
+                    }
+                }
+                ++nr;
+            }
         }
     }
     MaskT<T> mk;
     mk.init(r.mask);
-    const uint8_t *base = r.data + r.offsets[c];
-    const int64_t total = (int64_t)no * R;
-    for (int64_t f = threadIdx.x; f < total; f += kBlock) {
-        int64_t ol, rr;
-        if (ofast) {
-            rr = f / no;
-            ol = f - rr * no;
-        } else {
-            ol = f / R;
-            rr = f - ol * R;
-        }
-        if (!swant[ol]) continue;
-        int64_t oo = o0 + ol, e = 0, bidx = 0;
-        bool beyond = false;   // a kept coordinate outside the block is non-zero
-        Decomp o{0, {0, 0}};
+    const uint8_t *data = r.data + r.offsets[c];
+    uint64_t k1 = 0, kw = kTieWNone, ka = 0, stop1 = 0;   // stop1 = scan floor + 1 (0: none yet)
+    int64_t hi = R;
+    while (hi > 0 && (int64_t)stop1 - 1 < hi) {           // group-uniform
+        const int64_t lo = hi - (int64_t)G * V;
+        T x[V];
+        Decomp o[V];
 #pragma unroll
-        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-            if (d < r.ndim) {
-                int64_t k;
-                if ((a.axes >> d) & 1u) {
-                    const int64_t q = rr / cnt[d];
-                    k = rr - q * cnt[d];
-                    rr = q;
-                    e += k * wred[d];
-                } else {
-                    const int64_t q = oo / cnt[d];
-                    k = oo - q * cnt[d];
-                    oo = q;
-                    if ((call.block >> d) & 1u) bidx += k * bw[d];
-                    else beyond |= k != 0;
+        for (int j = 0; j < V; ++j) {
+            const int64_t e = lo + (int64_t)gl * V + j;
+            o[j] = base;
+            x[j] = (T)1;
+            if (e >= 0) {
+                uint32_t rr = (uint32_t)e;
+#pragma unroll
+                for (int i = 0; i < PYAS_MAX_DIMS; ++i) {
+                    if (i < nr) {
+                        const uint32_t q = rr / rc[i], k = rr - q * rc[i];
+                        rr = q;
+                        const int64_t idx = rsp[i] != 0 ? (int64_t)rst[i] + (int64_t)k * rsp[i]
+                                                        : (int64_t)r.pool[(int64_t)rst[i] + k];
+                        o[j].mem += idx * rcs[i];
+                        o[j].v[0] += (int64_t)k * rt0[i];
+                        o[j].v[1] += (int64_t)k * rt1[i];
+                    }
                 }
-                o.mem += sel_index(s, r.pool, d, k) * r.cstride[d];
-                o.v[0] += k * r.tab.stride[0][d];
-                o.v[1] += k * r.tab.stride[1][d];
+                x[j] = load_elem_rt<T>(data, r.chunk_elems, o[j].mem, a.shuf, a.bswap);
             }
         }
-        const T x = load_elem_rt<T>(base, r.chunk_elems, o.mem, a.shuf, a.bswap);
-        if (x == (T)0 && !all_masked(mk, r.tab, o, x)) {
-            const bool lanes = call.n_copy && e < call.lr && !beyond && bidx < call.n_copy;
-            uint64_t k1, w, ka;
-            tie_keys(e, __builtin_signbit(x) ? 1u : 0u, call, a.t, lanes, k1, w, ka);
-            if (k1) atomicMax(reinterpret_cast<unsigned long long *>(&sk1[ol]), (unsigned long long)k1);
-            if (w != kTieWNone) atomicMin(reinterpret_cast<unsigned long long *>(&sw[ol]), (unsigned long long)w);
-            if (ka) atomicMax(reinterpret_cast<unsigned long long *>(&ska[ol]), (unsigned long long)ka);
+        uint64_t thr1 = 0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const int64_t e = lo + (int64_t)gl * V + j;
+            if (e >= 0 && x[j] == (T)0 && !all_masked(mk, r.tab, o[j], x[j])) {
+                const bool lanes = olanes && e < call.lr;
+                uint64_t x1, xw, xa;
+                tie_keys(e, __builtin_signbit(x[j]) ? 1u : 0u, call, a.t, lanes, x1, xw, xa);
+                k1 = x1 > k1 ? x1 : k1;
+                kw = xw < kw ? xw : kw;
+                ka = xa > ka ? xa : ka;
+                int64_t thr = -1;
+                if (call.acc && !lanes) {          // finish this zero's row
+                    const int64_t q = e / call.lr, pos = e - q * call.lr;
+                    thr = q * call.lr + (pos / a.t.piece) * a.t.piece;
+                } else if (x1 != 0 && e > 0) {     // a significant zero decides
+                    thr = e;
+                }
+                const uint64_t t1 = (uint64_t)(thr + 1);
+                thr1 = t1 > thr1 ? t1 : thr1;
+            }
         }
+        thr1 = thr1 > stop1 ? thr1 : stop1;
+        stop1 = grp_max_u64<G>(thr1, lds);
+        hi = lo;
     }
-    __syncthreads();
-    for (int ol = threadIdx.x; ol < no; ol += kBlock) {
-        if (!swant[ol]) continue;
-        const int sg = tie_finalize(sk1[ol], sw[ol], ska[ol], call, a.t);
-        if (a.parts) {
-            if (sg >= 0) tie_put<T>(a.parts + ob + ol, a.which, sg);
-        } else {
-            a.flags[ob + ol] = sg < 0 ? (uint8_t)0 : (uint8_t)(1u | ((unsigned)sg << 1));
-        }
+    k1 = grp_max_u64<G>(k1, lds);
+    kw = grp_min_u64<G>(kw, lds);
+    ka = grp_max_u64<G>(ka, lds);
+    if (gl != 0) return;
+    const int sg = tie_finalize(k1, kw, ka, call, a.t);
+    if (a.parts) {
+        if (sg >= 0) tie_put<T>(a.parts + ob, a.which, sg);
+    } else {
+        a.flags[ob] = sg < 0 ? (uint8_t)0 : (uint8_t)(1u | ((unsigned)sg << 1));
     }
 }
 
@@ -3022,7 +3104,13 @@ hipError_t launch_tie_chunks_t(const TieChunkArgs &a, int64_t grid, hipStream_t 
     if constexpr (TT<T>::kind != 0) {
         return hipSuccess;
     } else {
-        hipLaunchKernelGGL((k_tie_chunks<T>), dim3((unsigned)grid), dim3(kBlock), 0, st, a);
+        switch (a.group) {
+        case 1: hipLaunchKernelGGL((k_tie_scan<T, 1>), dim3((unsigned)grid), dim3(kBlock), 0, st, a); break;
+        case 16: hipLaunchKernelGGL((k_tie_scan<T, 16>), dim3((unsigned)grid), dim3(kBlock), 0, st, a); break;
+        case 64: hipLaunchKernelGGL((k_tie_scan<T, 64>), dim3((unsigned)grid), dim3(kBlock), 0, st, a); break;
+        case kBlock: hipLaunchKernelGGL((k_tie_scan<T, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, a); break;
+        default: return hipErrorInvalidValue;
+        }
         return hipGetLastError();
     }
 }

@@ -409,6 +409,61 @@ def predict(arr: np.ndarray, axis, op, rule):
     return res
 
 
+def predict_scan(arr: np.ndarray, axis, op, rule, step: int = 1):
+    """:func:`predict` by the device's early-stopping backward scan
+    (``k_tie_scan``): each output's reduced positions are visited from the
+    last down in steps of ``step``, and the scan stops after the step that
+    holds a significant zero of a contiguous call (K1 != 0, not the seed),
+    or once the row of the first strided-call zero (KA) is finished; only
+    the scanned suffix's keys are finalized.  Returns ``(result, scanned)``:
+    the same dict as :func:`predict` and the elements read per output."""
+    nd = arr.ndim
+    red = set(range(nd)) if axis is None else {a % nd for a in (axis if isinstance(axis, tuple) else (axis,))}
+    st = [s // arr.itemsize for s in arr.strides]
+    perm = sorted(range(nd), key=lambda d: -abs(st[d]))
+    mode, lr, n_copy, block = call_structure(arr.shape, st, red, perm, not arr.dtype.isnative, rule.piece)
+    rdims = [d for d in perm if d in red]
+    kept_red = [d for d in range(nd) if d in red]
+    beyond = [d for d in perm if d not in red and d not in block]
+    vals = arr if op is np.min else -arr
+    out_shape = tuple(1 if d in red else n for d, n in enumerate(arr.shape))
+    res, scanned = {}, {}
+    P = rule.piece
+    for o in np.ndindex(out_shape):
+        sl = tuple(slice(None) if d in red else o[d] for d in range(nd))
+        tr = [kept_red.index(d) for d in rdims]
+        sub = np.transpose(np.asarray(vals[sl]), tr).reshape(-1)
+        raw = np.transpose(np.asarray(arr[sl]), tr).reshape(-1)
+        if np.isnan(sub).any() or sub.min() != 0:
+            res[o] = None
+            continue
+        olanes = False
+        if n_copy and all(o[d] == 0 for d in beyond):
+            bidx, f = 0, 1
+            for d in block:
+                bidx += o[d] * f
+                f *= arr.shape[d]
+            olanes = bidx < n_copy
+        k1, w, ka = 0, W_NONE, 0
+        stop, hi = -1, sub.size
+        while hi > 0 and hi > stop:
+            lo = max(hi - step, 0)
+            e = np.arange(lo, hi, dtype=np.int64)
+            zs = e[sub[lo:hi] == 0]
+            if zs.size:
+                lanes = (olanes & (zs < lr)) if mode == MODE_ACC else None
+                x1, xw, xa = element_keys(zs, np.signbit(raw[zs]).astype(np.uint64), mode, lr, rule, lanes)
+                k1, w, ka = max(k1, int(x1.max())), min(w, int(xw.min())), max(ka, int(xa.max()))
+                acc = (mode == MODE_ACC) & ~(np.zeros(zs.size, bool) if lanes is None else lanes)
+                rowst = (zs // lr) * lr + ((zs % lr) // P) * P
+                thr = np.where(acc, rowst, np.where((x1 != 0) & (zs > 0), zs, -1))
+                stop = max(stop, int(thr.max()))
+            hi = lo
+        scanned[o] = sub.size - hi
+        res[o] = finalize(k1, w, ka, lr, rule)
+    return res, scanned
+
+
 # ---------------------------------------------------------------------------
 # host planning of the device passes
 # ---------------------------------------------------------------------------

@@ -64,9 +64,14 @@ AXES = [(0,), (1,), (2,), (0, 1), (1, 2), (0, 2), (0, 1, 2)]
 @pytest.mark.parametrize("dt", ["<f4", ">f8"])
 @pytest.mark.parametrize("pattern", ["min0", "max0", "zeros"])
 @pytest.mark.parametrize("order", ["C", "F"])
-def test_per_call_chunk_sign(gpu, dt, pattern, order):
+@pytest.mark.parametrize("group", ["", "1", "16", "64", "256"])
+def test_per_call_chunk_sign(gpu, dt, pattern, order, group, monkeypatch):
     """storage.py:95-100 per call: every selection kind x axis subset, with
-    and without a mask attribute, against the oracle byte for byte."""
+    and without a mask attribute, against the oracle byte for byte.  The
+    level-1 backward scan (k_tie_scan) runs with the host's choice of lanes
+    per output ("") and forced to each layout (PYAS_TIE_GROUP): the result
+    may not depend on it."""
+    monkeypatch.setenv("PYAS_TIE_GROUP", group)
     if tie_rule(dt) is None:
         pytest.skip("no NumPy tie rule derived on this host")
     rng = np.random.default_rng(len(dt) * 7 + len(pattern) + len(order))
@@ -142,10 +147,13 @@ QUERIES = [(slice(None),) * 3, (slice(1, 15), slice(3, 21), slice(2, 75)), (slic
 @pytest.mark.parametrize("dt", ["<f4", "<f8"])
 @pytest.mark.parametrize("kind", ["min", "max"])
 @pytest.mark.parametrize("fill", [True, False])
-def test_active_sign(gpu, dt, kind, fill):
+@pytest.mark.parametrize("group", ["", "1", "64"])
+def test_active_sign(gpu, dt, kind, fill, group, monkeypatch):
     """Active full and partial-axis min/max (fold and two-step paths,
     resident and not) against active.py's combine over storage.py's
-    per-chunk results: the zero's sign bit included."""
+    per-chunk results: the zero's sign bit included (level-1 scan layout
+    forced by PYAS_TIE_GROUP, or the host's choice)."""
+    monkeypatch.setenv("PYAS_TIE_GROUP", group)
     if tie_rule(dt) is None:
         pytest.skip("no NumPy tie rule derived on this host")
     rng = np.random.default_rng(3 + len(kind) + fill + len(dt))
@@ -209,12 +217,14 @@ def test_replay_threads_share_a_query(gpu):
     active_mod.release_resident(var)
 
 
-def test_strided_full_reduction_sign(gpu):
+@pytest.mark.parametrize("group", ["", "1", "256"])
+def test_strided_full_reduction_sign(gpu, group, monkeypatch):
     """a full reduction of an unmasked strided view whose
     kept block is empty (a 1-D chunk[::k], or (8,12,40)[2:5,:,::4] reduced
     over every dim) is one strided call per run (NumPy's acc loop), not a
     copied contiguous call.  Dense signed zeros, compared byte for byte with
     NumPy through the oracle."""
+    monkeypatch.setenv("PYAS_TIE_GROUP", group)
     if tie_rule("<f4") is None or tie_rule("<f8") is None:
         pytest.skip("no NumPy tie rule derived on this host")
     rng = np.random.default_rng(590)

@@ -96,8 +96,12 @@ def _dense(rng, shape, dt, op):
 
 
 def _check_predict(a, axis, op):
+    """The key algorithm (full keys) and the device's early-stopping
+    backward scan (k_tie_scan, step 1 and a wave-sized step) against NumPy."""
     got = op(a, axis=axis, keepdims=True)
-    pred = zerosign.predict(a, axis, op, zerosign.tie_rule(a.dtype))
+    rule = zerosign.tie_rule(a.dtype)
+    pred = zerosign.predict(a, axis, op, rule)
+    scans = [zerosign.predict_scan(a, axis, op, rule, step)[0] for step in (1, 64)]
     n = 0
     for o, p in pred.items():
         if got[o] == 0:
@@ -105,6 +109,7 @@ def _check_predict(a, axis, op):
             assert p is not None and p == bool(np.signbit(got[o])), (a.shape, a.strides, axis, o)
         else:
             assert p is None
+        assert all(sc[o] == p for sc in scans), (a.shape, a.strides, axis, o, p, [sc[o] for sc in scans])
     return n
 
 
@@ -243,3 +248,19 @@ def test_missing_tie_rule_is_reported_once(monkeypatch):
     assert len(msgs) == 1 and "f8" in msgs[0], msgs
     assert [(dt, r is None) for _, dt, r in first] == [("f4", real("f4") is None), ("f8", True)]
     assert [(dt, r is None) for _, dt, r in again] == [(dt, r is None) for _, dt, r in first]
+
+
+def test_scan_stops_early_on_zero_heavy_data():
+    """The backward scan reads only a few elements per output when zeros are
+    dense (the cost the device pass pays on precipitation-like data)."""
+    rng = np.random.default_rng(31)
+    a = rng.uniform(1, 10, (16, 16, 256)).astype("f4")
+    z = rng.random(a.shape) < 0.5
+    a[z] = np.where(rng.random(int(z.sum())) < 0.5, -0.0, 0.0)
+    rule = zerosign.tie_rule("f4")
+    for axis in (None, (0,), (2,), (1, 2)):
+        res, scanned = zerosign.predict_scan(a, axis, np.min, rule)
+        want = zerosign.predict(a, axis, np.min, rule)
+        assert res == want
+        n_red = a.size // len(res)
+        assert np.mean(list(scanned.values())) < 0.2 * n_red, (axis, np.mean(list(scanned.values())), n_red)

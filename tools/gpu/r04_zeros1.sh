@@ -1,0 +1,22 @@
+# round 4: zero-sign pass on zero-heavy data, round-3 kernel (k_tie_chunks,
+# PYAS_LIB=lib/before) against the early-stopping scan (k_tie_scan); parity
+# first; then the per-chunk axes sweep on this library (grid rule d7df369)
+set -o pipefail
+O=gpurun_out/r04/zeros1
+mkdir -p $O
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_zero_sign.py -x -q --timeout 300 --timeout-method thread > $O/zs_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_sharded.py -x -q --timeout 250 --timeout-method thread > $O/sharded_tests.log 2>&1 || exit 1
+for lib in new before; do
+  if [ $lib = before ]; then export PYAS_LIB=$R/pyactivestorage_amd/lib/before/libpyas_before.so; else unset PYAS_LIB; fi
+  timeout -k 10 300 python -u tools/bench_zeros.py --zeros 0.5 --axes none,0,2 --reps 5 > $O/zeros50_$lib.json 2> $O/zeros50_$lib.err || exit 1
+  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/zt_$lib -o run -- \
+     python3 $R/tools/bench_zeros.py --zeros 0.5 --axes none,0,2 --reps 5 > $R/$O/zeros50_${lib}_prof.log 2>&1) || exit 1
+  cp $(find /tmp/zt_$lib -name '*kernel_stats.csv' | head -n 1) $O/zeros50_${lib}_kernel_stats.csv
+done
+unset PYAS_LIB
+timeout -k 10 300 python -u tools/bench_zeros.py --zeros 0 --axes none,0,2 --reps 5 > $O/zeros0.json 2> $O/zeros0.err || exit 1
+timeout -k 10 300 python -u tools/bench_zeros.py --zeros 0.02 --axes none,0,2 --reps 5 > $O/zeros2.json 2> $O/zeros2.err || exit 1
+timeout -k 10 300 python -u tools/bench_axes.py > $O/axes_plain.json 2> $O/axes_plain.err || exit 1
+timeout -k 10 300 python -u tools/bench_axes.py --shuffle > $O/axes_shuf.json 2> $O/axes_shuf.err || exit 1
