@@ -266,6 +266,32 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch,
                      const int64_t *out_offsets, pyas_partial *out,
                      void *stream);
 
+/* Compact per-output records (pyas_reduce_axes_ex): what storage.py:98-100
+ * returns per chunk for ONE method, with the sum rounded to the variable
+ * dtype as Active stores it in its `out` array (active.py:512,585).  A
+ * record is a value in the variable dtype -- the sum (PYAS_REC_SUM, for sum
+ * and mean; an integer sum wraps to the variable dtype), the min
+ * (PYAS_REC_MIN) or the max (PYAS_REC_MAX) -- and an int32 count:
+ * PYAS_REC_BYTES(itemsize) bytes, 8 for 1/2/4-byte dtypes (value in the low
+ * bytes of the first 4, count in the next 4), 16 for 8-byte dtypes (value,
+ * count, 4 zero bytes).  An all-zero record is neutral (count 0).  The
+ * combines read them with PYAS_COMBINE_REC(rec) in combine_flags, the
+ * zero-sign passes with PYAS_TIE_REC in `which`; their results are
+ * bit-identical to the 32-byte path with PYAS_COMBINE_ROUND_TO_VAR. */
+#define PYAS_REC_FULL 0    /* the 32-byte pyas_partial */
+#define PYAS_REC_SUM 1
+#define PYAS_REC_MIN 2
+#define PYAS_REC_MAX 3
+#define PYAS_REC_BYTES(itemsize) ((itemsize) <= 4 ? 8 : 16)
+#define PYAS_COMBINE_REC(rec) ((uint32_t)(rec) << 4)
+#define PYAS_TIE_REC 4u    /* which: parts are PYAS_REC_MIN (which 1) / _MAX (which 2) records */
+/* pyas_reduce_axes writing `rec` records (PYAS_REC_*; PYAS_REC_FULL is
+ * pyas_reduce_axes itself): out[out_offsets[c] + o] in record units.  A
+ * chunk's outputs must count < 2^31 elements each. */
+int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                        uint32_t axes_mask, int32_t rec, const int64_t *out_offsets, void *out,
+                        void *stream);
+
 /* method=None: decode + select + mask into dense row-major outputs.
  * values (device) receives native-endian elements, mask_out (device, may be
  * NULL) one byte per element (1 = masked); chunk c starts at element

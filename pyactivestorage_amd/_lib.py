@@ -123,6 +123,21 @@ class TieRule(ctypes.Structure):
     ]
 
 
+# compact per-output records of pyas_reduce_axes_ex (pyas.h PYAS_REC_*)
+REC_FULL, REC_SUM, REC_MIN, REC_MAX = 0, 1, 2, 3
+TIE_REC = 4
+
+
+def rec_nbytes(itemsize: int, rec: int) -> int:
+    """Bytes per output of a partial array of form ``rec``."""
+    return 32 if rec == REC_FULL else (8 if itemsize <= 4 else 16)
+
+
+def combine_rec(rec: int) -> int:
+    """PYAS_COMBINE_REC(rec): combine flag of record inputs."""
+    return int(rec) << 4
+
+
 PARTIAL_NBYTES = ctypes.sizeof(Partial)
 assert PARTIAL_NBYTES == 32
 
@@ -164,6 +179,7 @@ SIGNATURES = {
     "pyas_stream_wait": [_vp, _vp, _vp],
     "pyas_reduce_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _u32, _vp],
     "pyas_reduce_axes": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _u32, _vp, _vp, _vp],
+    "pyas_reduce_axes_ex": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _u32, _i32, _vp, _vp, _vp],
     "pyas_select_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), _vp, _vp, _vp, _vp],
     "pyas_select_scatter": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(Scatter),
                             _vp, _vp, _vp],

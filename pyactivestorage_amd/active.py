@@ -125,10 +125,11 @@ class _CachedQuery:
         if g["folded"]:
             engine.reduce_axes_grid(ctx, self.plan.batch, self.plan.mask_up.struct, g["g"], g["fin"].ptr,
                                     True, st)
-        else:
+        else:   # records of this replay's method (one size per dtype: the buffer fits every method)
+            g["rec"] = engine.method_rec(act._method)
             engine.reduce_axes(ctx, self.plan.batch, self.plan.mask_up.struct, g["axes_mask"], g["obuf"].ptr,
-                               g["parts"].ptr, st)
-            engine.combine_grid(ctx, act.ds.dtype, g["parts"].ptr, g["g"], g["fin"].ptr, True, st)
+                               g["parts"].ptr, st, rec=g["rec"])
+            engine.combine_grid(ctx, act.ds.dtype, g["parts"].ptr, g["g"], g["fin"].ptr, True, st, rec=g["rec"])
         act._tie_grid(ctx, st, self.plan, g)
         return act._format_device(ctx, st, g["fin"], g["n_final"], shape, bufs=self.fmt)
 
@@ -717,10 +718,11 @@ class Active:
             engine.tie_chunk_flags(ctx, plan.batch, plan.mask_up.struct, geom, rec["axes_mask"], which,
                                    rec["obuf"].ptr, rec["fin"].ptr, rec["n_final"], t["flags"].ptr, st)
             engine.tie_grid(ctx, dt, rec["g"], None, t["flags"].ptr, t["lr"], which, rec["fin"].ptr, keys_ptr, st)
-        else:
-            engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, geom, rec["axes_mask"], which,
+        else:   # per-chunk partials: compact records of the method (pyas_reduce_axes_ex)
+            pw = which | (_lib.TIE_REC if rec.get("rec") else 0)
+            engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, geom, rec["axes_mask"], pw,
                               rec["obuf"].ptr, rec["parts"].ptr, st)
-            engine.tie_grid(ctx, dt, rec["g"], rec["parts"].ptr, None, t["lr"], which, rec["fin"].ptr, keys_ptr,
+            engine.tie_grid(ctx, dt, rec["g"], rec["parts"].ptr, None, t["lr"], pw, rec["fin"].ptr, keys_ptr,
                             st)
 
     def _exchange(self, final, keys=None, lr=1):
@@ -829,17 +831,23 @@ class Active:
             except NotImplementedError:
                 pass   # geometry without the dense column or LDS row layout: two steps
         parts = None
+        prec = 0
         if not folded:
+            # per-chunk outputs as compact records of the method (storage.py:98-100
+            # per chunk, the sum rounded as active.py:512 stores it): 8 B per
+            # output for <= 4-byte dtypes instead of the 32-B partial
+            prec = engine.method_rec(self._method)
+            rb = _lib.rec_nbytes(dt.itemsize, prec)
             n_parts = top - base
-            parts = DeviceBuffer(ctx, max(n_parts + neutral, 1) * _lib.PARTIAL_NBYTES)
-            if neutral:
-                zeros = np.zeros(neutral * _lib.PARTIAL_NBYTES, dtype=np.uint8)
-                ctx.h2d(parts.ptr + n_parts * _lib.PARTIAL_NBYTES, zeros, st)
-            engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st)
-            engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st)
+            parts = DeviceBuffer(ctx, max(n_parts + neutral, 1) * rb)
+            if neutral:   # zero records: count 0, neutral in the combine
+                zeros = np.zeros(neutral * rb, dtype=np.uint8)
+                ctx.h2d(parts.ptr + n_parts * rb, zeros, st)
+            engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st, rec=prec)
+            engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st, rec=prec)
         ext = [tables["n_coords"][d] if d in axes else final_shape[d] for d in range(ds.ndim)]
         r = rec if rec is not None else {}
-        r.update(folded=folded, g=g, fin=fin, obuf=obuf, abuf=abuf, tbuf=tbuf, parts=parts,
+        r.update(folded=folded, g=g, fin=fin, obuf=obuf, abuf=abuf, tbuf=tbuf, parts=parts, rec=prec,
                  axes_mask=axes_mask, n_final=n_final,
                  tie={"lr": zerosign.grid_lr(ext, set(axes)), "n_parts": n_parts_all, "flags": None})
         if keys is not None and self._tie_which():
@@ -949,14 +957,16 @@ class Active:
         meta = np.concatenate([out_off[:-1], order, seg])
         mbuf = DeviceBuffer(ctx, meta.nbytes)
         ctx.h2d(mbuf.ptr, meta, st)
-        parts = DeviceBuffer(ctx, max(int(out_off[-1]), 1) * _lib.PARTIAL_NBYTES)
+        prec = engine.method_rec(self._method)   # compact per-output records (see _grid_partials)
+        parts = DeviceBuffer(ctx, max(int(out_off[-1]), 1) * _lib.rec_nbytes(dt.itemsize, prec))
         fin = DeviceBuffer(ctx, max(n_final, 1) * _lib.PARTIAL_NBYTES)
-        engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, mbuf.ptr, parts.ptr, st)
+        engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, mbuf.ptr, parts.ptr, st, rec=prec)
         engine.combine_segments(ctx, dt, parts.ptr, mbuf.ptr + 8 * len(chunk_list),
                                 mbuf.ptr + 8 * (len(chunk_list) + order.size), n_final, fin.ptr,
-                                True, st)
+                                True, st, rec=prec)
         which = self._tie_which()
         if which:   # NumPy's zero sign: per chunk output, then over each segment's layers
+            which |= _lib.TIE_REC
             engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, plan.tie_geom(), axes_mask, which, mbuf.ptr,
                               parts.ptr, st)
             ncoord = [len({cc[d] for cc, _ in chunk_list}) for d in range(ds.ndim)]

@@ -396,6 +396,8 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
     if (rc) return rc;
     if ((rc = check_geom(geom, batch->ndim))) return rc;
     const pyas::TieRule *t = tie_of(ctx, batch->dtype);
+    if ((which & PYAS_TIE_REC) && (which & 3u) != 1u && (which & 3u) != 2u)
+        return fail(PYAS_EINVAL, "PYAS_TIE_REC needs which 1 (min) or 2 (max)");
     if (!t || batch->n_chunks == 0 || (which & 3u) == 0) return PYAS_OK;
     const uint32_t full = (1u << batch->ndim) - 1u;
     if ((axes_mask & ~full) != 0) return fail(PYAS_EINVAL, "axes_mask 0x%x outside the chunk rank", axes_mask);
@@ -426,7 +428,7 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
     a.t = *t;
     a.g = *geom;
     a.axes = axes_mask;
-    a.which = which & 3u;
+    a.which = which & (3u | PYAS_TIE_REC);
     a.shuf = shuf;
     a.bswap = bsw;
     a.out_offsets = out_offsets;
@@ -547,7 +549,8 @@ int pyas_tie_grid(pyas_ctx *ctx, int32_t dtype, const pyas_grid *grid, const pya
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     if (!grid || !final_ || (!parts && !flags) || !grid->chunk_out_offsets)
         return fail(PYAS_EINVAL, "NULL argument");
-    if (which != 1u && which != 2u) return fail(PYAS_EINVAL, "which must be 1 (min) or 2 (max)");
+    if ((which & ~PYAS_TIE_REC) != 1u && (which & ~PYAS_TIE_REC) != 2u)
+        return fail(PYAS_EINVAL, "which must be 1 (min) or 2 (max), optionally | PYAS_TIE_REC");
     if (grid->ndim < 1 || grid->ndim > PYAS_MAX_DIMS) return fail(PYAS_EINVAL, "grid rank %d", grid->ndim);
     const pyas::TieRule *t = tie_of(ctx, dtype);
     if (!t) return PYAS_OK;
@@ -576,7 +579,8 @@ int pyas_tie_segments(pyas_ctx *ctx, int32_t dtype, const pyas_partial *parts, c
                       uint32_t which, pyas_partial *final_, uint64_t *keys, void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     if (!parts || !final_) return fail(PYAS_EINVAL, "NULL argument");
-    if (which != 1u && which != 2u) return fail(PYAS_EINVAL, "which must be 1 (min) or 2 (max)");
+    if ((which & ~PYAS_TIE_REC) != 1u && (which & ~PYAS_TIE_REC) != 2u)
+        return fail(PYAS_EINVAL, "which must be 1 (min) or 2 (max), optionally | PYAS_TIE_REC");
     if (!seg && (index || n_seg != 1)) return fail(PYAS_EINVAL, "seg NULL needs index NULL and one segment");
     if (n_layers < 0 || layer_base < 0) return fail(PYAS_EINVAL, "negative layer count or base");
     const pyas::TieRule *t = tie_of(ctx, dtype);
@@ -890,7 +894,14 @@ static void dense_geometry(pyas::AxesDense &d, const pyas_batch *b, uint32_t axe
 int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
                      uint32_t axes_mask, const int64_t *out_offsets, pyas_partial *out,
                      void *stream) {
+    return pyas_reduce_axes_ex(ctx, batch, mask, axes_mask, PYAS_REC_FULL, out_offsets, out, stream);
+}
+
+int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                        uint32_t axes_mask, int32_t rec, const int64_t *out_offsets, void *out,
+                        void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (rec < PYAS_REC_FULL || rec > PYAS_REC_MAX) return fail(PYAS_EINVAL, "unknown record form %d", rec);
     pyas::AxesArgs x;
     std::memset(&x, 0, sizeof(x));
     int es;
@@ -907,6 +918,9 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *ma
         if ((axes_mask >> d) & 1u) red_elems *= batch->chunk_shape[d];
         else keep_elems *= batch->chunk_shape[d];
     }
+    if (rec != PYAS_REC_FULL && red_elems >= (int64_t(1) << 31))
+        return fail(PYAS_ENOTSUP, "records count in int32: 2^31 or more reduced elements per output");
+    x.rec = rec;
     x.row = ((axes_mask >> (batch->ndim - 1)) & 1u) != 0;
     // 16-B vector walks: >= 4-byte unshuffled elements, no index tables, the
     // reduced offsets fit the LDS map and the last dim is whole 16-B vectors.
@@ -941,7 +955,7 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *ma
     x.axes = axes_mask;
     x.bpc = bpc;
     x.out_offsets = out_offsets;
-    x.out = out;
+    x.out = reinterpret_cast<pyas_partial *>(out);
     x.shuf = shuf;
     x.bswap = bsw;
     dense_geometry(x.d, batch, axes_mask, es, shuf ? es : 1, x.r.tab.on[0] || x.r.tab.on[1]);
@@ -1175,7 +1189,8 @@ int pyas_combine_segments(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
     if (n_segments < 0) return fail(PYAS_EINVAL, "negative segment count");
     if (n_segments == 0) return PYAS_OK;
     if (!in || !index || !seg_offsets || !out) return fail(PYAS_EINVAL, "NULL argument");
-    if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
+    // PYAS_COMBINE_REC: `in` holds compact records (pyas_reduce_axes_ex)
+    if (combine_flags & ~(PYAS_COMBINE_ROUND_TO_VAR | PYAS_COMBINE_REC(3)))
         return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
     PYAS_HIP(hipSetDevice(ctx->device));
     PYAS_HIP(pyas::launch_combine_segments(dtype, in, index, seg_offsets, n_segments, combine_flags,
@@ -1191,7 +1206,8 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, cons
     if (g->ndim < 1 || g->ndim > PYAS_MAX_DIMS)
         return fail(PYAS_EINVAL, "grid rank %d outside 1..%d", g->ndim, PYAS_MAX_DIMS);
     if (g->axes_mask >> g->ndim) return fail(PYAS_EINVAL, "axes mask 0x%x beyond rank %d", g->axes_mask, g->ndim);
-    if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
+    // PYAS_COMBINE_REC: `in` holds compact records (pyas_reduce_axes_ex)
+    if (combine_flags & ~(PYAS_COMBINE_ROUND_TO_VAR | PYAS_COMBINE_REC(3)))
         return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
     int64_t n_out = 1, n_layers = 1;
     for (int d = 0; d < g->ndim; ++d) {

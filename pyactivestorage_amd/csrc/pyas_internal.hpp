@@ -71,6 +71,7 @@ struct AxesArgs {
     int32_t group;                    // row layout: lanes per output (power of 2)
     int32_t split;                    // column layout: splits of the reduced range
     bool vec;                         // geometry admits 16-B vector walks (kernel re-checks per chunk)
+    int32_t rec;                      // per-chunk outputs: 0 pyas_partial, else a PYAS_REC_* record
 };
 
 // pyas_reduce_axes_grid: the chunk layers of a whole-chunk box query folded

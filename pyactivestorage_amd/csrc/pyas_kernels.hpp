@@ -391,6 +391,123 @@ __device__ __forceinline__ void merge(WAcc<T> &acc, const pyas_partial &p, bool 
     }
 }
 
+// ---------------------------------------------------------------------------
+// compact per-output records (pyas.h PYAS_REC_*): one method's value in the
+// variable dtype (the sum rounded as sum_of(round) rounds it) + int32 count
+// ---------------------------------------------------------------------------
+template <typename T> struct Rec {
+    static constexpr int kBytes = sizeof(T) <= 4 ? 8 : 16;
+};
+
+template <typename T>
+__device__ __forceinline__ int64_t out_bytes(int rec) {
+    return rec ? (int64_t)Rec<T>::kBytes : (int64_t)sizeof(pyas_partial);
+}
+
+// p as record `rec` (the first Rec<T>::kBytes bytes of the result)
+template <typename T>
+__device__ __forceinline__ uint4 rec_of(const pyas_partial &p, int rec) {
+    T v;
+    if (rec == PYAS_REC_SUM) v = (T)sum_of<T>(p.sum, true);
+    else v = TT<T>::from(rec == PYAS_REC_MIN ? p.min : p.max);
+    uint4 r = {0u, 0u, 0u, 0u};
+    if constexpr (sizeof(T) <= 4) {
+        __builtin_memcpy(&r.x, &v, sizeof(T));
+        r.y = (uint32_t)p.count;
+    } else {
+        __builtin_memcpy(&r.x, &v, 8);
+        r.z = (uint32_t)p.count;
+    }
+    return r;
+}
+
+// Entry i of a partial array of form `rec` as a pyas_partial (the fields a
+// record does not carry are 0: neutral for the method that reads it).
+template <typename T>
+__device__ __forceinline__ pyas_partial part_at(const void *base, int64_t i, int rec) {
+    if (rec == 0) return reinterpret_cast<const pyas_partial *>(base)[i];
+    pyas_partial p;
+    p.sum.u = 0;
+    p.min.u = 0;
+    p.max.u = 0;
+    T v;
+    if constexpr (sizeof(T) <= 4) {
+        const uint2 r = reinterpret_cast<const uint2 *>(base)[i];
+        __builtin_memcpy(&v, &r.x, sizeof(T));
+        p.count = (int64_t)(int32_t)r.y;
+    } else {
+        const uint4 r = reinterpret_cast<const uint4 *>(base)[i];
+        __builtin_memcpy(&v, &r.x, 8);
+        p.count = (int64_t)(int32_t)r.z;
+    }
+    if (rec == PYAS_REC_SUM) {
+        if constexpr (TT<T>::kind == 0) p.sum.f = (double)v;
+        else if constexpr (TT<T>::kind == 1) p.sum.i = (int64_t)v;
+        else p.sum.u = (uint64_t)v;
+    } else {
+        TT<T>::put(rec == PYAS_REC_MIN ? p.min : p.max, v);
+    }
+    return p;
+}
+
+// Output o of the per-chunk partial-axis kernels in the caller's form
+template <typename T>
+__device__ __forceinline__ void put_out(const AxesArgs &a, int64_t o, const pyas_partial &p) {
+    if (a.rec == 0) {
+        a.out[o] = p;
+        return;
+    }
+    const uint4 r = rec_of<T>(p, a.rec);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(a.out) + o * Rec<T>::kBytes;
+    if constexpr (Rec<T>::kBytes == 8) *reinterpret_cast<uint2 *>(dst) = make_uint2(r.x, r.y);
+    else *reinterpret_cast<uint4 *>(dst) = r;
+}
+
+// Staged writes of a tile's outputs: slot k of the LDS stage (uint4 array)
+// holds output k in the caller's form; stage_flush copies n of them to
+// outputs o0.. as consecutive non-temporal stores (16-B pieces where the
+// destination allows, else 8-B records).
+template <typename T>
+__device__ __forceinline__ void stage_put(const AxesArgs &a, uint4 *stage, int k, const pyas_partial &p) {
+    if (a.rec == 0) {
+        uint4 h[2];
+        __builtin_memcpy(h, &p, 32);
+        stage[k * 2] = h[0];
+        stage[k * 2 + 1] = h[1];
+    } else if constexpr (Rec<T>::kBytes == 16) {
+        stage[k] = rec_of<T>(p, a.rec);
+    } else {
+        const uint4 r = rec_of<T>(p, a.rec);
+        reinterpret_cast<uint2 *>(stage)[k] = make_uint2(r.x, r.y);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_flush(const AxesArgs &a, const uint4 *stage, int64_t o0, int64_t n,
+                                            int tid, int nthr) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const int64_t rb = out_bytes<T>(a.rec);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(a.out) + o0 * rb;
+    if (rb == 8 && ((o0 & 1) || (n & 1))) {      // odd record boundaries: 8-B pieces
+        const uint2 *s2 = reinterpret_cast<const uint2 *>(stage);
+        u32x2 *d2 = reinterpret_cast<u32x2 *>(dst);
+        for (int64_t q = tid; q < n; q += nthr) {
+            const uint2 h = s2[q];
+            u32x2 v = {h.x, h.y};
+            __builtin_nontemporal_store(v, d2 + q);
+        }
+        return;
+    }
+    u32x4 *d4 = reinterpret_cast<u32x4 *>(dst);
+    const int64_t nq = n * rb / 16;
+    for (int64_t q = tid; q < nq; q += nthr) {
+        const uint4 h = stage[q];
+        u32x4 v = {h.x, h.y, h.z, h.w};
+        __builtin_nontemporal_store(v, d4 + q);
+    }
+}
+
 // n partials -> one per block (contiguous segments), fixed order
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_combine(const pyas_partial *in, int64_t n, int64_t seg,
@@ -624,7 +741,8 @@ __global__ __launch_bounds__(kBlock) void k_combine_segments(const pyas_partial 
     const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
     WAcc<T> acc;
     acc.init();
-    for (int64_t k = seg[sidx]; k < seg[sidx + 1]; ++k) merge(acc, in[index[k]], round);
+    const int rec = (int)((flags >> 4) & 3u);   // PYAS_COMBINE_REC
+    for (int64_t k = seg[sidx]; k < seg[sidx + 1]; ++k) merge(acc, part_at<T>(in, index[k], rec), round);
     store_wpartial(out + sidx, acc);
 }
 
@@ -696,7 +814,7 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
         pyas_partial p[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (l0 + u < n_layers) p[u] = in[off[u] + j];
+            if (l0 + u < n_layers) p[u] = part_at<T>(in, off[u] + j, (int)((flags >> 4) & 3u));
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (l0 + u < n_layers) merge(acc, p[u], round);
@@ -785,7 +903,7 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid_wave(const pyas_partial
 #pragma unroll
         for (int u = 0; u < kCwTiles; ++u) {
             const int64_t l = l0 + u * kWave + lane;
-            if (l < n_layers) p[u] = in[off[u] + j];
+            if (l < n_layers) p[u] = part_at<T>(in, off[u] + j, (int)((flags >> 4) & 3u));
         }
 #pragma unroll
         for (int u = 0; u < kCwTiles; ++u) {
@@ -1045,7 +1163,11 @@ __device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_
 #pragma unroll
                 for (int k = 0; k < N; ++k) {
                     if (S > 1) fold_splits(acc[k], S, OT, ol, sp);
-                    if (sp == 0 && oi < n_items) tile_store_lane(acc[k], a.out + a.out_offsets[c] + oi * N + k);
+                    if (sp == 0 && oi < n_items) {
+                        pyas_partial pp;
+                        tile_store_lane(acc[k], &pp);
+                        put_out<T>(a, a.out_offsets[c] + oi * N + k, pp);
+                    }
                 }
                 continue;
             }
@@ -1061,7 +1183,11 @@ __device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_
                 }
             }
             if (S > 1) fold_splits(acc, S, OT, ol, sp);
-            if (sp == 0 && oi < n_items) tile_store_lane(acc, a.out + a.out_offsets[c] + oi);
+            if (sp == 0 && oi < n_items) {
+                pyas_partial pp;
+                tile_store_lane(acc, &pp);
+                put_out<T>(a, a.out_offsets[c] + oi, pp);
+            }
         }
     } else {
         // G lanes per output (host-sized for element or 16-B vector walks)
@@ -1112,7 +1238,9 @@ __device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_
                     axes_walk<T, 4, SHUF, BSWAP>(r, base, s, red, base_o, rc, gl, n_red, G, tabs, mk, acc);
                 }
             }
-            group_finish(acc, G, (o < n_out && gl == 0) ? a.out + a.out_offsets[c] + o : nullptr);
+            pyas_partial pp;
+            group_finish(acc, G, (o < n_out && gl == 0) ? &pp : nullptr);
+            if (o < n_out && gl == 0) put_out<T>(a, a.out_offsets[c] + o, pp);
         }
     }
 }
@@ -1581,7 +1709,7 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     const int IT = d.it, S = d.split;
     const int il = threadIdx.x & (IT - 1), sp = threadIdx.x / IT;
     const int64_t items = d.KO * (d.KI / N);
-    pyas_partial *out = a.out + a.out_offsets[c];
+    const int64_t ob = a.out_offsets[c];
     // aligned chunks: the ring walk (measured faster than the shuffled unit
     // exchange too); PYAS_COL_RING=0 builds the earlier walks
     constexpr bool ring = PYAS_COL_RING && AL;
@@ -1616,27 +1744,21 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
                 if (sp == 0) {
                     pyas_partial pp;
                     tile_store_lane(acc[k], &pp);
-                    uint4 h[2];
-                    __builtin_memcpy(h, &pp, 32);
-                    stage[(il * N + k) * 2] = h[0];
-                    stage[(il * N + k) * 2 + 1] = h[1];
+                    stage_put<T>(a, stage, il * N + k, pp);
                 }
             }
             __syncthreads();
-            const int64_t n_valid = ((items - i0 < IT) ? items - i0 : IT) * N * 2;   // uint4s
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 *dst = reinterpret_cast<u32x4 *>(out + i0 * N);
-            for (int64_t q = threadIdx.x; q < n_valid; q += kBlock) {
-                const uint4 h = stage[q];
-                u32x4 v = {h.x, h.y, h.z, h.w};
-                __builtin_nontemporal_store(v, dst + q);
-            }
+            stage_flush<T>(a, stage, ob + i0 * N, ((items - i0 < IT) ? items - i0 : IT) * N, threadIdx.x, kBlock);
             __syncthreads();
         } else {
 #pragma unroll
             for (int k = 0; k < N; ++k) {
                 if (S > 1) fold_splits(acc[k], S, IT, il, sp);
-                if (sp == 0 && i < items) tile_store_lane(acc[k], out + i * N + k);
+                if (sp == 0 && i < items) {
+                    pyas_partial pp;
+                    tile_store_lane(acc[k], &pp);
+                    put_out<T>(a, ob + i * N + k, pp);
+                }
             }
         }
     }
@@ -1656,7 +1778,7 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     const int64_t nwaves = d.bpc * (kBlock / kWave);
     const int64_t vstep = (int64_t)G * N * VPL * ES;             // bytes (plain layout)
     const int64_t wrap = (d.KO - 1) * d.RI * ES;                 // next run of the output
-    pyas_partial *out = a.out + a.out_offsets[c];
+    const int64_t ob = a.out_offsets[c];
     for (int64_t o0 = wave * P * UO; o0 < d.KO; o0 += nwaves * P * UO) {   // wave-uniform
         TileAcc<T> acc[UO];
 #pragma unroll
@@ -1709,7 +1831,11 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
             uint32_t cnt, nan;
             group_reduce(acc[u], G, cnt, nan);
             const int64_t o = o0 + u * P + pg;
-            if (gl == 0 && o < d.KO) store_group(acc[u], cnt, nan, out + o);
+            if (gl == 0 && o < d.KO) {
+                pyas_partial pp;
+                store_group(acc[u], cnt, nan, &pp);
+                put_out<T>(a, ob + o, pp);
+            }
         }
     }
 }
@@ -1738,7 +1864,7 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
     uint4 *t = tile + (threadIdx.x / kWave) * RPW * kRowLdsStride;
     const int64_t wave = j * (kBlock / kWave) + threadIdx.x / kWave;
     const int64_t nwaves = d.bpc * (kBlock / kWave);
-    pyas_partial *out = a.out + a.out_offsets[c];
+    const int64_t ob = a.out_offsets[c];
     // tile unit q = u * kWave + lane: vectors q*VPL .. +VPL-1, in run q*VPL / V
     int lrow[UL], lcol[UL];
 #pragma unroll
@@ -1787,22 +1913,10 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
         if (h == 0) {
             pyas_partial pp;
             store_group(acc, cnt, nan, &pp);
-            uint4 hv[2];
-            __builtin_memcpy(hv, &pp, 32);
-            t[r * 2] = hv[0];
-            t[r * 2 + 1] = hv[1];
+            stage_put<T>(a, t, r, pp);
         }
         wave_sync_lds();
-        {
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            const int nq = (int)(nvec / V) * 2;   // runs in this tile x 2 uint4
-            u32x4 *dst = reinterpret_cast<u32x4 *>(out + o0);
-            for (int q = lane; q < nq; q += kWave) {
-                const uint4 hv = t[q];
-                u32x4 x = {hv.x, hv.y, hv.z, hv.w};
-                __builtin_nontemporal_store(x, dst + q);
-            }
-        }
+        stage_flush<T>(a, t, ob + o0, nvec / V, lane, kWave);
         wave_sync_lds();
     }
 }
@@ -2362,8 +2476,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_c
         offs[v] = (ko * d.RI * d.KI + vv * N) * sizeof(T);
     }
     auto chunk_end = [&](int64_t cl, TileAcc<T> *acc) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        pyas_partial *cout = a.out + a.out_offsets[c0 + cl];
+        const int64_t cob = a.out_offsets[c0 + cl];
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             const int64_t iv = iw + v * kWave;
@@ -2372,19 +2485,11 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_c
             for (int k = 0; k < N; ++k) {
                 pyas_partial pp;
                 tile_store_lane(acc[v * N + k], &pp);
-                uint4 h[2];
-                __builtin_memcpy(h, &pp, 32);
-                ws[(lane * N + k) * 2] = h[0];
-                ws[(lane * N + k) * 2 + 1] = h[1];
+                stage_put<T>(a, ws, lane * N + k, pp);
                 acc[v * N + k].init();
             }
             wave_sync_lds();
-            u32x4 *dst = reinterpret_cast<u32x4 *>(cout + iv * N);
-            for (int64_t q = lane; q < nvv * 2 * N; q += nv) {
-                const uint4 h = ws[q];
-                u32x4 x = {h.x, h.y, h.z, h.w};
-                __builtin_nontemporal_store(x, dst + q);
-            }
+            stage_flush<T>(a, ws, cob + iv * N, nvv * N, lane, nv);
             wave_sync_lds();   // the area is rewritten next
         }
     };
@@ -2737,6 +2842,24 @@ __device__ __forceinline__ void tie_put(pyas_partial *p, uint32_t which, int sg)
     if ((which & 2u) && TT<T>::from(p->max) == (T)0) TT<T>::put(p->max, z);
 }
 
+// The form of level-1 partial arrays: PYAS_TIE_REC in `which` = records of
+// the queried method (pyas_reduce_axes_ex), else 32-byte partials.
+__device__ __forceinline__ int tie_rec(uint32_t which) {
+    return (which & PYAS_TIE_REC) ? ((which & 1u) ? PYAS_REC_MIN : PYAS_REC_MAX) : 0;
+}
+
+// tie_put on entry i of a partial array of form `rec` (a record's value is
+// the queried min or max itself)
+template <typename T>
+__device__ __forceinline__ void tie_put_at(void *parts, int64_t i, int rec, uint32_t which, int sg) {
+    if (rec == 0) {
+        tie_put<T>(reinterpret_cast<pyas_partial *>(parts) + i, which, sg);
+        return;
+    }
+    T *v = reinterpret_cast<T *>(reinterpret_cast<uint8_t *>(parts) + i * Rec<T>::kBytes);
+    if (*v == (T)0) *v = sg ? -(T)0 : (T)0;
+}
+
 // Group reductions over G consecutive lanes: G = 1 (none), 16 or 64 (inside
 // a wave, DPP/bpermute butterflies that never leave the group), kBlock (the
 // workgroup, through LDS; every thread of the block must call it).
@@ -2816,7 +2939,8 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
     // group-uniform from here; G == kBlock: NG == 1, so ol < n_out
     if (ol >= n_out) return;
     const int64_t ob = (a.out_offsets ? a.out_offsets[c] : c) + ol;
-    if (a.parts && !tie_zero<T>(a.parts[ob], a.which)) return;
+    const int rec = tie_rec(a.which);
+    if (a.parts && !tie_zero<T>(part_at<T>(a.parts, ob, rec), a.which)) return;
     int64_t vstride[PYAS_MAX_DIMS];
     {
         int64_t st = 1;
@@ -2855,7 +2979,9 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
         bool beyond = false;   // a kept coordinate outside the block is non-zero
 #pragma unroll
         for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-            if (d < r.ndim && !((a.axes >> d) & 1u)) {
+            if (d < r.ndim && ((a.axes >> d) & 1u) && cnt[d] == 1) {
+                base.mem += sel_index(s, r.pool, d, 0) * r.cstride[d];   // not a scan slot
+            } else if (d < r.ndim && !((a.axes >> d) & 1u)) {
                 const int64_t q = oo / cnt[d], k = oo - q * cnt[d];
                 oo = q;
                 if ((call.block >> d) & 1u) bidx += k * bw[d];
@@ -2955,7 +3081,7 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
     if (gl != 0) return;
     const int sg = tie_finalize(k1, kw, ka, call, a.t);
     if (a.parts) {
-        if (sg >= 0) tie_put<T>(a.parts + ob, a.which, sg);
+        if (sg >= 0) tie_put_at<T>(a.parts, ob, rec, a.which, sg);
     } else {
         a.flags[ob] = sg < 0 ? (uint8_t)0 : (uint8_t)(1u | ((unsigned)sg << 1));
     }
@@ -3057,7 +3183,7 @@ __global__ __launch_bounds__(kBlock) void k_tie_grid(TieGridArgs a) {
             zero = (b & 1u) != 0;
             sg = (b >> 1) & 1u;
         } else {
-            const pyas_partial p = a.parts[idx];
+            const pyas_partial p = part_at<T>(a.parts, idx, tie_rec(a.which));
             const T v = TT<T>::from((a.which & 1u) ? p.min : p.max);
             zero = p.count > 0 && v == (T)0;
             sg = __builtin_signbit(v) ? 1u : 0u;

@@ -134,10 +134,19 @@ def tie_finalize(ctx: Context, dt, keys_ptr, n_out: int, n_sets: int, lr: int, w
 
 
 def reduce_axes(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, axes_mask: int, out_offsets_ptr,
-                out_ptr, stream) -> None:
-    _lib.check(ctx.lib.pyas_reduce_axes(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
-                                        int(axes_mask), out_offsets_ptr, out_ptr, stream),
-               "pyas_reduce_axes")
+                out_ptr, stream, rec: int = 0) -> None:
+    """pyas_reduce_axes, or with ``rec`` (PYAS_REC_SUM/MIN/MAX) the compact
+    per-output records of pyas_reduce_axes_ex."""
+    _lib.check(ctx.lib.pyas_reduce_axes_ex(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
+                                           int(axes_mask), int(rec), out_offsets_ptr, out_ptr, stream),
+               "pyas_reduce_axes_ex")
+
+
+def method_rec(method) -> int:
+    """The record form a partial-axis query of ``method`` needs per chunk
+    output (storage.py:98-100): the rounded sum for sum/mean, else the min
+    or the max."""
+    return {"min": _lib.REC_MIN, "max": _lib.REC_MAX}.get(method, _lib.REC_SUM)
 
 
 def reduce_axes_grid(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, grid: _lib.Grid, out_ptr,
@@ -171,15 +180,16 @@ def combine_partials(ctx: Context, dt, in_ptr, n, out_ptr, round_to_var: bool, s
 
 
 def combine_segments(ctx: Context, dt, in_ptr, index_ptr, seg_ptr, n_seg, out_ptr, round_to_var: bool,
-                     stream) -> None:
-    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
+                     stream, rec: int = 0) -> None:
+    flags = (_lib.COMBINE_ROUND_TO_VAR if round_to_var else 0) | _lib.combine_rec(rec)
     _lib.check(ctx.lib.pyas_combine_segments(ctx.handle, dtype_code(dt), in_ptr, index_ptr, seg_ptr,
                                              int(n_seg), flags, out_ptr, stream),
                "pyas_combine_segments")
 
 
-def combine_grid(ctx: Context, dt, in_ptr, grid: _lib.Grid, out_ptr, round_to_var: bool, stream) -> None:
-    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
+def combine_grid(ctx: Context, dt, in_ptr, grid: _lib.Grid, out_ptr, round_to_var: bool, stream,
+                 rec: int = 0) -> None:
+    flags = (_lib.COMBINE_ROUND_TO_VAR if round_to_var else 0) | _lib.combine_rec(rec)
     _lib.check(ctx.lib.pyas_combine_grid(ctx.handle, dtype_code(dt), in_ptr, ctypes.byref(grid), flags,
                                          out_ptr, stream), "pyas_combine_grid")
 

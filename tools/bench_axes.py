@@ -80,22 +80,32 @@ def main():
         print(json.dumps({"workload": "c3 box query, chunk layers folded in-kernel (pyas_reduce_axes_grid)"
                           + (", byte-shuffled chunks" if shuffled else ""), "results": res}))
         return
+    # --rec sum|min|max: compact per-output records (pyas_reduce_axes_ex,
+    # 8 B per f32 output) instead of the 32-B partials
+    rec = 0
+    if "--rec" in sys.argv:
+        rec = {"sum": _lib.REC_SUM, "min": _lib.REC_MIN, "max": _lib.REC_MAX}[sys.argv[sys.argv.index("--rec") + 1]]
+    rb = _lib.rec_nbytes(4, rec)
     for axes in axis_sets:
         n_out = int(np.prod([1 if d in axes else chunks[d] for d in range(3)]))
-        out = DeviceBuffer(ctx, len(offsets) * n_out * _lib.PARTIAL_NBYTES)
+        out = DeviceBuffer(ctx, len(offsets) * n_out * rb)
         offs = torch.from_numpy(np.arange(len(offsets), dtype=np.int64) * n_out).to(dev)
         mask = 0
         for a in axes:
             mask |= 1 << a
         for _ in range(2):
-            engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, mask, offs.data_ptr(), out.ptr, st)
+            engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, mask, offs.data_ptr(), out.ptr, st, rec=rec)
         dt, dmin = timed(lambda: engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, mask,
-                                                    offs.data_ptr(), out.ptr, st))
+                                                    offs.data_ptr(), out.ptr, st, rec=rec))
+        wbytes = len(offsets) * n_out * rb
         res[str(axes)] = {"ms": round(dt * 1e3, 3), "ms_min": round(dmin * 1e3, 3),
-                          "GBps": round(nbytes / dt / 1e9, 1), "outputs_per_chunk": n_out}
+                          "GBps": round(nbytes / dt / 1e9, 1), "frac_read": round(nbytes / dt / 8e12, 4),
+                          "GBps_read_write": round((nbytes + wbytes) / dt / 1e9, 1),
+                          "outputs_per_chunk": n_out, "write_bytes": wbytes}
         del out
-    print(json.dumps({"workload": "c3 partial-axis per-chunk reduce_axes" + (", byte-shuffled chunks" if shuffled else ""),
-                      "results": res}))
+    print(json.dumps({"workload": "c3 partial-axis per-chunk reduce_axes" + (", byte-shuffled chunks" if shuffled else "")
+                      + (f", {sys.argv[sys.argv.index('--rec') + 1]} records ({rb} B per output)" if rec else
+                         ", 32-B partials"), "results": res}))
 
 
 if __name__ == "__main__":
