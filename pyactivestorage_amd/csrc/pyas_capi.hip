@@ -1001,6 +1001,30 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
             x.d.bpc = bpc;
         }
     }
+    // Shuffled chunks whose reduced rows lie inside each kept-outer block
+    // (RO == 1, e.g. C3 axis (1,)): k_axes_shuf_slab stages each block's
+    // byte-plane runs (RI x KI bytes per plane, whole 1 KiB loads) through
+    // LDS.  KI of 64 or 128 output columns, RB rows per 16 KiB tile.
+    // PYAS_SHUF_SLAB=0 (or a forced PYAS_COL_STREAM) keeps the column walks.
+    if (x.d.mode == 1 && shuf && !batch->sel && es >= 2 && x.d.RO == 1 && (x.d.KI == 64 || x.d.KI == 128) &&
+        !x.r.tab.on[0] && !x.r.tab.on[1]) {
+        const char *e = getenv("PYAS_SHUF_SLAB");   // per call: tests and benches switch it
+        int64_t rb = pyas::kSlabBytes / (x.d.KI * es);
+        if (rb > x.d.RI) rb = x.d.RI;
+        rb -= rb % 4;
+        const char *e_cs = getenv("PYAS_COL_STREAM");   // a forced column walk keeps that walk
+        if (!(e && *e == '0') && !(e_cs && *e_cs) && rb >= 4 && x.d.RI % rb == 0 && (rb * x.d.KI) % 1024 == 0) {
+            x.d.rb = rb;
+            x.d.cpb = 0;
+            x.d.n_chunks = batch->n_chunks;
+            // persistent waves: two 4-wave workgroups per CU (64 KiB of LDS each)
+            const int64_t units = batch->n_chunks * x.d.KO;
+            int64_t wgs = (int64_t)ctx->n_cu * 2;
+            if (wgs * (pyas::kBlock / pyas::kWave) > units) wgs = (units + 3) / 4;
+            PYAS_HIP(pyas::launch_axes_dense(batch->dtype, x, masked, wgs, (hipStream_t)stream));
+            return PYAS_OK;
+        }
+    }
     if (x.d.mode) {
         const int64_t g = (x.d.cpb > 0 ? (batch->n_chunks + x.d.cpb - 1) / x.d.cpb : batch->n_chunks) * x.d.bpc;
         if (g >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");

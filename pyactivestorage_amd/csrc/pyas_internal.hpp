@@ -47,6 +47,8 @@ constexpr int kAxesLds = 8192;   // reduced-index offsets kept in LDS (int32, 32
 
 // Dense partial-axis geometry (k_axes_dense): the chunk dims merged into
 // (RO, KO, RI, KI) = (reduced outer, kept outer, reduced inner, kept inner).
+constexpr int kSlabBytes = 16384;     // k_axes_shuf_slab: LDS tile per wave (plain elements)
+
 struct AxesDense {
     int32_t mode;                     // 0 off, 1 column, 2 row, 3 row with 4 outputs per lane,
                                       // 4/5/6 row through LDS with 1/2/4 lanes per output
@@ -56,7 +58,8 @@ struct AxesDense {
     int64_t bpc;                      // workgroups per chunk of the dense launch
     int64_t cpb;                      // column layout: chunks per workgroup of k_axes_col_stream (0: off)
     int32_t nv;                       // k_axes_col_stream: items per lane (1, 2 or 4)
-    int64_t n_chunks;                 // k_axes_col_stream: chunks in the batch
+    int64_t n_chunks;                 // k_axes_col_stream / k_axes_shuf_slab: chunks in the batch
+    int64_t rb;                       // k_axes_shuf_slab: rows per LDS tile (0: off)
 };
 
 struct AxesArgs {

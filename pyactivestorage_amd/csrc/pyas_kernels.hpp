@@ -2505,6 +2505,165 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_c
             d, r.chunk_elems, offs, 0, nc, mk, layer_base, acc, chunk_end);
 }
 
+// Shuffled chunks whose reduced rows sit inside each kept-outer block (dense
+// form RO == 1, e.g. axis (1,) of a 64^3 chunk): the block of kept-outer
+// index ko is RI x KI elements, contiguous in every byte plane (RI*KI bytes
+// per plane, 4 KiB for C3).  A wave streams one such slab (or RB rows of it)
+// with 16-B loads -- every load instruction reads 1 KiB of one plane, and
+// the slab's planes are 4 contiguous 4 KiB runs -- transposes each lane's
+// 16 elements out of the byte planes in registers (v_perm, as ldu does) and
+// writes them to its LDS tile in the plain layout; each lane then walks the
+// rows of its output columns ki = lane + 64 q from LDS in 4-row groups,
+// exactly col_rows_ring's arithmetic (same groups, order and counts), so the
+// partials equal dense_col's bit for bit.  The next slab's plane loads are
+// in flight (registers) while the current one is reduced from LDS.  Waves
+// are persistent: wave gw of TW takes units (chunk, ko) gw, gw + TW, ...
+// (adjacent waves read adjacent slabs).  Round 3's dword-plane walks ran this
+// geometry at 58 % of 8 TB/s: their loads are 64-B pieces of 4 rows.
+template <typename T, bool BSWAP, int MASKED, int KPL>
+__global__ __launch_bounds__(kBlock) void k_axes_shuf_slab(AxesArgs a) {
+    constexpr int ES = sizeof(T), MM = kSlabBytes / 1024 / ES;   // load steps per plane (max)
+    using U = typename TT<T>::U;
+    __shared__ uint4 tiles[kBlock / kWave][kSlabBytes / 16];
+    const AxesDense &d = a.d;
+    const ReduceArgs &r = a.r;
+    const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    const int64_t gw = (int64_t)blockIdx.x * (kBlock / kWave) + w;
+    const int64_t TW = (int64_t)gridDim.x * (kBlock / kWave);
+    const int64_t KI = d.KI, RI = d.RI, RB = d.rb, NS = RI / RB;
+    const int64_t n = r.chunk_elems;
+    const int M = (int)(RB * KI / 1024);                 // 16-B loads per lane per plane
+    const int64_t units = d.n_chunks * d.KO;
+    uint4 *tile = tiles[w];
+    const T *tv = reinterpret_cast<const T *>(tile);
+    MaskT<T> mk;
+    mk.init(r.mask);
+    uint4 pl[MM][ES];
+    bool al = true;
+    // issue the plane loads of sub-slab s of unit u (16-B pieces; AL per chunk)
+    auto load = [&](int64_t u, int64_t s) {
+        const int64_t c = u / d.KO, ko = u - c * d.KO;
+        const uint8_t *base = r.data + r.offsets[c];
+        al = ((((uintptr_t)base) | (uint64_t)n) & 15) == 0;    // wave-uniform
+        const int64_t e0 = (ko * RI + s * RB) * KI + 16 * lane;
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            if (m < M) {
+#pragma unroll
+                for (int b = 0; b < ES; ++b) {
+                    const uint8_t *q = base + b * n + e0 + m * 1024;
+                    pl[m][b] = al ? ld16<true>(q) : ld16<false>(q);
+                }
+            }
+        }
+    };
+    TileAcc<T> acc[KPL];
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) acc[q].init();
+    int64_t u = gw, s = 0;
+    if (u < units) load(u, 0);
+    while (u < units) {   // wave-uniform
+        // plane bytes -> plain elements (raw byte order) -> LDS
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            if (m < M) {
+                uint4 v[ES];
+                if constexpr (ES == 4) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        uint32_t e[4];
+                        transpose4(word(pl[m][0], j), word(pl[m][1], j), word(pl[m][2], j), word(pl[m][3], j), e);
+                        v[j] = make_uint4(e[0], e[1], e[2], e[3]);
+                    }
+                } else if constexpr (ES == 2) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const uint32_t a0 = word(pl[m][0], 2 * j), b0 = word(pl[m][1], 2 * j);
+                        const uint32_t a1 = word(pl[m][0], 2 * j + 1), b1 = word(pl[m][1], 2 * j + 1);
+                        v[j] = make_uint4(perm(b0, a0, 0x05010400u), perm(b0, a0, 0x07030602u),
+                                          perm(b1, a1, 0x05010400u), perm(b1, a1, 0x07030602u));
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        uint32_t lo[4], hi[4];
+                        transpose4(word(pl[m][0], j), word(pl[m][1], j), word(pl[m][2], j), word(pl[m][3], j), lo);
+                        transpose4(word(pl[m][4], j), word(pl[m][5], j), word(pl[m][6], j), word(pl[m][7], j), hi);
+                        v[2 * j] = make_uint4(lo[0], hi[0], lo[1], hi[1]);
+                        v[2 * j + 1] = make_uint4(lo[2], hi[2], lo[3], hi[3]);
+                    }
+                }
+#pragma unroll
+                for (int b = 0; b < ES; ++b) tile[(m * 64 + lane) * ES + b] = v[b];
+            }
+        }
+        wave_sync_lds();
+        const int64_t cu = u, cs = s;
+        if (++s == NS) {
+            s = 0;
+            u += TW;
+        }
+        if (u < units) load(u, s);   // the next slab's loads fly while this one is reduced
+        // rows of this sub-slab, output columns ki = lane + 64 q, 4-row groups
+        int64_t rr = 0;
+        for (; rr + 4 <= RB; rr += 4) {
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < KPL; ++q) {
+                T x[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    U raw;
+                    const T y = tv[(rr + k) * KI + q * 64 + lane];
+                    __builtin_memcpy(&raw, &y, ES);
+                    if (BSWAP) raw = bswap(raw);
+                    x[k] = bits_to<T>(raw);
+                }
+                bad |= acc[q].template add_lazy<4, MASKED, false>(x, mk);
+            }
+            if (__builtin_expect(__ballot(bad) != 0, 0)) {
+#pragma unroll
+                for (int q = 0; q < KPL; ++q) {
+                    T x[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        U raw;
+                        const T y = tv[(rr + k) * KI + q * 64 + lane];
+                        __builtin_memcpy(&raw, &y, ES);
+                        if (BSWAP) raw = bswap(raw);
+                        x[k] = bits_to<T>(raw);
+                    }
+                    acc[q].template check_nan<4>(x);
+                }
+            }
+        }
+        for (; rr < RB; ++rr) {   // a row tail (RB % 4): single rows, as col_rows does
+#pragma unroll
+            for (int q = 0; q < KPL; ++q) {
+                U raw;
+                const T y = tv[rr * KI + q * 64 + lane];
+                __builtin_memcpy(&raw, &y, ES);
+                if (BSWAP) raw = bswap(raw);
+                const T x = bits_to<T>(raw);
+                acc[q].template add_n<1, MASKED, false>(&x, mk);
+            }
+        }
+        if (cs == NS - 1) {   // the unit's last rows: its KPL * 64 outputs
+            const int64_t c = cu / d.KO, ko = cu - c * d.KO;
+            const int64_t ob = a.out_offsets[c] + ko * KI;
+#pragma unroll
+            for (int q = 0; q < KPL; ++q) {
+                if constexpr (!MASKED) acc[q].count += (uint32_t)RI;
+                pyas_partial pp;
+                tile_store_lane(acc[q], &pp);
+                put_out<T>(a, ob + q * 64 + lane, pp);
+                acc[q].init();
+            }
+        }
+        wave_sync_lds();   // the tile is rewritten next
+    }
+}
+
 // Whole-chunk box query, LDS row layout (modes 4/5/6), chunk layers folded
 // in the kernel (pyas_reduce_axes_grid).  Block (col, j), wave w owns the
 // output tiles j*4 + w, + 4*bpc, ... of kept-dims chunk column `col`; for
@@ -3439,9 +3598,33 @@ static void launch_col_stream(const AxesArgs &a, bool masked, dim3 gr, hipStream
     }
 }
 
+template <typename T, int KPL>
+static void launch_shuf_slab(const AxesArgs &a, bool masked, dim3 gr, hipStream_t st) {
+    const dim3 blk(kBlock);
+    const int mm = mask_mode(a.r.mask, masked);
+    if (a.bswap) {
+        if (mm) hipLaunchKernelGGL((k_axes_shuf_slab<T, true, kMaskAll, KPL>), gr, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_shuf_slab<T, true, 0, KPL>), gr, blk, 0, st, a);
+    } else if (mm == kMaskRange) {
+        hipLaunchKernelGGL((k_axes_shuf_slab<T, false, kMaskRange, KPL>), gr, blk, 0, st, a);
+    } else if (mm == kMaskNoEq1) {
+        hipLaunchKernelGGL((k_axes_shuf_slab<T, false, kMaskNoEq1, KPL>), gr, blk, 0, st, a);
+    } else {
+        if (mm) hipLaunchKernelGGL((k_axes_shuf_slab<T, false, kMaskAll, KPL>), gr, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_shuf_slab<T, false, 0, KPL>), gr, blk, 0, st, a);
+    }
+}
+
 template <typename T>
 hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st) {
     const dim3 g((unsigned)grid);
+    if constexpr (sizeof(T) >= 2) {
+        if (a.d.mode == 1 && a.d.rb > 0 && a.shuf) {   // k_axes_shuf_slab (host: RO == 1, whole chunks)
+            if (a.d.KI == 64) launch_shuf_slab<T, 1>(a, masked, g, st);
+            else launch_shuf_slab<T, 2>(a, masked, g, st);
+            return hipGetLastError();
+        }
+    }
     if constexpr (sizeof(T) >= 4) {
         if (a.d.mode == 1 && a.d.cpb > 0) {   // k_axes_col_stream (host: split 1, whole chunks)
             // host: shuffled chunks stream with one item per lane, plain

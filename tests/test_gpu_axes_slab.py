@@ -1,0 +1,44 @@
+"""``k_axes_shuf_slab``: shuffled chunks whose reduced rows lie inside each
+kept-outer block (dense form RO == 1, e.g. axis (1,) of a 64^3 chunk), staged
+block by block through LDS.  Its partials must equal the per-chunk column
+walk's (``dense_col``, ``PYAS_SHUF_SLAB=0 PYAS_COL_STREAM=0``) byte for byte:
+the same 4-row groups in the same order (``storage.py:95-104`` per chunk,
+before ``active.py:575-598`` folds them).  Covers 64 and 128 output columns,
+several tiles per block (RB < RI), f32/f64/i16 and big-endian data, every
+mask mode, NaN, chunk counts that leave waves idle, misaligned chunk
+offsets, and the compact records.
+"""
+import numpy as np
+import pytest
+
+from pyactivestorage_amd import _lib
+from tests.test_gpu_axes_stream import _chunks, _partials
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [((8, 64, 64), (1,)), ((4, 16, 64), (1,)), ((6, 128, 128), (1,)), ((4, 12, 128), (1,)),
+         ((3, 32, 64), (1,)), ((2, 8, 64, 64), (2,))]
+DTYPES = ["<f4", ">f4", "<f8", "<i2"]
+MISSING = [None, (-999, None, -50, 140), (None, None, -1e30, None), (-999, 77, None, None)]
+
+
+@pytest.mark.parametrize("misalign", [False, True])
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("geom", range(len(GEOMS)))
+def test_slab_equals_column_walk(gpu, monkeypatch, geom, dt, misalign):
+    from pyactivestorage_amd.device import get_context
+    shape, axes = GEOMS[geom]
+    dt = np.dtype(dt)
+    ctx = get_context(0)
+    st = ctx.thread_stream()
+    rng = np.random.default_rng(300 + 10 * geom + len(dt.str))
+    n = 5 if geom % 2 else 9
+    chunks = _chunks(dt, shape, n, rng, nan=True)
+    for mi, miss in enumerate(MISSING):
+        if miss is not None and dt.kind == "i":
+            miss = (7, None, -500, 900) if mi == 1 else None
+        monkeypatch.setenv("PYAS_SHUF_SLAB", "0")
+        want = _partials(ctx, st, dt, shape, chunks, axes, miss, True, misalign, 0, monkeypatch)
+        monkeypatch.setenv("PYAS_SHUF_SLAB", "1")
+        got = _partials(ctx, st, dt, shape, chunks, axes, miss, True, misalign, "", monkeypatch)
+        assert got.tobytes() == want.tobytes(), f"{dt} {shape} axes={axes} miss={mi} misalign={misalign}"

@@ -36,11 +36,14 @@ def main():
     ap.add_argument("--chunks", type=int, default=2048)
     ap.add_argument("--level", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host zlib pool size (0: every core this process may run on, os.sched_getaffinity)")
     ap.add_argument("--wbits", type=int, default=13, help="LDS history ring (13-15)")
     ap.add_argument("--no-check", action="store_true", help="timing experiments: skip status/output checks")
     ap.add_argument("--sweep", default="", help="comma list of stream counts: per-stream rate vs streams in flight")
     args = ap.parse_args()
+    if args.cpu_threads <= 0:
+        args.cpu_threads = len(os.sched_getaffinity(0))
     import torch
     from pyactivestorage_amd.device import DeviceBuffer, get_context
     from pyactivestorage_amd.inflate import InflateBatch, pack_streams
