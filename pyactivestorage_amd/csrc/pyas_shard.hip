@@ -10,6 +10,7 @@
 // exchange pyactivestorage_amd/distributed.py makes with torch.distributed
 // (one process per GPU); here a non-Python host that holds every device in
 // one process gets it through the C ABI.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -22,6 +23,40 @@
 
 namespace {
 
+// RCCL is opened on first use, not linked: a process that never shards does
+// not load it, and a process that already holds an RCCL (torch's, loaded by
+// `import torch`) shares that copy instead of loading a second one.
+struct Rccl {
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+int rccl(const Rccl *&out) {
+    static std::once_flag once;
+    static Rccl r;
+    static bool ok = false;
+    std::call_once(once, [] {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);   // already loaded?
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
+        r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+        r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+        r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+        r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+        r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+        ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.all_gather && r.error_string;
+    });
+    if (!ok) return pyas::set_error(PYAS_ENOTSUP, "RCCL (librccl.so.1) could not be loaded");
+    out = &r;
+    return PYAS_OK;
+}
+
 struct CommSet {
     std::vector<ncclComm_t> comms;   // comms[k] drives devices[k]
 };
@@ -29,21 +64,21 @@ struct CommSet {
 std::mutex g_mu;
 std::map<std::vector<int>, CommSet> g_comms;   // keyed by the device list, in order
 
-int nccl_fail(ncclResult_t r, const char *what) {
-    return pyas::set_error(PYAS_EDEVICE, "%s: %s", what, ncclGetErrorString(r));
+int nccl_fail(const Rccl *x, ncclResult_t r, const char *what) {
+    return pyas::set_error(PYAS_EDEVICE, "%s: %s", what, x->error_string(r));
 }
 
 // Communicators over `devs` (ncclCommInitAll: one rank per listed device,
 // rank k = devs[k]); created once per device list and kept until
 // pyas_shard_release().
-int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> &out) {
+int comms_for(const Rccl *x, const std::vector<int> &devs, std::vector<ncclComm_t> &out) {
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_comms.find(devs);
     if (it == g_comms.end()) {
         CommSet cs;
         cs.comms.resize(devs.size());
-        ncclResult_t r = ncclCommInitAll(cs.comms.data(), (int)devs.size(), devs.data());
-        if (r != ncclSuccess) return nccl_fail(r, "ncclCommInitAll");
+        ncclResult_t r = x->comm_init_all(cs.comms.data(), (int)devs.size(), devs.data());
+        if (r != ncclSuccess) return nccl_fail(x, r, "ncclCommInitAll");
         it = g_comms.emplace(devs, std::move(cs)).first;
     }
     out = it->second.comms;
@@ -79,21 +114,24 @@ int pyas_reduce_sharded(pyas_ctx *const *ctx, const pyas_batch *const *per_dev, 
         if (rc) return rc;
     }
     // 2. ONE all-gather of the 32-byte totals over xGMI, in place
-    std::vector<ncclComm_t> comms;
-    int rc = comms_for(devs, comms);
+    const Rccl *x = nullptr;
+    int rc = rccl(x);
     if (rc) return rc;
-    ncclResult_t r = ncclGroupStart();
-    if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
+    std::vector<ncclComm_t> comms;
+    rc = comms_for(x, devs, comms);
+    if (rc) return rc;
+    ncclResult_t r = x->group_start();
+    if (r != ncclSuccess) return nccl_fail(x, r, "ncclGroupStart");
     for (int k = 0; k < ndev; ++k) {
-        r = ncclAllGather(out[k] + 1 + k, out[k] + 1, sizeof(pyas_partial), ncclUint8, comms[k],
+        r = x->all_gather(out[k] + 1 + k, out[k] + 1, sizeof(pyas_partial), ncclUint8, comms[k],
                           (hipStream_t)streams[k]);
         if (r != ncclSuccess) {
-            ncclGroupEnd();
-            return nccl_fail(r, "ncclAllGather");
+            x->group_end();
+            return nccl_fail(x, r, "ncclAllGather");
         }
     }
-    r = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail(r, "ncclGroupEnd");
+    r = x->group_end();
+    if (r != ncclSuccess) return nccl_fail(x, r, "ncclGroupEnd");
     // 3. every device folds the totals in device order (the per-chunk sums
     //    were already rounded to the variable dtype under combine_flags)
     for (int k = 0; k < ndev; ++k) {
@@ -105,11 +143,14 @@ int pyas_reduce_sharded(pyas_ctx *const *ctx, const pyas_batch *const *per_dev, 
 
 int pyas_shard_release(void) {
     std::lock_guard<std::mutex> lk(g_mu);
-    int rc = PYAS_OK;
+    if (g_comms.empty()) return PYAS_OK;
+    const Rccl *x = nullptr;
+    int rc = rccl(x);
+    if (rc) return rc;
     for (auto &kv : g_comms)
         for (ncclComm_t c : kv.second.comms) {
-            ncclResult_t r = ncclCommDestroy(c);
-            if (r != ncclSuccess && rc == PYAS_OK) rc = nccl_fail(r, "ncclCommDestroy");
+            ncclResult_t r = x->comm_destroy(c);
+            if (r != ncclSuccess && rc == PYAS_OK) rc = nccl_fail(x, r, "ncclCommDestroy");
         }
     g_comms.clear();
     return rc;

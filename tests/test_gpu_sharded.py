@@ -19,12 +19,25 @@ from pyactivestorage_amd.device import DeviceBuffer, get_context
 pytestmark = pytest.mark.gpu
 
 MISSING = (np.float32(-999.0), None, np.float32(1000.0), np.float32(5e8))
+SHAPE, CHUNKS = (256, 128, 128), (64, 64, 64)
 
 
-def _data(torch, dev, chunk_range=None):
-    from pyactivestorage_amd.synthetic import chunk_major_device
-    return chunk_major_device(torch, (256, 256, 256), (64, 64, 64), np.float32, dev, chunk_range=chunk_range,
-                              fill=-999.0, fill_frac=0.01)
+def _data(ctx, st, lo=0, hi=None):
+    """Chunks [lo, hi) of a dummy_data-style variable with planted fill
+    values, uploaded with the library's own copies (this process's HIP
+    runtime belongs to libpyas_hip: no torch here)."""
+    from pyactivestorage_amd.device import DeviceBuffer
+    from pyactivestorage_amd.synthetic import chunk_major_host
+    buf, offsets = chunk_major_host(SHAPE, CHUNKS, np.float32)
+    vals = buf.view(np.float32).copy()
+    vals[np.random.default_rng(5).random(vals.size) < 0.01] = -999.0
+    cb = int(np.prod(CHUNKS)) * 4
+    hi = len(offsets) if hi is None else hi
+    part = vals.view(np.uint8)[lo * cb: hi * cb]
+    d = DeviceBuffer(ctx, max(part.nbytes, 16))
+    ctx.h2d(d.ptr, part, st)
+    ctx.synchronize(st)
+    return d, np.arange(hi - lo, dtype=np.int64) * cb
 
 
 def _arr(ctype, vals):
@@ -51,11 +64,9 @@ def _sharded(ctxs, plans, streams, flags=1):
 
 
 def test_one_device_equals_reduce_chunks(gpu):
-    import torch
-    dev = torch.device("cuda", 0)
-    data, offsets, _ = _data(torch, dev)
-    st = torch.cuda.current_stream().cuda_stream
-    plan = ReductionPlan(gpu, np.float32, (64, 64, 64), data.data_ptr(), offsets, missing=MISSING, stream=st)
+    st = gpu.thread_stream()
+    data, offsets = _data(gpu, st)
+    plan = ReductionPlan(gpu, np.float32, CHUNKS, data.ptr, offsets, missing=MISSING, stream=st)
     plan.launch(st, chunk_partials=False)
     want = plan.read_total(st)
     for _ in range(3):   # the communicator is created once and reused
@@ -68,11 +79,9 @@ def test_one_device_equals_reduce_chunks(gpu):
 def test_argument_errors(gpu):
     lib = gpu.lib
     assert lib.pyas_reduce_sharded(None, None, None, 0, 0, None, None) == _lib.EINVAL
-    import torch
-    dev = torch.device("cuda", 0)
-    data, offsets, _ = _data(torch, dev, chunk_range=(0, 4))
-    st = torch.cuda.current_stream().cuda_stream
-    plan = ReductionPlan(gpu, np.float32, (64, 64, 64), data.data_ptr(), offsets, missing=MISSING, stream=st)
+    st = gpu.thread_stream()
+    data, offsets = _data(gpu, st, 0, 4)
+    plan = ReductionPlan(gpu, np.float32, CHUNKS, data.ptr, offsets, missing=MISSING, stream=st)
     out = DeviceBuffer(gpu, 3 * _lib.PARTIAL_NBYTES)
     rc = lib.pyas_reduce_sharded(_arr(ctypes.c_void_p, [gpu.handle, gpu.handle]),
                                  _arr(ctypes.c_void_p, [ctypes.addressof(plan.batch)] * 2), None, 2, 0,
@@ -81,29 +90,25 @@ def test_argument_errors(gpu):
 
 
 def test_several_devices_equal_one(gpu):
-    import torch
-    n = torch.cuda.device_count()
-    if n < 2:
+    n = ctypes.c_int(0)
+    _lib.check(gpu.lib.pyas_device_count(ctypes.byref(n)), "pyas_device_count")
+    if n.value < 2:
         pytest.skip("one GPU visible: the ndev > 1 exchange runs on multi-GPU nodes only")
-    n_chunks = 64
     from pyactivestorage_amd.distributed import equal_ranges
+    n_chunks = int(np.prod([s // c for s, c in zip(SHAPE, CHUNKS)]))
     ctxs, plans, streams, keep = [], [], [], []
-    for k, (lo, hi) in enumerate(equal_ranges(n_chunks, n)):
-        dev = torch.device("cuda", k)
-        with torch.cuda.device(dev):
-            data, offsets, _ = _data(torch, dev, chunk_range=(lo, hi))
-            st = torch.cuda.current_stream(dev).cuda_stream
+    for k, (lo, hi) in enumerate(equal_ranges(n_chunks, n.value)):
         c = get_context(k)
-        plans.append(ReductionPlan(c, np.float32, (64, 64, 64), data.data_ptr(), offsets, missing=MISSING,
-                                   stream=st))
+        st = c.thread_stream()
+        data, offsets = _data(c, st, lo, hi)
+        plans.append(ReductionPlan(c, np.float32, CHUNKS, data.ptr, offsets, missing=MISSING, stream=st))
         ctxs.append(c)
         streams.append(st)
         keep.append(data)
     res = _sharded(ctxs, plans, streams)
-    dev0 = torch.device("cuda", 0)
-    data, offsets, _ = _data(torch, dev0)
-    st0 = torch.cuda.current_stream(dev0).cuda_stream
-    one = ReductionPlan(gpu, np.float32, (64, 64, 64), data.data_ptr(), offsets, missing=MISSING, stream=st0)
+    st0 = gpu.thread_stream()
+    data, offsets = _data(gpu, st0)
+    one = ReductionPlan(gpu, np.float32, CHUNKS, data.ptr, offsets, missing=MISSING, stream=st0)
     one.launch(st0, chunk_partials=False)
     want = one.read_total(st0)[0]
     for r in res:
