@@ -1006,8 +1006,11 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
     // byte-plane runs (RI x KI bytes per plane, whole 1 KiB loads) through
     // LDS.  KI of 64 or 128 output columns, RB rows per 16 KiB tile.
     // PYAS_SHUF_SLAB=0 (or a forced PYAS_COL_STREAM) keeps the column walks.
+    // Split 1 only (one lane set walks all rows): the same 4-row groups in the
+    // same order as dense_col / k_axes_col_stream / k_axes_fold_lean, so the
+    // partials stay bit-identical to theirs.
     if (x.d.mode == 1 && shuf && !batch->sel && es >= 2 && x.d.RO == 1 && (x.d.KI == 64 || x.d.KI == 128) &&
-        !x.r.tab.on[0] && !x.r.tab.on[1]) {
+        x.d.split == 1 && !x.r.tab.on[0] && !x.r.tab.on[1]) {
         const char *e = getenv("PYAS_SHUF_SLAB");   // per call: tests and benches switch it
         int64_t rb = pyas::kSlabBytes / (x.d.KI * es);
         if (rb > x.d.RI) rb = x.d.RI;

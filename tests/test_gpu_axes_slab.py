@@ -16,8 +16,10 @@ from tests.test_gpu_axes_stream import _chunks, _partials
 
 pytestmark = pytest.mark.gpu
 
-GEOMS = [((8, 64, 64), (1,)), ((4, 16, 64), (1,)), ((6, 128, 128), (1,)), ((4, 12, 128), (1,)),
-         ((3, 32, 64), (1,)), ((2, 8, 64, 64), (2,))]
+# >= 256 column items per chunk (the column layout's split 1, which the
+# slab kernel requires): KO * KI / (16 / itemsize) >= 256
+GEOMS = [((16, 64, 64), (1,)), ((32, 16, 64), (1,)), ((8, 128, 128), (1,)), ((8, 12, 128), (1,)),
+         ((24, 32, 64), (1,)), ((4, 4, 64, 64), (2,))]
 DTYPES = ["<f4", ">f4", "<f8", "<i2"]
 MISSING = [None, (-999, None, -50, 140), (None, None, -1e30, None), (-999, 77, None, None)]
 

@@ -29,3 +29,4 @@ for lib in new before; do
   if [ $lib = before ]; then export PYAS_LIB=$R/pyactivestorage_amd/lib/before/libpyas_before.so; else unset PYAS_LIB; fi
   timeout -k 10 300 python -u tools/bench_inflate.py --sweep 1,8,30,256 > $O/inflate_bench_$lib.json 2> $O/inflate_bench_$lib.err || exit 1
 done
+PYAS_LIB=$R/pyactivestorage_amd/lib/before/libpyas_prof.so timeout -k 10 300 python -u tools/bench_inflate.py --chunks 64 --reps 1 --no-check > $O/inflate_phase_profile.txt 2>&1 || exit 1
