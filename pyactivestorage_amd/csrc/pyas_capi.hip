@@ -418,13 +418,16 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
         const int d = geom->perm[i];
         if (batch->chunk_shape[d] != 1) inner_kept = ((axes_mask >> d) & 1u) ? 0 : 1;
     }
-    int group = inner_kept == 1 ? 1 : red >= 16384 ? pyas::kBlock : red >= 1024 ? 64 : 16;
+    // (a full reduction: a wave per chunk, four chunks per workgroup)
+    int group = kept == 1 ? pyas::kWave : inner_kept == 1 ? 1 : red >= 1024 ? pyas::kWave : 16;
     const char *e_group = getenv("PYAS_TIE_GROUP");   // per call: tests force each layout
     if (e_group && *e_group) {
         const int g = atoi(e_group);
-        if (g == 1 || g == 16 || g == 64 || g == pyas::kBlock) group = g;
+        if (g == 1 || g == 16 || g == pyas::kWave) group = g;
     }
     a.group = group;
+    a.n_chunks = batch->n_chunks;
+    a.cpw = (kept == 1 && group == pyas::kWave) ? pyas::kBlock / pyas::kWave : 1;
     a.t = *t;
     a.g = *geom;
     a.axes = axes_mask;
@@ -435,9 +438,7 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
     a.parts = partials;
     a.flags = flags;
     a.gate = gate;
-    const int64_t per_wg = pyas::kBlock / group;   // outputs per workgroup
-    a.tpc = (kept + per_wg - 1) / per_wg;
-    const int64_t grid = batch->n_chunks * a.tpc;
+    const int64_t grid = (batch->n_chunks + a.cpw - 1) / a.cpw;   // a workgroup per chunk (or per cpw)
     if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "tie grid too large");
     PYAS_HIP(hipSetDevice(ctx->device));
     PYAS_HIP(pyas::launch_tie_chunks(batch->dtype, a, grid, st));
@@ -495,6 +496,8 @@ int tie_level2(pyas_ctx *ctx, int32_t dtype, pyas::TieGridArgs &a, int64_t max_l
         if (slices > cap) slices = cap;
     }
     a.slices = slices;
+    // few layers per output (<= 64) and many outputs: a thread per output
+    a.per_thread = (max_layers <= pyas::kWave && a.n_out >= 4096) ? 1 : 0;
     if ((a.n_out * slices) / (pyas::kBlock / pyas::kWave) >= (int64_t(1) << 31))
         return fail(PYAS_ENOTSUP, "tie grid too large");
     PYAS_HIP(hipSetDevice(ctx->device));

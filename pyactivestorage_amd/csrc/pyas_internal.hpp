@@ -164,8 +164,9 @@ struct TieChunkArgs {
     pyas_partial *parts;              // rewrite mode, or NULL and:
     uint8_t *flags;                   //   flag mode (one byte per chunk output)
     const uint32_t *gate;             //   flag mode: skip when *gate == 0
-    int64_t tpc;                      // output tiles per chunk (kBlock / group outputs each)
-    int32_t group;                    // lanes per output: 1, 16, 64 or kBlock (k_tie_scan)
+    int64_t n_chunks;
+    int32_t cpw;                      // chunks per workgroup: 1, or a wave per chunk (one output each)
+    int32_t group;                    // lanes per output: 1, 16 or 64 (k_tie_scan)
 };
 struct TieGridArgs {
     pyas_grid g;                      // kind 0: layers from the grid tables
@@ -176,6 +177,7 @@ struct TieGridArgs {
     pyas_partial *fin;
     uint64_t *keys;
     int64_t n_out, n_layers, layer_base, slices;
+    int32_t per_thread;               // k_tie_grid_t: a thread per output (few layers, many outputs)
     TieCall call;
     TieRule t;
     uint32_t which;

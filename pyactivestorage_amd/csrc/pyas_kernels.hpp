@@ -3019,39 +3019,61 @@ __device__ __forceinline__ void tie_put_at(void *parts, int64_t i, int rec, uint
     if (*v == (T)0) *v = sg ? -(T)0 : (T)0;
 }
 
-// Group reductions over G consecutive lanes: G = 1 (none), 16 or 64 (inside
-// a wave, DPP/bpermute butterflies that never leave the group), kBlock (the
-// workgroup, through LDS; every thread of the block must call it).
+// Group reductions over G consecutive lanes of a wave (G = 1: none; 16 or
+// 64: DPP/bpermute butterflies that never leave the group).
 template <int G>
-__device__ __forceinline__ uint64_t grp_max_u64(uint64_t v, uint64_t *lds) {
-    if constexpr (G == 1) {
-        return v;
-    } else if constexpr (G <= kWave) {
+__device__ __forceinline__ uint64_t grp_max_u64(uint64_t v) {
+    static_assert(G == 1 || G == 16 || G == kWave, "lanes per output: 1, 16 or a wave");
 #pragma unroll
-        for (int m = G / 2; m >= 1; m >>= 1) {
-            const uint64_t o = shfl_xor(v, m);
-            v = o > v ? o : v;
-        }
-        return v;
-    } else {
-        static_assert(G == kBlock, "group = lanes of a wave or the workgroup");
-#pragma unroll
-        for (int m = kWave / 2; m >= 1; m >>= 1) {
-            const uint64_t o = shfl_xor(v, m);
-            v = o > v ? o : v;
-        }
-        __syncthreads();
-        if ((threadIdx.x & (kWave - 1)) == 0) lds[threadIdx.x / kWave] = v;
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < kBlock / kWave; ++i) v = lds[i] > v ? lds[i] : v;
-        return v;
+    for (int m = G / 2; m >= 1; m >>= 1) {
+        const uint64_t o = shfl_xor(v, m);
+        v = o > v ? o : v;
     }
+    return v;
 }
 
 template <int G>
-__device__ __forceinline__ uint64_t grp_min_u64(uint64_t v, uint64_t *lds) {
-    return ~grp_max_u64<G>(~v, lds);
+__device__ __forceinline__ uint64_t grp_min_u64(uint64_t v) {
+    return ~grp_max_u64<G>(~v);
+}
+
+// tie_keys in 32-bit arithmetic: every position, call length and piece of a
+// chunk output is < 2^31 (pyas_tie_chunks checks the reduced count).
+__device__ __forceinline__ void tie_keys32(uint32_t e, uint64_t sg, const TieCall &c, const TieRule &t, bool lanes,
+                                           uint64_t &k1, uint64_t &w, uint64_t &ka) {
+    k1 = 0;
+    w = kTieWNone;
+    ka = 0;
+    const bool acc = c.acc && !lanes;
+    if (e == 0) {
+        if (acc) ka = 2u | sg;
+        else {
+            k1 = 2u | sg;
+            w = sg;
+        }
+        return;
+    }
+    const uint32_t P = (uint32_t)t.piece, lr = (uint32_t)c.lr;
+    const uint32_t q = e / lr, pos = e - q * lr;
+    const uint32_t k = pos / P;
+    const uint32_t s0 = (q == 0 && k == 0) ? 1u : k * P;
+    const uint32_t e1 = (k + 1) * P < lr ? (k + 1) * P : lr;
+    const uint32_t m = e1 - s0, off = pos - s0;
+    const uint64_t row1 = (uint64_t)q * (uint64_t)c.npr + k + 1;
+    if (acc) {
+        const uint32_t A = (uint32_t)t.acc;
+        const uint32_t nv = m - m % A;
+        const bool vec = off < nv;
+        const uint64_t prio = vec ? (uint64_t)(t.acc - 1 - t.acc_rank[off % A]) : 0u;
+        ka = (row1 << 33) | ((uint64_t)(vec ? 0 : 1) << 32) | (prio << 25) | ((uint64_t)off << 1) | sg;
+        return;
+    }
+    const uint32_t L = (uint32_t)t.lanes;
+    const uint32_t nv = m - m % L;
+    const bool vec = off < nv;
+    const uint32_t rank = vec ? (uint32_t)t.rank[off % L] : kTieRemRank;
+    k1 = (!vec || rank == 0) ? ((((uint64_t)e + 1) << 1) | sg) : 0u;
+    w = (row1 << 32) | ((uint64_t)rank << 25) | ((uint64_t)(((uint32_t)1 << kTieOffBits) - 1 - off) << 1) | sg;
 }
 
 // Level 1 (storage.py:99-100 over chunk[sel]): the sign NumPy gives each zero
@@ -3068,20 +3090,35 @@ __device__ __forceinline__ uint64_t grp_min_u64(uint64_t v, uint64_t *lds) {
 // step holding the first significant zero, or once it has finished the row of
 // the first strided zero; only an output with neither is scanned to e = 0, and
 // then its keys are complete.  tie_finalize of the scanned suffix's keys
-// equals that of all keys (zerosign.finalize; tests compare with NumPy).
+// equals that of all keys (zerosign.predict_scan; tests compare with NumPy).
 // G lanes share an output (1: one output per lane, for elementwise calls,
-// where adjacent lanes hold adjacent outputs), NG = kBlock/G outputs per
-// workgroup.  Rewrite mode (parts): outputs whose min/max is a zero get
-// NumPy's sign.  Flag mode (flags): one byte per chunk output, bit 0 an
-// unmasked zero, bit 1 the winning zero's sign; skipped when *gate == 0.
+// where adjacent lanes hold adjacent outputs).  A workgroup takes one chunk
+// and loops over its outputs, kBlock / G at a time, so the chunk's setup
+// (selection, call structure, visiting order) is paid once per chunk; when
+// every chunk has one output (a full reduction), each wave takes a chunk
+// (a.cpw = kBlock / kWave chunks per workgroup).  Rewrite mode (parts):
+// outputs whose min/max is a zero get NumPy's sign.  Flag mode (flags): one
+// byte per chunk output, bit 0 an unmasked zero, bit 1 the winning zero's
+// sign; skipped when *gate == 0.
 template <typename T, int G>
 __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
     constexpr int NG = kBlock / G;
-    constexpr int V = G >= kWave ? 4 : 1;     // elements per lane per step
-    __shared__ uint64_t lds[kBlock / kWave];
+    constexpr int V = G == kWave ? 4 : 1;     // elements per lane per step
     const ReduceArgs &r = a.r;
     if (a.gate && *a.gate == 0u) return;
-    const int64_t c = (int64_t)blockIdx.x / a.tpc, tile = (int64_t)blockIdx.x - c * a.tpc;
+    const int grp = (int)threadIdx.x / G, gl = (int)threadIdx.x % G;
+    int64_t c, o_first, o_step;
+    if (a.cpw > 1) {   // one output per chunk, a wave per chunk (host: G == kWave)
+        c = (int64_t)blockIdx.x * a.cpw + threadIdx.x / kWave;
+        o_first = 0;
+        o_step = 1;
+        if (c >= a.n_chunks) return;   // wave-uniform
+    } else {
+        c = blockIdx.x;
+        o_first = grp;
+        o_step = NG;
+    }
+    const int rec = tie_rec(a.which);
     Sel s;
     load_sel(s, r.sel, c, r.ndim, r.shape);
     int64_t cnt[PYAS_MAX_DIMS];
@@ -3092,14 +3129,7 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
         if ((a.axes >> d) & 1u) R *= cnt[d];
         else n_out *= cnt[d];
     }
-    if (n_out == 0 || R == 0 || tile * NG >= n_out) return;   // block-uniform
-    const int grp = (int)threadIdx.x / G, gl = (int)threadIdx.x % G;
-    const int64_t ol = tile * NG + grp;
-    // group-uniform from here; G == kBlock: NG == 1, so ol < n_out
-    if (ol >= n_out) return;
-    const int64_t ob = (a.out_offsets ? a.out_offsets[c] : c) + ol;
-    const int rec = tie_rec(a.which);
-    if (a.parts && !tie_zero<T>(part_at<T>(a.parts, ob, rec), a.which)) return;
+    if (n_out == 0 || R == 0) return;   // uniform per chunk
     int64_t vstride[PYAS_MAX_DIMS];
     {
         int64_t st = 1;
@@ -3119,12 +3149,8 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
     }
     const TieCall call = tie_call(cnt, vstride, a.axes, a.g.perm, r.ndim, (a.g.flags & PYAS_TIE_BUFFERED) != 0,
                                   a.t.piece);
-    // the output's kept coordinates: memory / table base, and whether its
-    // first run is a copied (contiguous) call of a strided reduction
-    Decomp base{0, {0, 0}};
-    bool olanes = false;
+    int64_t bw[PYAS_MAX_DIMS];   // kept-block weights (NumPy's copied first fill), inner first
     {
-        int64_t bw[PYAS_MAX_DIMS];   // kept-block weights (NumPy's copied first fill), inner first
         int64_t st = 1;
 #pragma unroll
         for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
@@ -3134,25 +3160,9 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
                 if ((call.block >> d) & 1u) st *= cnt[d];
             }
         }
-        int64_t oo = ol, bidx = 0;
-        bool beyond = false;   // a kept coordinate outside the block is non-zero
-#pragma unroll
-        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-            if (d < r.ndim && ((a.axes >> d) & 1u) && cnt[d] == 1) {
-                base.mem += sel_index(s, r.pool, d, 0) * r.cstride[d];   // not a scan slot
-            } else if (d < r.ndim && !((a.axes >> d) & 1u)) {
-                const int64_t q = oo / cnt[d], k = oo - q * cnt[d];
-                oo = q;
-                if ((call.block >> d) & 1u) bidx += k * bw[d];
-                else beyond |= k != 0;
-                base.mem += sel_index(s, r.pool, d, k) * r.cstride[d];
-                base.v[0] += k * r.tab.stride[0][d];
-                base.v[1] += k * r.tab.stride[1][d];
-            }
-        }
-        olanes = call.n_copy && !beyond && bidx < call.n_copy;
     }
-    // reduced dims in visiting order, innermost first (slot i = perm[nd-1-i])
+    // reduced dims in visiting order, innermost first (slot i = perm[nd-1-i]);
+    // reduced dims of one selected index only offset the base
     uint32_t rc[PYAS_MAX_DIMS];
     int32_t rst[PYAS_MAX_DIMS], rsp[PYAS_MAX_DIMS];
     int64_t rcs[PYAS_MAX_DIMS], rt0[PYAS_MAX_DIMS], rt1[PYAS_MAX_DIMS];
@@ -3177,72 +3187,104 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
             }
         }
     }
+    int64_t base_red = 0;   // reduced dims of extent 1 (not scan slots)
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+        if (d < r.ndim && ((a.axes >> d) & 1u) && cnt[d] == 1) base_red += sel_index(s, r.pool, d, 0) * r.cstride[d];
     MaskT<T> mk;
     mk.init(r.mask);
     const uint8_t *data = r.data + r.offsets[c];
-    uint64_t k1 = 0, kw = kTieWNone, ka = 0, stop1 = 0;   // stop1 = scan floor + 1 (0: none yet)
-    int64_t hi = R;
-    while (hi > 0 && (int64_t)stop1 - 1 < hi) {           // group-uniform
-        const int64_t lo = hi - (int64_t)G * V;
-        T x[V];
-        Decomp o[V];
+    const int64_t obase = a.out_offsets ? a.out_offsets[c] : c;
+    for (int64_t ol = o_first; ol < n_out; ol += o_step) {   // group-uniform
+        const int64_t ob = obase + ol;
+        if (a.parts && !tie_zero<T>(part_at<T>(a.parts, ob, rec), a.which)) continue;
+        // the output's kept coordinates: memory / table base, and whether its
+        // first run is a copied (contiguous) call of a strided reduction
+        Decomp base{base_red, {0, 0}};
+        bool olanes = false;
+        {
+            int64_t oo = ol, bidx = 0;
+            bool beyond = false;   // a kept coordinate outside the block is non-zero
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-            const int64_t e = lo + (int64_t)gl * V + j;
-            o[j] = base;
-            x[j] = (T)1;
-            if (e >= 0) {
-                uint32_t rr = (uint32_t)e;
+            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+                if (d < r.ndim && !((a.axes >> d) & 1u)) {
+                    const int64_t q = oo / cnt[d], k = oo - q * cnt[d];
+                    oo = q;
+                    if ((call.block >> d) & 1u) bidx += k * bw[d];
+                    else beyond |= k != 0;
+                    base.mem += sel_index(s, r.pool, d, k) * r.cstride[d];
+                    base.v[0] += k * r.tab.stride[0][d];
+                    base.v[1] += k * r.tab.stride[1][d];
+                }
+            }
+            olanes = call.n_copy && !beyond && bidx < call.n_copy;
+        }
+        uint64_t k1 = 0, kw = kTieWNone, ka = 0, stop1 = 0;   // stop1 = scan floor + 1 (0: none yet)
+        int64_t hi = R;
+        while (hi > 0 && (int64_t)stop1 - 1 < hi) {           // group-uniform
+            const int64_t lo = hi - (int64_t)G * V;
+            T x[V];
+            Decomp o[V];
 #pragma unroll
-                for (int i = 0; i < PYAS_MAX_DIMS; ++i) {
-                    if (i < nr) {
-                        const uint32_t q = rr / rc[i], k = rr - q * rc[i];
-                        rr = q;
-                        const int64_t idx = rsp[i] != 0 ? (int64_t)rst[i] + (int64_t)k * rsp[i]
-                                                        : (int64_t)r.pool[(int64_t)rst[i] + k];
-                        o[j].mem += idx * rcs[i];
-                        o[j].v[0] += (int64_t)k * rt0[i];
-                        o[j].v[1] += (int64_t)k * rt1[i];
+            for (int j = 0; j < V; ++j) {   // lanes of a load adjacent in e
+                const int64_t e = lo + (int64_t)j * G + gl;
+                o[j] = base;
+                x[j] = (T)1;
+                if (e >= 0) {
+                    uint32_t rr = (uint32_t)e;
+#pragma unroll
+                    for (int i = 0; i < PYAS_MAX_DIMS; ++i) {
+                        if (i < nr) {
+                            const uint32_t q = rr / rc[i], k = rr - q * rc[i];
+                            rr = q;
+                            const int64_t idx = rsp[i] != 0 ? (int64_t)rst[i] + (int64_t)k * rsp[i]
+                                                            : (int64_t)r.pool[(int64_t)rst[i] + k];
+                            o[j].mem += idx * rcs[i];
+                            o[j].v[0] += (int64_t)k * rt0[i];
+                            o[j].v[1] += (int64_t)k * rt1[i];
+                        }
                     }
+                    x[j] = load_elem_rt<T>(data, r.chunk_elems, o[j].mem, a.shuf, a.bswap);
                 }
-                x[j] = load_elem_rt<T>(data, r.chunk_elems, o[j].mem, a.shuf, a.bswap);
             }
-        }
-        uint64_t thr1 = 0;
+            uint64_t thr1 = 0;
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-            const int64_t e = lo + (int64_t)gl * V + j;
-            if (e >= 0 && x[j] == (T)0 && !all_masked(mk, r.tab, o[j], x[j])) {
-                const bool lanes = olanes && e < call.lr;
-                uint64_t x1, xw, xa;
-                tie_keys(e, __builtin_signbit(x[j]) ? 1u : 0u, call, a.t, lanes, x1, xw, xa);
-                k1 = x1 > k1 ? x1 : k1;
-                kw = xw < kw ? xw : kw;
-                ka = xa > ka ? xa : ka;
-                int64_t thr = -1;
-                if (call.acc && !lanes) {          // finish this zero's row
-                    const int64_t q = e / call.lr, pos = e - q * call.lr;
-                    thr = q * call.lr + (pos / a.t.piece) * a.t.piece;
-                } else if (x1 != 0 && e > 0) {     // a significant zero decides
-                    thr = e;
+            for (int j = 0; j < V; ++j) {
+                const int64_t e = lo + (int64_t)j * G + gl;
+                if (e >= 0 && x[j] == (T)0 && !all_masked(mk, r.tab, o[j], x[j])) {
+                    const bool lanes = olanes && e < call.lr;
+                    uint64_t x1, xw, xa;
+                    tie_keys32((uint32_t)e, __builtin_signbit(x[j]) ? 1u : 0u, call, a.t, lanes, x1, xw, xa);
+                    k1 = x1 > k1 ? x1 : k1;
+                    kw = xw < kw ? xw : kw;
+                    ka = xa > ka ? xa : ka;
+                    int64_t thr = -1;
+                    if (call.acc && !lanes) {          // finish this zero's row
+                        const uint32_t ue = (uint32_t)e, lr = (uint32_t)call.lr, P = (uint32_t)a.t.piece;
+                        const uint32_t q = ue / lr, pos = ue - q * lr;
+                        thr = (int64_t)q * lr + (pos / P) * P;
+                    } else if (x1 != 0 && e > 0) {     // a significant zero decides
+                        thr = e;
+                    }
+                    const uint64_t t1 = (uint64_t)(thr + 1);
+                    thr1 = t1 > thr1 ? t1 : thr1;
                 }
-                const uint64_t t1 = (uint64_t)(thr + 1);
-                thr1 = t1 > thr1 ? t1 : thr1;
+            }
+            thr1 = thr1 > stop1 ? thr1 : stop1;
+            stop1 = grp_max_u64<G>(thr1);
+            hi = lo;
+        }
+        k1 = grp_max_u64<G>(k1);
+        kw = grp_min_u64<G>(kw);
+        ka = grp_max_u64<G>(ka);
+        if (gl == 0) {
+            const int sg = tie_finalize(k1, kw, ka, call, a.t);
+            if (a.parts) {
+                if (sg >= 0) tie_put_at<T>(a.parts, ob, rec, a.which, sg);
+            } else {
+                a.flags[ob] = sg < 0 ? (uint8_t)0 : (uint8_t)(1u | ((unsigned)sg << 1));
             }
         }
-        thr1 = thr1 > stop1 ? thr1 : stop1;
-        stop1 = grp_max_u64<G>(thr1, lds);
-        hi = lo;
-    }
-    k1 = grp_max_u64<G>(k1, lds);
-    kw = grp_min_u64<G>(kw, lds);
-    ka = grp_max_u64<G>(ka, lds);
-    if (gl != 0) return;
-    const int sg = tie_finalize(k1, kw, ka, call, a.t);
-    if (a.parts) {
-        if (sg >= 0) tie_put_at<T>(a.parts, ob, rec, a.which, sg);
-    } else {
-        a.flags[ob] = sg < 0 ? (uint8_t)0 : (uint8_t)(1u | ((unsigned)sg << 1));
     }
 }
 
@@ -3281,13 +3323,11 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // reduced position is layer_base + l.  keys == NULL: the output's sign is
 // written to fin[f] (one slice per output); else the wave's keys are folded
 // into keys[f] (max) / keys[n_out + f] (min).
+// Keys of layers [lb, le) of final output f, lanes l0, l0 + ls, ... (the
+// callers: a wave per output slice, or a thread per output).
 template <typename T>
-__global__ __launch_bounds__(kBlock) void k_tie_grid(TieGridArgs a) {
-    const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
-    const int64_t gw = (int64_t)blockIdx.x * (kBlock / kWave) + w;
-    const int64_t f = gw / a.slices, sl = gw - f * a.slices;
-    if (f >= a.n_out) return;   // wave-uniform
-    if (!tie_zero<T>(a.fin[f], a.which)) return;
+__device__ __forceinline__ void tie_grid_keys(const TieGridArgs &a, int64_t f, int64_t sl, int l0, int ls,
+                                              uint64_t &k1, uint64_t &kw) {
     const pyas_grid &g = a.g;
     int64_t gstride[PYAS_MAX_DIMS];
     int64_t j = 0, nk = 0, l_lo = 0, l_n = a.n_layers;
@@ -3315,8 +3355,10 @@ __global__ __launch_bounds__(kBlock) void k_tie_grid(TieGridArgs a) {
     }
     const int64_t per = (l_n + a.slices - 1) / a.slices;
     const int64_t lb = sl * per, le = (lb + per) < l_n ? (lb + per) : l_n;
-    uint64_t k1 = 0, kw = kTieWNone;
-    for (int64_t l = lb + lane; l < le; l += kWave) {
+    const int rec = tie_rec(a.which);
+    k1 = 0;
+    kw = kTieWNone;
+    for (int64_t l = lb + l0; l < le; l += ls) {
         int64_t idx;
         if (a.kind == 0) {
             int64_t n = nk;
@@ -3342,7 +3384,7 @@ __global__ __launch_bounds__(kBlock) void k_tie_grid(TieGridArgs a) {
             zero = (b & 1u) != 0;
             sg = (b >> 1) & 1u;
         } else {
-            const pyas_partial p = part_at<T>(a.parts, idx, tie_rec(a.which));
+            const pyas_partial p = part_at<T>(a.parts, idx, rec);
             const T v = TT<T>::from((a.which & 1u) ? p.min : p.max);
             zero = p.count > 0 && v == (T)0;
             sg = __builtin_signbit(v) ? 1u : 0u;
@@ -3354,9 +3396,10 @@ __global__ __launch_bounds__(kBlock) void k_tie_grid(TieGridArgs a) {
             kw = xw < kw ? xw : kw;
         }
     }
-    k1 = wave_max_u64(k1);
-    kw = wave_min_u64(kw);
-    if (lane != 0) return;
+}
+
+template <typename T>
+__device__ __forceinline__ void tie_grid_out(const TieGridArgs &a, int64_t f, uint64_t k1, uint64_t kw) {
     if (a.keys) {
         if (k1) atomicMax(reinterpret_cast<unsigned long long *>(a.keys + f), (unsigned long long)k1);
         if (kw != kTieWNone)
@@ -3365,6 +3408,40 @@ __global__ __launch_bounds__(kBlock) void k_tie_grid(TieGridArgs a) {
         const int sg = tie_finalize(k1, kw, 0, a.call, a.t);
         if (sg >= 0) tie_put<T>(a.fin + f, a.which, sg);
     }
+}
+
+// Level 2 (active.py:594 over the `out` array): one wave per (final output,
+// slice of its chunk layers).  Layer l of output f comes from the grid
+// tables (kind 0, pyas_combine_grid's walk), a segment list (kind 1,
+// pyas_combine_segments') or parts[l] itself (kind 2, one output); its
+// reduced position is layer_base + l.  keys == NULL: the output's sign is
+// written to fin[f] (one slice per output); else the wave's keys are folded
+// into keys[f] (max) / keys[n_out + f] (min).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_tie_grid(TieGridArgs a) {
+    const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    const int64_t gw = (int64_t)blockIdx.x * (kBlock / kWave) + w;
+    const int64_t f = gw / a.slices, sl = gw - f * a.slices;
+    if (f >= a.n_out) return;   // wave-uniform
+    if (!tie_zero<T>(a.fin[f], a.which)) return;
+    uint64_t k1, kw;
+    tie_grid_keys<T>(a, f, sl, lane, kWave, k1, kw);
+    k1 = wave_max_u64(k1);
+    kw = wave_min_u64(kw);
+    if (lane == 0) tie_grid_out<T>(a, f, k1, kw);
+}
+
+// Level 2 with a thread per final output (one slice): many outputs with few
+// layers each (C3 partial axes: 2^20 outputs x 16 layers), where a wave per
+// output would leave most lanes idle.  Adjacent threads read adjacent flags
+// or partials of the same chunk.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_tie_grid_t(TieGridArgs a) {
+    const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (f >= a.n_out || !tie_zero<T>(a.fin[f], a.which)) return;
+    uint64_t k1, kw;
+    tie_grid_keys<T>(a, f, 0, 0, 1, k1, kw);
+    tie_grid_out<T>(a, f, k1, kw);
 }
 
 // Keys of n_sets slices or ranks ([K1[n_out], W[n_out]] each) -> fin's signs.
@@ -3393,7 +3470,6 @@ hipError_t launch_tie_chunks_t(const TieChunkArgs &a, int64_t grid, hipStream_t 
         case 1: hipLaunchKernelGGL((k_tie_scan<T, 1>), dim3((unsigned)grid), dim3(kBlock), 0, st, a); break;
         case 16: hipLaunchKernelGGL((k_tie_scan<T, 16>), dim3((unsigned)grid), dim3(kBlock), 0, st, a); break;
         case 64: hipLaunchKernelGGL((k_tie_scan<T, 64>), dim3((unsigned)grid), dim3(kBlock), 0, st, a); break;
-        case kBlock: hipLaunchKernelGGL((k_tie_scan<T, kBlock>), dim3((unsigned)grid), dim3(kBlock), 0, st, a); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
@@ -3417,6 +3493,11 @@ hipError_t launch_tie_grid_t(const TieGridArgs &a, hipStream_t st) {
     if constexpr (TT<T>::kind != 0) {
         return hipSuccess;
     } else {
+        if (a.per_thread) {
+            const int64_t blocks = (a.n_out + kBlock - 1) / kBlock;
+            hipLaunchKernelGGL((k_tie_grid_t<T>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a);
+            return hipGetLastError();
+        }
         const int64_t waves = a.n_out * a.slices;
         const int64_t blocks = (waves + kBlock / kWave - 1) / (kBlock / kWave);
         hipLaunchKernelGGL((k_tie_grid<T>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a);

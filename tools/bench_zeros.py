@@ -23,6 +23,8 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("PYAS_TREE"):   # A/B: another build of the package (e.g. the previous round's)
+    sys.path.insert(0, os.environ["PYAS_TREE"])
 
 
 def make_variable(torch, path, n, c, zeros, seed=0):
