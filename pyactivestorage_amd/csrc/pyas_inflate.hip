@@ -303,6 +303,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
     const int64_t n_in = x.src_sizes[c];
     const uint32_t mis = (uint32_t)((uintptr_t)src & 3);
     __shared__ uint32_t in_ring[kInRing];
+    __shared__ uint8_t mark[64];              // symbol starts of one 64-byte output step
     BitIn in;
     in.ring = in_ring;
     in.w = reinterpret_cast<const uint32_t *>(src - mis);
@@ -637,7 +638,6 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
             PYAS_PROF(3);
             if (par) {
                 issue_pending();
-                wave_lds_sync();                         // ring bytes other lanes wrote since the last step
                 const uint32_t pos0 = o.pos;
                 uint64_t mm = __ballot(on2 && kind == kMatch);
                 PYAS_STAT(0, __builtin_popcountll(M));
@@ -661,25 +661,18 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
                 const bool any_far = __ballot(on2 && kind == kMatch && dd > kWin) != 0;
                 if (any_far) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 const uint32_t pk = (kind << 16) | (sym & 255u);
-                const uint64_t chain = __ballot(on2);    // the window's symbols, in output order
+                uint32_t carry = 0;                      // lane + 1 of the symbol covering position c
                 for (uint32_t c = 0; c < T; c += 64) {
                     const uint32_t p = c + (uint32_t)lane;
-                    // the symbol covering p: the last one starting at or before
-                    // p.  A scalar walk over the chain (a few symbols) with one
-                    // readlane per field and a select per lane: no LDS marks,
-                    // scan or bpermutes on this path (round 3 spent half the
-                    // decode time on that round trip chain).
-                    uint32_t s_d = 0, s_pk = 0;
-                    for (uint64_t mm = chain; mm; mm &= mm - 1ull) {
-                        const uint32_t sl = (uint32_t)__builtin_ctzll(mm);
-                        const uint32_t e = rl(excl, sl);
-                        if (e >= c + 64u) break;          // uniform: later symbols start past this step
-                        const uint32_t d_s = rl(dd, sl), pk_s = rl(pk, sl);
-                        if (p >= e) {
-                            s_d = d_s;
-                            s_pk = pk_s;
-                        }
-                    }
+                    mark[lane] = 0;
+                    if (on2 && excl >= c && excl < c + 64u) mark[excl - c] = (uint8_t)(lane + 1);
+                    wave_lds_sync();                     // other lanes' marks (no store forwarding)
+                    uint32_t S = wave_incl_max(mark[lane]);
+                    S = S > carry ? S : carry;
+                    carry = rl(S, 63);
+                    const uint32_t k = (S - 1u) & 63u;
+                    const uint32_t s_d = (uint32_t)__shfl((int)dd, (int)k, 64);
+                    const uint32_t s_pk = (uint32_t)__shfl((int)pk, (int)k, 64);
                     const bool valid = p < T;
                     const bool is_m = (s_pk >> 16) == kMatch;
                     const int32_t src = (int32_t)p - (int32_t)s_d;   // window-relative source

@@ -92,6 +92,16 @@ __device__ __forceinline__ uint4 ldg16(const uint4 *p) {
 #endif
 }
 
+// A load through the constant address space: with a wave-uniform address the
+// compiler issues s_load (counted by lgkmcnt), so waiting for it never waits
+// for the wave's vector loads in flight.  For read-only tables only (chunk and output
+// offsets: a vector load of one at a chunk boundary used to stall the column
+// walks' ring of loads with vmcnt(0)).
+template <typename V>
+__device__ __forceinline__ V sload(const V *p) {
+    return *(const __attribute__((address_space(4))) V *)p;
+}
+
 // Raw 16 bytes of the plain layout -> 16/ES values
 template <typename T, bool BSWAP>
 __device__ __forceinline__ void unpack16(const uint4 &r, T *x) {
@@ -407,9 +417,10 @@ __device__ __forceinline__ int64_t out_bytes(int rec) {
 // p as record `rec` (the first Rec<T>::kBytes bytes of the result)
 template <typename T>
 __device__ __forceinline__ uint4 rec_of(const pyas_partial &p, int rec) {
-    T v;
-    if (rec == PYAS_REC_SUM) v = (T)sum_of<T>(p.sum, true);
-    else v = TT<T>::from(rec == PYAS_REC_MIN ? p.min : p.max);
+    // every field converted, then values selected: a field picked by a
+    // runtime index would put p in scratch memory
+    const T vs = (T)sum_of<T>(p.sum, true), vmin = TT<T>::from(p.min), vmax = TT<T>::from(p.max);
+    const T v = rec == PYAS_REC_SUM ? vs : rec == PYAS_REC_MIN ? vmin : vmax;
     uint4 r = {0u, 0u, 0u, 0u};
     if constexpr (sizeof(T) <= 4) {
         __builtin_memcpy(&r.x, &v, sizeof(T));
@@ -440,13 +451,14 @@ __device__ __forceinline__ pyas_partial part_at(const void *base, int64_t i, int
         __builtin_memcpy(&v, &r.x, 8);
         p.count = (int64_t)(int32_t)r.z;
     }
-    if (rec == PYAS_REC_SUM) {
-        if constexpr (TT<T>::kind == 0) p.sum.f = (double)v;
-        else if constexpr (TT<T>::kind == 1) p.sum.i = (int64_t)v;
-        else p.sum.u = (uint64_t)v;
-    } else {
-        TT<T>::put(rec == PYAS_REC_MIN ? p.min : p.max, v);
-    }
+    pyas_scalar sv, mv;
+    if constexpr (TT<T>::kind == 0) sv.f = (double)v;
+    else if constexpr (TT<T>::kind == 1) sv.i = (int64_t)v;
+    else sv.u = (uint64_t)v;
+    TT<T>::put(mv, v);
+    p.sum.u = rec == PYAS_REC_SUM ? sv.u : 0u;
+    p.min.u = rec == PYAS_REC_MIN ? mv.u : 0u;
+    p.max.u = rec == PYAS_REC_MAX ? mv.u : 0u;
     return p;
 }
 
@@ -469,11 +481,11 @@ __device__ __forceinline__ void put_out(const AxesArgs &a, int64_t o, const pyas
 // destination allows, else 8-B records).
 template <typename T>
 __device__ __forceinline__ void stage_put(const AxesArgs &a, uint4 *stage, int k, const pyas_partial &p) {
-    if (a.rec == 0) {
-        uint4 h[2];
-        __builtin_memcpy(h, &p, 32);
-        stage[k * 2] = h[0];
-        stage[k * 2 + 1] = h[1];
+    if (a.rec == 0) {   // the 32-byte partial as two 16-B words, from its fields
+        stage[k * 2] = make_uint4((uint32_t)p.sum.u, (uint32_t)(p.sum.u >> 32), (uint32_t)(uint64_t)p.count,
+                                  (uint32_t)((uint64_t)p.count >> 32));
+        stage[k * 2 + 1] = make_uint4((uint32_t)p.min.u, (uint32_t)(p.min.u >> 32), (uint32_t)p.max.u,
+                                      (uint32_t)(p.max.u >> 32));
     } else if constexpr (Rec<T>::kBytes == 16) {
         stage[k] = rec_of<T>(p, a.rec);
     } else {
@@ -1709,7 +1721,7 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     const int IT = d.it, S = d.split;
     const int il = threadIdx.x & (IT - 1), sp = threadIdx.x / IT;
     const int64_t items = d.KO * (d.KI / N);
-    const int64_t ob = a.out_offsets[c];
+    const int64_t ob = sload(a.out_offsets + c);
     // aligned chunks: the ring walk (measured faster than the shuffled unit
     // exchange too); PYAS_COL_RING=0 builds the earlier walks
     constexpr bool ring = PYAS_COL_RING && AL;
@@ -1778,7 +1790,7 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     const int64_t nwaves = d.bpc * (kBlock / kWave);
     const int64_t vstep = (int64_t)G * N * VPL * ES;             // bytes (plain layout)
     const int64_t wrap = (d.KO - 1) * d.RI * ES;                 // next run of the output
-    const int64_t ob = a.out_offsets[c];
+    const int64_t ob = sload(a.out_offsets + c);
     for (int64_t o0 = wave * P * UO; o0 < d.KO; o0 += nwaves * P * UO) {   // wave-uniform
         TileAcc<T> acc[UO];
 #pragma unroll
@@ -1864,7 +1876,7 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
     uint4 *t = tile + (threadIdx.x / kWave) * RPW * kRowLdsStride;
     const int64_t wave = j * (kBlock / kWave) + threadIdx.x / kWave;
     const int64_t nwaves = d.bpc * (kBlock / kWave);
-    const int64_t ob = a.out_offsets[c];
+    const int64_t ob = sload(a.out_offsets + c);
     // tile unit q = u * kWave + lane: vectors q*VPL .. +VPL-1, in run q*VPL / V
     int lrow[UL], lcol[UL];
 #pragma unroll
@@ -2025,7 +2037,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes
                 rr = q;
             }
         }
-        return r.data + r.offsets[n];
+        return r.data + sload(r.offsets + n);
     };
     // Pipelined walk (block-uniform choice): every lane has the same rows per
     // layer, a multiple of U, and every layer is aligned, so the walk is
@@ -2340,7 +2352,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
                 rr = q;
             }
         }
-        return r.data + r.offsets[cn];
+        return r.data + sload(r.offsets + cn);
     };
     MaskT<T> mk;
     mk.init(r.mask);
@@ -2448,7 +2460,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_c
     const int64_t j = blockIdx.x - g * d.bpc;
     const int64_t c0 = g * d.cpb;
     const int64_t nc = d.n_chunks - c0 < d.cpb ? d.n_chunks - c0 : d.cpb;
-    auto layer_base = [&](int64_t l) { return r.data + r.offsets[c0 + l]; };
+    auto layer_base = [&](int64_t l) { return r.data + sload(r.offsets + c0 + l); };
     MaskT<T> mk;
     mk.init(r.mask);
     __shared__ uint4 stage[kBlock * 2 * N > col_units_lds<T>() ? kBlock * 2 * N : col_units_lds<T>()];
@@ -2476,7 +2488,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_c
         offs[v] = (ko * d.RI * d.KI + vv * N) * sizeof(T);
     }
     auto chunk_end = [&](int64_t cl, TileAcc<T> *acc) {
-        const int64_t cob = a.out_offsets[c0 + cl];
+        const int64_t cob = sload(a.out_offsets + c0 + cl);
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             const int64_t iv = iw + v * kWave;
@@ -2527,7 +2539,11 @@ __global__ __launch_bounds__(kBlock) void k_axes_shuf_slab(AxesArgs a) {
     __shared__ uint4 tiles[kBlock / kWave][kSlabBytes / 16];
     const AxesDense &d = a.d;
     const ReduceArgs &r = a.r;
-    const int w = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    // wave-uniform unit indices in SGPRs: the chunk offsets and output
+    // offsets then come with scalar loads, which never wait on the vector
+    // loads of the next slab in flight (a vector load of out_offsets[c] at a
+    // unit's end made the wave wait for those with vmcnt(0))
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
     const int64_t gw = (int64_t)blockIdx.x * (kBlock / kWave) + w;
     const int64_t TW = (int64_t)gridDim.x * (kBlock / kWave);
     const int64_t KI = d.KI, RI = d.RI, RB = d.rb, NS = RI / RB;
@@ -2543,7 +2559,7 @@ __global__ __launch_bounds__(kBlock) void k_axes_shuf_slab(AxesArgs a) {
     // issue the plane loads of sub-slab s of unit u (16-B pieces; AL per chunk)
     auto load = [&](int64_t u, int64_t s) {
         const int64_t c = u / d.KO, ko = u - c * d.KO;
-        const uint8_t *base = r.data + r.offsets[c];
+        const uint8_t *base = r.data + sload(r.offsets + c);
         al = ((((uintptr_t)base) | (uint64_t)n) & 15) == 0;    // wave-uniform
         const int64_t e0 = (ko * RI + s * RB) * KI + 16 * lane;
 #pragma unroll
@@ -2650,7 +2666,7 @@ __global__ __launch_bounds__(kBlock) void k_axes_shuf_slab(AxesArgs a) {
         }
         if (cs == NS - 1) {   // the unit's last rows: its KPL * 64 outputs
             const int64_t c = cu / d.KO, ko = cu - c * d.KO;
-            const int64_t ob = a.out_offsets[c] + ko * KI;
+            const int64_t ob = sload(a.out_offsets + c) + ko * KI;
 #pragma unroll
             for (int q = 0; q < KPL; ++q) {
                 if constexpr (!MASKED) acc[q].count += (uint32_t)RI;
@@ -2708,7 +2724,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
                 rr = q;
             }
         }
-        return r.data + r.offsets[n];
+        return r.data + sload(r.offsets + n);
     };
     MaskT<T> mk;
     mk.init(r.mask);
@@ -3038,9 +3054,11 @@ __device__ __forceinline__ uint64_t grp_min_u64(uint64_t v) {
 }
 
 // tie_keys in 32-bit arithmetic: every position, call length and piece of a
-// chunk output is < 2^31 (pyas_tie_chunks checks the reduced count).
-__device__ __forceinline__ void tie_keys32(uint32_t e, uint64_t sg, const TieCall &c, const TieRule &t, bool lanes,
-                                           uint64_t &k1, uint64_t &w, uint64_t &ka) {
+// chunk output is < 2^31 (pyas_tie_chunks checks the reduced count).  The
+// rule's priority tables are read from LDS (rank / arank).
+__device__ __forceinline__ void tie_keys32(uint32_t e, uint64_t sg, const TieCall &c, const TieRule &t,
+                                           const uint8_t *rank, const uint8_t *arank, bool lanes, uint64_t &k1,
+                                           uint64_t &w, uint64_t &ka) {
     k1 = 0;
     w = kTieWNone;
     ka = 0;
@@ -3064,16 +3082,99 @@ __device__ __forceinline__ void tie_keys32(uint32_t e, uint64_t sg, const TieCal
         const uint32_t A = (uint32_t)t.acc;
         const uint32_t nv = m - m % A;
         const bool vec = off < nv;
-        const uint64_t prio = vec ? (uint64_t)(t.acc - 1 - t.acc_rank[off % A]) : 0u;
+        const uint64_t prio = vec ? (uint64_t)(t.acc - 1 - arank[off % A]) : 0u;
         ka = (row1 << 33) | ((uint64_t)(vec ? 0 : 1) << 32) | (prio << 25) | ((uint64_t)off << 1) | sg;
         return;
     }
     const uint32_t L = (uint32_t)t.lanes;
     const uint32_t nv = m - m % L;
     const bool vec = off < nv;
-    const uint32_t rank = vec ? (uint32_t)t.rank[off % L] : kTieRemRank;
-    k1 = (!vec || rank == 0) ? ((((uint64_t)e + 1) << 1) | sg) : 0u;
-    w = (row1 << 32) | ((uint64_t)rank << 25) | ((uint64_t)(((uint32_t)1 << kTieOffBits) - 1 - off) << 1) | sg;
+    const uint32_t rk = vec ? (uint32_t)rank[off % L] : kTieRemRank;
+    k1 = (!vec || rk == 0) ? ((((uint64_t)e + 1) << 1) | sg) : 0u;
+    w = (row1 << 32) | ((uint64_t)rk << 25) | ((uint64_t)(((uint32_t)1 << kTieOffBits) - 1 - off) << 1) | sg;
+}
+
+// Per-chunk state of the level-1 scan, worked out once by one lane and
+// shared through LDS: the call structure, the reduced dims in visiting
+// order (scan slots, innermost first) and the kept dims (innermost first).
+struct TieSetup {
+    TieCall call;
+    int64_t n_out, R, base_red, data_off, out_base;
+    int32_t nr, nk;
+    uint32_t rc[PYAS_MAX_DIMS];
+    int32_t rst[PYAS_MAX_DIMS], rsp[PYAS_MAX_DIMS], rcs[PYAS_MAX_DIMS];
+    int64_t rt0[PYAS_MAX_DIMS], rt1[PYAS_MAX_DIMS];
+    uint32_t kc[PYAS_MAX_DIMS];
+    int32_t kst[PYAS_MAX_DIMS], ksp[PYAS_MAX_DIMS], kcs[PYAS_MAX_DIMS];
+    int64_t kbw[PYAS_MAX_DIMS], kt0[PYAS_MAX_DIMS], kt1[PYAS_MAX_DIMS];
+    uint32_t kin;                     // bit j: kept slot j lies in NumPy's copied first fill
+};
+
+__device__ void tie_setup(const TieChunkArgs &a, int64_t c, TieSetup &S) {
+    const ReduceArgs &r = a.r;
+    Sel s;
+    load_sel(s, r.sel, c, r.ndim, r.shape);
+    int64_t cnt[PYAS_MAX_DIMS];
+    int64_t n_out = 1, R = 1;
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+        cnt[d] = d < r.ndim ? (int64_t)s.cnt[d] : 1;
+        if ((a.axes >> d) & 1u) R *= cnt[d];
+        else n_out *= cnt[d];
+    }
+    S.n_out = n_out;
+    S.R = R;
+    S.data_off = r.offsets[c];
+    S.out_base = a.out_offsets ? a.out_offsets[c] : c;
+    int64_t vstride[PYAS_MAX_DIMS];
+    int64_t st = 1;
+    for (int i = r.ndim - 1; i >= 0; --i) {
+        const int d = a.g.perm[i];
+        vstride[d] = st;
+        st *= cnt[d];
+    }
+    if (a.g.flags & PYAS_TIE_VIEW)
+        for (int d = 0; d < r.ndim; ++d) vstride[d] = (int64_t)s.step[d] * r.cstride[d];
+    S.call = tie_call(cnt, vstride, a.axes, a.g.perm, r.ndim, (a.g.flags & PYAS_TIE_BUFFERED) != 0, a.t.piece);
+    int64_t bw[PYAS_MAX_DIMS];   // kept-block weights (NumPy's copied first fill), inner first
+    st = 1;
+    for (int i = r.ndim - 1; i >= 0; --i) {
+        const int d = a.g.perm[i];
+        bw[d] = ((S.call.block >> d) & 1u) ? st : 0;
+        if ((S.call.block >> d) & 1u) st *= cnt[d];
+    }
+    int nr = 0;
+    S.base_red = 0;
+    for (int i = r.ndim - 1; i >= 0; --i) {
+        const int d = a.g.perm[i];
+        if (!((a.axes >> d) & 1u)) continue;
+        if (cnt[d] == 1) {   // one selected index: an offset, not a scan slot
+            S.base_red += sel_index(s, r.pool, d, 0) * r.cstride[d];
+            continue;
+        }
+        S.rc[nr] = (uint32_t)cnt[d];
+        S.rst[nr] = s.start[d];
+        S.rsp[nr] = s.step[d];
+        S.rcs[nr] = (int32_t)r.cstride[d];
+        S.rt0[nr] = r.tab.stride[0][d];
+        S.rt1[nr] = r.tab.stride[1][d];
+        ++nr;
+    }
+    S.nr = nr;
+    int nk = 0;
+    S.kin = 0;
+    for (int d = r.ndim - 1; d >= 0; --d) {   // outputs are C-ordered over the kept dims
+        if ((a.axes >> d) & 1u) continue;
+        S.kc[nk] = (uint32_t)cnt[d];
+        S.kst[nk] = s.start[d];
+        S.ksp[nk] = s.step[d];
+        S.kcs[nk] = (int32_t)r.cstride[d];
+        S.kbw[nk] = bw[d];
+        S.kt0[nk] = r.tab.stride[0][d];
+        S.kt1[nk] = r.tab.stride[1][d];
+        if ((S.call.block >> d) & 1u) S.kin |= 1u << nk;
+        ++nk;
+    }
+    S.nk = nk;
 }
 
 // Level 1 (storage.py:99-100 over chunk[sel]): the sign NumPy gives each zero
@@ -3093,128 +3194,90 @@ __device__ __forceinline__ void tie_keys32(uint32_t e, uint64_t sg, const TieCal
 // equals that of all keys (zerosign.predict_scan; tests compare with NumPy).
 // G lanes share an output (1: one output per lane, for elementwise calls,
 // where adjacent lanes hold adjacent outputs).  A workgroup takes one chunk
-// and loops over its outputs, kBlock / G at a time, so the chunk's setup
-// (selection, call structure, visiting order) is paid once per chunk; when
-// every chunk has one output (a full reduction), each wave takes a chunk
-// (a.cpw = kBlock / kWave chunks per workgroup).  Rewrite mode (parts):
-// outputs whose min/max is a zero get NumPy's sign.  Flag mode (flags): one
-// byte per chunk output, bit 0 an unmasked zero, bit 1 the winning zero's
-// sign; skipped when *gate == 0.
+// and loops over its outputs, kBlock / G at a time; when every chunk has one
+// output (a full reduction) each wave takes a chunk (a.cpw = 4 chunks per
+// workgroup).  The chunk's setup is worked out once, by one lane, into LDS
+// (TieSetup); the scan reads it as wave-uniform values.  Rewrite mode
+// (parts): outputs whose min/max is a zero get NumPy's sign.  Flag mode
+// (flags): one byte per chunk output, bit 0 an unmasked zero, bit 1 the
+// winning zero's sign; skipped when *gate == 0.
 template <typename T, int G>
 __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
     constexpr int NG = kBlock / G;
     constexpr int V = G == kWave ? 4 : 1;     // elements per lane per step
+    constexpr int NW = kBlock / kWave;
+    __shared__ TieSetup setups[NW];
+    __shared__ uint8_t rank[64], arank[64];
     const ReduceArgs &r = a.r;
     if (a.gate && *a.gate == 0u) return;
     const int grp = (int)threadIdx.x / G, gl = (int)threadIdx.x % G;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+    if (threadIdx.x < 64) {
+        rank[threadIdx.x] = a.t.rank[threadIdx.x];
+        arank[threadIdx.x] = a.t.acc_rank[threadIdx.x];
+    }
     int64_t c, o_first, o_step;
+    int slot;
     if (a.cpw > 1) {   // one output per chunk, a wave per chunk (host: G == kWave)
-        c = (int64_t)blockIdx.x * a.cpw + threadIdx.x / kWave;
+        c = (int64_t)blockIdx.x * a.cpw + wv;
         o_first = 0;
         o_step = 1;
-        if (c >= a.n_chunks) return;   // wave-uniform
+        slot = wv;
+        if (c < a.n_chunks && lane == 0) tie_setup(a, c, setups[slot]);
     } else {
         c = blockIdx.x;
         o_first = grp;
         o_step = NG;
+        slot = 0;
+        if (threadIdx.x == 0) tie_setup(a, c, setups[0]);
     }
+    __syncthreads();
+    if (c >= a.n_chunks) return;   // wave-uniform
+    const TieSetup &S = setups[slot];
     const int rec = tie_rec(a.which);
-    Sel s;
-    load_sel(s, r.sel, c, r.ndim, r.shape);
-    int64_t cnt[PYAS_MAX_DIMS];
-    int64_t n_out = 1, R = 1;
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
-        cnt[d] = d < r.ndim ? (int64_t)s.cnt[d] : 1;
-        if ((a.axes >> d) & 1u) R *= cnt[d];
-        else n_out *= cnt[d];
-    }
-    if (n_out == 0 || R == 0) return;   // uniform per chunk
-    int64_t vstride[PYAS_MAX_DIMS];
-    {
-        int64_t st = 1;
-#pragma unroll
-        for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
-            if (i < r.ndim) {
-                const int d = a.g.perm[i];
-                vstride[d] = st;
-                st *= cnt[d];
-            }
-        }
-        if (a.g.flags & PYAS_TIE_VIEW) {
-#pragma unroll
-            for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-                if (d < r.ndim) vstride[d] = (int64_t)s.step[d] * r.cstride[d];
-        }
-    }
-    const TieCall call = tie_call(cnt, vstride, a.axes, a.g.perm, r.ndim, (a.g.flags & PYAS_TIE_BUFFERED) != 0,
-                                  a.t.piece);
-    int64_t bw[PYAS_MAX_DIMS];   // kept-block weights (NumPy's copied first fill), inner first
-    {
-        int64_t st = 1;
-#pragma unroll
-        for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
-            if (i < r.ndim) {
-                const int d = a.g.perm[i];
-                bw[d] = ((call.block >> d) & 1u) ? st : 0;
-                if ((call.block >> d) & 1u) st *= cnt[d];
-            }
-        }
-    }
-    // reduced dims in visiting order, innermost first (slot i = perm[nd-1-i]);
-    // reduced dims of one selected index only offset the base
+    const int64_t n_out = S.n_out, R = S.R;
+    if (n_out == 0 || R == 0) return;
+    const TieCall call = S.call;
+    const int nr = S.nr, nk = S.nk;
+    const bool tabs = r.tab.on[0] || r.tab.on[1];
     uint32_t rc[PYAS_MAX_DIMS];
-    int32_t rst[PYAS_MAX_DIMS], rsp[PYAS_MAX_DIMS];
-    int64_t rcs[PYAS_MAX_DIMS], rt0[PYAS_MAX_DIMS], rt1[PYAS_MAX_DIMS];
-    int nr = 0;
+    int32_t rst[PYAS_MAX_DIMS], rsp[PYAS_MAX_DIMS], rcs[PYAS_MAX_DIMS];
 #pragma unroll
-    for (int i = PYAS_MAX_DIMS - 1; i >= 0; --i) {
-        if (i < r.ndim) {
-            const int d = a.g.perm[i];
-            if (((a.axes >> d) & 1u) && cnt[d] != 1) {
-#pragma unroll
-                for (int j = 0; j < PYAS_MAX_DIMS; ++j) {
-                    if (j == nr) {
-                        rc[j] = (uint32_t)cnt[d];
-                        rst[j] = s.start[d];
-                        rsp[j] = s.step[d];
-                        rcs[j] = r.cstride[d];
-                        rt0[j] = r.tab.stride[0][d];
-                        rt1[j] = r.tab.stride[1][d];
-                    }
-                }
-                ++nr;
-            }
-        }
+    for (int i = 0; i < PYAS_MAX_DIMS; ++i) {   // wave-uniform: scalar registers
+        rc[i] = __builtin_amdgcn_readfirstlane(i < nr ? S.rc[i] : 1u);
+        rst[i] = __builtin_amdgcn_readfirstlane(i < nr ? S.rst[i] : 0);
+        rsp[i] = __builtin_amdgcn_readfirstlane(i < nr ? S.rsp[i] : 0);
+        rcs[i] = __builtin_amdgcn_readfirstlane(i < nr ? S.rcs[i] : 0);
     }
-    int64_t base_red = 0;   // reduced dims of extent 1 (not scan slots)
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-        if (d < r.ndim && ((a.axes >> d) & 1u) && cnt[d] == 1) base_red += sel_index(s, r.pool, d, 0) * r.cstride[d];
     MaskT<T> mk;
     mk.init(r.mask);
-    const uint8_t *data = r.data + r.offsets[c];
-    const int64_t obase = a.out_offsets ? a.out_offsets[c] : c;
+    const uint8_t *data = r.data + S.data_off;
+    const int64_t obase = S.out_base;
     for (int64_t ol = o_first; ol < n_out; ol += o_step) {   // group-uniform
         const int64_t ob = obase + ol;
         if (a.parts && !tie_zero<T>(part_at<T>(a.parts, ob, rec), a.which)) continue;
         // the output's kept coordinates: memory / table base, and whether its
         // first run is a copied (contiguous) call of a strided reduction
-        Decomp base{base_red, {0, 0}};
+        Decomp base{S.base_red, {0, 0}};
         bool olanes = false;
         {
-            int64_t oo = ol, bidx = 0;
+            uint32_t oo = (uint32_t)ol;
+            int64_t bidx = 0;
             bool beyond = false;   // a kept coordinate outside the block is non-zero
 #pragma unroll
-            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-                if (d < r.ndim && !((a.axes >> d) & 1u)) {
-                    const int64_t q = oo / cnt[d], k = oo - q * cnt[d];
+            for (int j = 0; j < PYAS_MAX_DIMS; ++j) {
+                if (j < nk) {
+                    const uint32_t kcj = S.kc[j], q = oo / kcj, k = oo - q * kcj;
                     oo = q;
-                    if ((call.block >> d) & 1u) bidx += k * bw[d];
+                    if ((S.kin >> j) & 1u) bidx += (int64_t)k * S.kbw[j];
                     else beyond |= k != 0;
-                    base.mem += sel_index(s, r.pool, d, k) * r.cstride[d];
-                    base.v[0] += k * r.tab.stride[0][d];
-                    base.v[1] += k * r.tab.stride[1][d];
+                    const int64_t idx = S.ksp[j] != 0 ? (int64_t)S.kst[j] + (int64_t)k * S.ksp[j]
+                                                      : (int64_t)r.pool[(int64_t)S.kst[j] + k];
+                    base.mem += idx * S.kcs[j];
+                    if (tabs) {
+                        base.v[0] += (int64_t)k * S.kt0[j];
+                        base.v[1] += (int64_t)k * S.kt1[j];
+                    }
                 }
             }
             olanes = call.n_copy && !beyond && bidx < call.n_copy;
@@ -3240,8 +3303,10 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
                             const int64_t idx = rsp[i] != 0 ? (int64_t)rst[i] + (int64_t)k * rsp[i]
                                                             : (int64_t)r.pool[(int64_t)rst[i] + k];
                             o[j].mem += idx * rcs[i];
-                            o[j].v[0] += (int64_t)k * rt0[i];
-                            o[j].v[1] += (int64_t)k * rt1[i];
+                            if (tabs) {
+                                o[j].v[0] += (int64_t)k * S.rt0[i];
+                                o[j].v[1] += (int64_t)k * S.rt1[i];
+                            }
                         }
                     }
                     x[j] = load_elem_rt<T>(data, r.chunk_elems, o[j].mem, a.shuf, a.bswap);
@@ -3254,7 +3319,8 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
                 if (e >= 0 && x[j] == (T)0 && !all_masked(mk, r.tab, o[j], x[j])) {
                     const bool lanes = olanes && e < call.lr;
                     uint64_t x1, xw, xa;
-                    tie_keys32((uint32_t)e, __builtin_signbit(x[j]) ? 1u : 0u, call, a.t, lanes, x1, xw, xa);
+                    tie_keys32((uint32_t)e, __builtin_signbit(x[j]) ? 1u : 0u, call, a.t, rank, arank, lanes, x1,
+                               xw, xa);
                     k1 = x1 > k1 ? x1 : k1;
                     kw = xw < kw ? xw : kw;
                     ka = xa > ka ? xa : ka;

@@ -1,0 +1,20 @@
+# round 4: k_tie_scan with per-chunk setup in LDS; scalar-loaded chunk/output
+# offsets and scratch-free partial staging in the axes kernels
+set -o pipefail
+O=gpurun_out/r04/zeros2
+mkdir -p $O
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+T="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+timeout -k 10 1200 $T tests/test_gpu_zero_sign.py tests/test_gpu_records.py tests/test_gpu_axes_slab.py tests/test_gpu_axes_stream.py tests/test_gpu_axes_fold.py tests/test_gpu_axes_dense.py tests/test_gpu_axes_rowlds.py > $O/tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/bench_zeros.py --zeros 0.5 --axes none,0,2 --reps 5 > $O/zeros50.json 2> $O/zeros50.err || exit 1
+timeout -k 10 300 python -u tools/bench_zeros.py --zeros 0.02 --axes none,0,2 --reps 5 > $O/zeros2.json 2> $O/zeros2.err || exit 1
+(cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/zt -o run -- \
+   python3 $R/tools/bench_zeros.py --zeros 0.5 --axes none,0,2 --reps 5 > $R/$O/zeros50_prof.log 2>&1) || exit 1
+cp $(find /tmp/zt -name '*kernel_stats.csv' | head -n 1) $O/zeros50_kernel_stats.csv
+timeout -k 10 300 python -u tools/bench_axes.py > $O/axes_plain.json 2> $O/axes_plain.err || exit 1
+timeout -k 10 300 python -u tools/bench_axes.py --rec sum > $O/axes_plain_rec.json 2> $O/axes_plain_rec.err || exit 1
+timeout -k 10 300 python -u tools/bench_axes.py --shuffle > $O/axes_shuf.json 2> $O/axes_shuf.err || exit 1
+timeout -k 10 300 python -u tools/bench_axes.py --shuffle --rec sum > $O/axes_shuf_rec.json 2> $O/axes_shuf_rec.err || exit 1
+timeout -k 10 300 python -u tools/bench_axes.py --fold > $O/axes_fold.json 2> $O/axes_fold.err || exit 1
+timeout -k 10 300 python -u tools/bench_axes.py --fold --shuffle > $O/axes_fold_shuf.json 2> $O/axes_fold_shuf.err || exit 1
