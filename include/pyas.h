@@ -394,6 +394,18 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
 int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
                           const pyas_grid *grid, uint32_t combine_flags, pyas_partial *out,
                           void *stream);
+/* combine_flags of pyas_reduce_axes_grid: NumPy's sign of a zero min (MIN)
+ * or max (MAX), fused into the fold.  Valid only where both reductions NumPy
+ * runs are elementwise, which the caller checks: the chunks' innermost dim
+ * in memory and the `out` array's innermost dim (active.py:594) are kept
+ * dims, so storage.py:99-100 and active.py:594 let every later zero win.
+ * Each lane then tracks its outputs' last zero (layer order, then row order)
+ * and writes that zero's sign to a zero result: pyas_tie_chunk_flags and
+ * pyas_tie_grid are not needed.  Float dtypes; PYAS_ENOTSUP (nothing
+ * launched) when the geometry takes a kernel other than the lean column
+ * fold -- fold without the flag and run the zero-sign passes then. */
+#define PYAS_FOLD_ZERO_SIGN_MIN 0x100u
+#define PYAS_FOLD_ZERO_SIGN_MAX 0x200u
 
 /* ---- NumPy's sign of a zero min/max, level 2 (see pyas_tie_chunks) ---- */
 /* Level 2, across chunks (active.py:594): every final output f (partials

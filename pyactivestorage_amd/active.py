@@ -123,8 +123,7 @@ class _CachedQuery:
             return act._format(final.reshape(shape), shape)
         g = self.grid
         if g["folded"]:
-            engine.reduce_axes_grid(ctx, self.plan.batch, self.plan.mask_up.struct, g["g"], g["fin"].ptr,
-                                    True, st)
+            g["tie"]["fused"] = act._fold(ctx, st, self.plan, g["g"], g["fin"].ptr, g["zs_ok"])
         else:   # records of this replay's method (one size per dtype: the buffer fits every method)
             g["rec"] = engine.method_rec(act._method)
             engine.reduce_axes(ctx, self.plan.batch, self.plan.mask_up.struct, g["axes_mask"], g["obuf"].ptr,
@@ -710,6 +709,8 @@ class Active:
         if not which:
             return
         t = rec["tie"]
+        if t.get("fused"):   # the fold wrote NumPy's sign itself (elementwise at both levels)
+            return
         dt = self.ds.dtype
         geom = plan.tie_geom()
         if rec["folded"]:   # no per-chunk partials: per chunk output flags
@@ -822,11 +823,12 @@ class Active:
                 g.coord_count[d] = tbuf.ptr + 4 * tables["coord_count"][d]
         g.chunk_out_offsets = abuf.ptr
         fin = DeviceBuffer(ctx, max(n_final, 1) * _lib.PARTIAL_NBYTES)
-        folded = False
+        folded = fused = False
+        zs_ok = self._elementwise_sign(axes)
         if (_AXES_FOLD and lo == 0 and hi == n_all and not plan.batch.sel
                 and self._whole_chunk_grid(tables, final_shape, axes)):
             try:   # one launch: chunk layers folded inside the reduction kernel
-                engine.reduce_axes_grid(ctx, plan.batch, plan.mask_up.struct, g, fin.ptr, True, st)
+                fused = self._fold(ctx, st, plan, g, fin.ptr, zs_ok)
                 folded = True
             except NotImplementedError:
                 pass   # geometry without the dense column or LDS row layout: two steps
@@ -848,8 +850,9 @@ class Active:
         ext = [tables["n_coords"][d] if d in axes else final_shape[d] for d in range(ds.ndim)]
         r = rec if rec is not None else {}
         r.update(folded=folded, g=g, fin=fin, obuf=obuf, abuf=abuf, tbuf=tbuf, parts=parts, rec=prec,
-                 axes_mask=axes_mask, n_final=n_final,
-                 tie={"lr": zerosign.grid_lr(ext, set(axes)), "n_parts": n_parts_all, "flags": None})
+                 axes_mask=axes_mask, n_final=n_final, zs_ok=zs_ok,
+                 tie={"lr": zerosign.grid_lr(ext, set(axes)), "n_parts": n_parts_all, "flags": None,
+                      "fused": fused})
         if keys is not None and self._tie_which():
             kbuf = DeviceBuffer(ctx, max(n_final, 1) * 16)
             engine.tie_keys_reset(ctx, kbuf.ptr, n_final, st)
@@ -866,6 +869,38 @@ class Active:
         ctx.d2h(final, fin.ptr, st)
         ctx.synchronize(st)
         return final
+
+    def _elementwise_sign(self, axes) -> bool:
+        """Whether NumPy's zero sign of this partial-axis query is "the last
+        zero wins" at both levels: the chunks are C-ordered with their
+        innermost dim kept (storage.py:99-100 reduces elementwise), and so is
+        the `out` array's innermost dim (active.py:594).  Then the in-kernel
+        fold can track it (PYAS_FOLD_ZERO_SIGN_*), if this host's NumPy rule
+        is known at all."""
+        ds = self.ds
+        nd = ds.ndim
+        if ds.dtype.kind != "f" or getattr(ds, "order", "C") != "C" or (nd - 1) in axes:
+            return False
+        if ds.chunks[nd - 1] < 2:
+            return False
+        ctx = get_context(self.device)
+        return bool(getattr(ctx, "tie_signs_exact", {}).get("f4" if ds.dtype.itemsize == 4 else "f8"))
+
+    def _fold(self, ctx, st, plan, g, fin_ptr, zs_ok) -> bool:
+        """pyas_reduce_axes_grid, with NumPy's zero sign fused in when the
+        query allows it (min/max of a float variable, elementwise at both
+        levels) and the lean column fold takes the geometry.  Returns
+        whether the sign was fused (else the zero-sign passes run)."""
+        which = self._tie_which() if zs_ok else 0
+        if which:
+            try:
+                engine.reduce_axes_grid(ctx, plan.batch, plan.mask_up.struct, g, fin_ptr, True, st,
+                                        zero_sign=which)
+                return True
+            except NotImplementedError:
+                pass   # another fold kernel: the sign comes from the tie passes
+        engine.reduce_axes_grid(ctx, plan.batch, plan.mask_up.struct, g, fin_ptr, True, st)
+        return False
 
     def _whole_chunk_grid(self, tables, final_shape, axes):
         """Every kept dim's output positions are whole chunks in coordinate

@@ -1055,7 +1055,7 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
     bool shuf, bsw, masked;
     int rc = prepare(ctx, batch, mask, x.r, es, shuf, bsw, masked);
     if (rc) return rc;
-    if (combine_flags & ~PYAS_COMBINE_ROUND_TO_VAR)
+    if (combine_flags & ~(PYAS_COMBINE_ROUND_TO_VAR | PYAS_FOLD_ZERO_SIGN_MIN | PYAS_FOLD_ZERO_SIGN_MAX))
         return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
     if (g->ndim != batch->ndim) return fail(PYAS_EINVAL, "grid rank %d != batch rank %d", g->ndim, batch->ndim);
     const uint32_t axes_mask = g->axes_mask;
@@ -1064,6 +1064,10 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
     if (batch->sel) return fail(PYAS_ENOTSUP, "the in-kernel layer fold needs whole chunks (sel == NULL)");
     pyas::FoldGrid fg;
     std::memset(&fg, 0, sizeof(fg));
+    // NumPy's zero sign fused into the lean column fold (floats; the caller
+    // has checked that both reductions are elementwise)
+    fg.zs = (batch->dtype == PYAS_F32 || batch->dtype == PYAS_F64) ? (combine_flags >> 8) & 3u : 0u;
+    combine_flags &= ~(PYAS_FOLD_ZERO_SIGN_MIN | PYAS_FOLD_ZERO_SIGN_MAX);
     int64_t n_pos = 1, ost = 1;
     fg.n_layers = 1;
     fg.n_cols = 1;
@@ -1128,6 +1132,9 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
     if (fg.n_cols * x.d.bpc < min_blocks / 4)
         return fail(PYAS_ENOTSUP, "in-kernel layer fold: %lld workgroups are too few to fill the device",
                     (long long)(fg.n_cols * x.d.bpc));
+    if (fg.zs && !fg.lean)
+        return fail(PYAS_ENOTSUP, "the zero sign is fused into the lean column fold only (this geometry takes "
+                                  "another kernel)");
     x.axes = axes_mask;
     x.out = out;
     x.shuf = shuf;

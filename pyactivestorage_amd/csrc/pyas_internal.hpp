@@ -91,6 +91,7 @@ struct FoldGrid {
     uint32_t flags;                   // PYAS_COMBINE_*
     int32_t lean;                     // column layout: k_axes_fold_lean (split 1, rows % 4 == 0),
                                       // 1 = one lane per column item, 2 = layers split over two
+    uint32_t zs;                      // k_axes_fold_lean: NumPy's zero sign fused for min (1) / max (2)
 };
 
 struct InflateArgs {

@@ -2183,11 +2183,16 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_COL_WAVES) void k_axes
 // NV > 1: the lane walks NV items at once (row-0 byte offsets offs[s],
 // partials in acc[s * N ...]), so a wave's loads of one row cover NV KiB
 // when its items are adjacent.
+struct NoGroupHook {
+    __device__ void operator()(const uint4 *) const {}
+};
+
 template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, bool NT, int NV, typename LB,
-          typename LE>
+          typename LE, typename OG = NoGroupHook>
 __device__ __forceinline__ void col_walk_layers(const AxesDense &d, int64_t n, const int64_t *offs, int64_t l0,
                                                 int64_t n_layers, const MaskT<T> &mk, const LB &layer_base,
-                                                TileAcc<T> *acc, const LE &layer_end) {
+                                                TileAcc<T> *acc, const LE &layer_end,
+                                                const OG &on_group = OG{}) {
     constexpr int N = 16 / sizeof(T), ES = sizeof(T), U = 4;
     const int64_t R = d.RO * d.RI;                      // rows per layer, a multiple of U
     const int64_t step = d.KI * ES;                     // next ri
@@ -2218,6 +2223,7 @@ __device__ __forceinline__ void col_walk_layers(const AxesDense &d, int64_t n, c
     auto consume = [&](const uint4 *buf) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) col_consume<T, BSWAP, MASKED, U>(buf + v * U, acc + v * N, mk);
+        on_group(buf);   // rows u = 0..U-1 of the group, in order (item set 0)
         if (++cg == gpl) {
             cg = 0;
             if constexpr (!MASKED) {
@@ -2252,11 +2258,15 @@ __device__ __forceinline__ void col_walk_layers(const AxesDense &d, int64_t n, c
 // sum is stored at sink[(layer - l0) * sstride + k * IB] instead of being
 // added to w[k].sum (the second half of a split column, added in order by
 // the first half's lane).
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, bool SINK, bool NT, typename LB>
+// ZS: zs[k] tracks output k's last zero in (layer, row) order -- 0 none, 1
+// +0.0, 2 -0.0 (the elementwise rule both NumPy reductions follow when the
+// innermost dim is kept; k_axes_fold_lean writes it to a zero min/max).
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, bool SINK, bool NT, bool ZS,
+          typename LB>
 __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t off0, int64_t l0,
                                           int64_t n_layers, bool round, const MaskT<T> &mk,
                                           const LB &layer_base, WAcc<T> *w,
-                                          typename TT<T>::Acc *sink, int sstride, int IB) {
+                                          typename TT<T>::Acc *sink, int sstride, int IB, uint32_t *zs) {
     constexpr int N = 16 / sizeof(T);
     // acc[k]: the current layer's sum / min / max; its count and NaN flag run
     // over every layer (merge adds counts, and a NaN layer min/max stays NaN
@@ -2282,8 +2292,26 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
             ac[k].mx = TT<T>::lowest();
         }
     };
-    col_walk_layers<T, SHUF, BSWAP, MASKED, AL, DEPTH, NT, 1>(d, n, &off0, l0, n_layers, mk, layer_base, acc,
-                                                             merge_layer);
+    if constexpr (ZS) {
+        // a zero's maskedness is one fact per query (value-based rules), so
+        // the trackers take every zero; a masked zero never makes the min
+        // or max a zero, and only a zero min/max reads them
+        auto track = [&](const uint4 *buf) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                T x[N];
+                unpack16<T, BSWAP>(buf[u], x);
+#pragma unroll
+                for (int k = 0; k < N; ++k)
+                    if (x[k] == (T)0) zs[k] = __builtin_signbit(x[k]) ? 2u : 1u;
+            }
+        };
+        col_walk_layers<T, SHUF, BSWAP, MASKED, AL, DEPTH, NT, 1>(d, n, &off0, l0, n_layers, mk, layer_base, acc,
+                                                                 merge_layer, track);
+    } else {
+        col_walk_layers<T, SHUF, BSWAP, MASKED, AL, DEPTH, NT, 1>(d, n, &off0, l0, n_layers, mk, layer_base, acc,
+                                                                 merge_layer);
+    }
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         w[k].count = (int64_t)acc[k].count;   // host: n_layers * rows < 2^31
@@ -2310,7 +2338,13 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
 // own, in layer order, and folds in the second half's min/max (pmin/pmax,
 // earlier half first), count and NaN.  Either way the arithmetic is
 // k_axes_dense (split 1) + k_combine_grid's: bit-identical.
-template <typename T, bool SHUF, bool BSWAP, int MASKED>
+// ZS (g.zs = which: 1 min, 2 max; the host checks that both NumPy reductions
+// are elementwise, pyas.h PYAS_FOLD_ZERO_SIGN_*): each lane also tracks its
+// outputs' last zero, in layer order then row order, and a zero min/max of
+// the result takes that zero's sign -- what storage.py:99-100 and
+// active.py:594 return when every later zero wins -- so the zero-sign passes
+// (pyas_tie_chunk_flags + pyas_tie_grid) need not re-read the chunks.
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool ZS>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fold_lean(AxesArgs a, FoldGrid g) {
     constexpr int N = 16 / sizeof(T), ES = sizeof(T), IB2 = kBlock / 2;
     using A = typename TT<T>::Acc;
@@ -2366,20 +2400,25 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
     __shared__ A s_sum[kLeanMaxB * N * IB2];      // second half: per-layer sums [layer][k][item]
     __shared__ T s_mn[N * IB2], s_mx[N * IB2];
     __shared__ uint32_t s_cnt[N * IB2];
+    __shared__ uint32_t s_zs[ZS ? N * IB2 : 1];
     A *sink = half ? s_sum + il : nullptr;
     WAcc<T> w[N];
+    uint32_t zs[N];
 #pragma unroll
-    for (int k = 0; k < N; ++k) w[k].init();
+    for (int k = 0; k < N; ++k) {
+        w[k].init();
+        zs[k] = 0;
+    }
     // AL_ / NT_: compile-time aligned walk / non-temporal plane loads
     auto walk = [&](auto al_c, auto nt_c) {
         constexpr bool AL_ = decltype(al_c)::value, NT_ = decltype(nt_c)::value;
         constexpr int DEP = AL_ ? PYAS_LEAN_DEPTH : 1;
         if (half)
-            lean_walk<T, SHUF, BSWAP, MASKED, AL_, DEP, true, NT_>(d, r.chunk_elems, off0, l0, nl, round,
-                                                                 mk, layer_base, w, sink, N * IB, IB);
+            lean_walk<T, SHUF, BSWAP, MASKED, AL_, DEP, true, NT_, ZS>(d, r.chunk_elems, off0, l0, nl, round,
+                                                                     mk, layer_base, w, sink, N * IB, IB, zs);
         else
-            lean_walk<T, SHUF, BSWAP, MASKED, AL_, DEP, false, NT_>(d, r.chunk_elems, off0, l0, nl, round,
-                                                                  mk, layer_base, w, sink, N * IB, IB);
+            lean_walk<T, SHUF, BSWAP, MASKED, AL_, DEP, false, NT_, ZS>(d, r.chunk_elems, off0, l0, nl, round,
+                                                                      mk, layer_base, w, sink, N * IB, IB, zs);
     };
     if (act) {
         bool done = false;
@@ -2405,6 +2444,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
                 s_mn[k * IB + il] = w[k].mn;
                 s_mx[k * IB + il] = w[k].mx;
                 s_cnt[k * IB + il] = (uint32_t)w[k].count;
+                if constexpr (ZS) s_zs[k * IB + il] = zs[k];
             }
         }
         __syncthreads();
@@ -2418,6 +2458,20 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
             w[k].mn = pmin(w[k].mn, s_mn[k * IB + il]);
             w[k].mx = pmax(w[k].mx, s_mx[k * IB + il]);
             w[k].count += (int64_t)s_cnt[k * IB + il];
+            if constexpr (ZS) {   // the second half's layers come later
+                const uint32_t z2 = s_zs[k * IB + il];
+                zs[k] = z2 ? z2 : zs[k];
+            }
+        }
+    }
+    if constexpr (ZS) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const T z = zs[k] == 2u ? -(T)0 : (T)0;
+            if (zs[k] && w[k].count > 0) {
+                if ((g.zs & 1u) && w[k].mn == (T)0) w[k].mn = z;
+                if ((g.zs & 2u) && w[k].mx == (T)0) w[k].mx = z;
+            }
         }
     }
 #pragma unroll
@@ -3814,21 +3868,32 @@ static void launch_fold_row(const AxesArgs &a, const FoldGrid &g, bool masked, d
     else launch_fold_row_s<T, false, H>(a, g, masked, gr, st);
 }
 
-template <typename T, bool SHUF>
-static void launch_fold_lean(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
+template <typename T, bool SHUF, bool ZS>
+static void launch_fold_lean_z(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
     const dim3 blk(kBlock);
     const int mm = mask_mode(a.r.mask, masked);
     if (a.bswap) {
-        if (mm) hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, true, kMaskAll>), gr, blk, 0, st, a, g);
-        else hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, true, 0>), gr, blk, 0, st, a, g);
+        if (mm) hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, true, kMaskAll, ZS>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, true, 0, ZS>), gr, blk, 0, st, a, g);
     } else if (mm == kMaskRange) {
-        hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, kMaskRange>), gr, blk, 0, st, a, g);
+        hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, kMaskRange, ZS>), gr, blk, 0, st, a, g);
     } else if (mm == kMaskNoEq1) {
-        hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, kMaskNoEq1>), gr, blk, 0, st, a, g);
+        hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, kMaskNoEq1, ZS>), gr, blk, 0, st, a, g);
     } else {
-        if (mm) hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, kMaskAll>), gr, blk, 0, st, a, g);
-        else hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, 0>), gr, blk, 0, st, a, g);
+        if (mm) hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, kMaskAll, ZS>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_lean<T, SHUF, false, 0, ZS>), gr, blk, 0, st, a, g);
     }
+}
+
+template <typename T, bool SHUF>
+static void launch_fold_lean(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
+    if constexpr (TT<T>::kind == 0) {   // signed zeros: floats only
+        if (g.zs) {
+            launch_fold_lean_z<T, SHUF, true>(a, g, masked, gr, st);
+            return;
+        }
+    }
+    launch_fold_lean_z<T, SHUF, false>(a, g, masked, gr, st);
 }
 
 template <typename T, bool SHUF>

@@ -150,10 +150,13 @@ def method_rec(method) -> int:
 
 
 def reduce_axes_grid(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, grid: _lib.Grid, out_ptr,
-                     round_to_var: bool, stream) -> None:
+                     round_to_var: bool, stream, zero_sign: int = 0) -> None:
     """pyas_reduce_axes + pyas_combine_grid in one launch (whole chunks);
-    NotImplementedError when the geometry does not admit it."""
-    flags = _lib.COMBINE_ROUND_TO_VAR if round_to_var else 0
+    NotImplementedError when the geometry does not admit it.  ``zero_sign``
+    (1 min, 2 max): NumPy's sign of a zero result fused into the fold
+    (PYAS_FOLD_ZERO_SIGN_*; the caller checks both reductions are
+    elementwise)."""
+    flags = (_lib.COMBINE_ROUND_TO_VAR if round_to_var else 0) | (int(zero_sign) << 8)
     _lib.check(ctx.lib.pyas_reduce_axes_grid(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
                                              ctypes.byref(grid), flags, out_ptr, stream),
                "pyas_reduce_axes_grid")

@@ -263,3 +263,54 @@ def test_strided_full_reduction_sign(gpu, group, monkeypatch):
                     _same_bytes(want, got, (dt, rep, sel, axis))
                     n_cases += 1
     assert n_cases >= 800
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("lean", ["1", "2"])
+@pytest.mark.parametrize("kind", ["min", "max"])
+def test_fused_fold_sign(gpu, dt, lean, kind, monkeypatch):
+    """PYAS_FOLD_ZERO_SIGN_*: where both NumPy reductions are elementwise
+    (innermost dim kept, C order), the lean column fold tracks the last zero
+    itself.  Its bytes must equal the zero-sign passes' (the same query with
+    the fusion refused) and active.py's combine over storage.py's results,
+    for the unsplit and the layer-split lean kernel."""
+    if tie_rule(dt) is None:
+        pytest.skip("no NumPy tie rule derived on this host")
+    monkeypatch.setenv("PYAS_FOLD_LEAN", lean)
+    gpu.set_fold_min_blocks(1)
+    try:
+        rng = np.random.default_rng(17 + len(lean) + len(kind))
+        shape, chunks = (32, 32, 128), (16, 16, 64)
+        a = _chunk(rng, shape, np.dtype(dt), "min0" if kind == "min" else "max0", dens=0.4, n_fill=40)
+        attrs = {"_FillValue": np.array([-999.0], dtype=dt)}
+        missing = (np.dtype(dt).type(-999.0), None, None, None)
+        var, data = _variable(a, chunks, attrs)
+        data_of = lambda cc: data[var.chunk_index[cc][0]: var.chunk_index[cc][0] + var.chunk_index[cc][1]]
+        calls = []
+        real = active_mod.Active._fold
+
+        def spy(self, *args):
+            fused = real(self, *args)
+            calls.append(fused)
+            return fused
+        monkeypatch.setattr(active_mod.Active, "_fold", spy)
+        for axis in ((0,), (1,)):
+            want = _reference_active(a, chunks, (slice(None),) * 3, axis, kind, missing, data_of)
+            for resident in (False, True):
+                act = Active(var, axis=axis, resident=resident)
+                act.method = kind
+                got = act[...]
+                _same_bytes(want, got, (axis, resident, "fused"))
+                if resident:   # the cached replay folds with the fusion again
+                    act.method = kind
+                    _same_bytes(want, act[...], (axis, "replay"))
+            active_mod.release_resident(var)
+        assert calls and all(calls), calls   # the lean kernel took every query with the fusion
+        monkeypatch.setattr(active_mod.Active, "_elementwise_sign", lambda self, axes: False)
+        for axis in ((0,), (1,)):
+            want = _reference_active(a, chunks, (slice(None),) * 3, axis, kind, missing, data_of)
+            act = Active(var, axis=axis)
+            act.method = kind
+            _same_bytes(want, act[...], (axis, "passes"))
+    finally:
+        gpu.set_fold_min_blocks(0)
