@@ -59,8 +59,19 @@ def _variable(shape, chunks, dtype, rng, masked, nan=False, shuffle=False):
     return var, data
 
 
-def _partials(var, axis, index, fold, monkeypatch):
-    """Combined partials of an Active mean query, raw (before formatting)."""
+_FIELDS = {"mean": ["sum", "count"], "min": ["min", "count"], "max": ["max", "count"]}
+
+
+def _same_final(f1, f0, method="mean"):
+    """The fields a method reads of the combined partials, byte for byte (the
+    two-step path's per-chunk records carry only those: pyas_reduce_axes_ex)."""
+    for k in _FIELDS[method]:
+        assert f1[k].tobytes() == f0[k].tobytes(), (method, k)
+
+
+def _partials(var, axis, index, fold, monkeypatch, method="mean"):
+    """Combined partials of an Active query (mean by default), raw (before
+    formatting)."""
     monkeypatch.setattr(active_mod, "_AXES_FOLD", fold)
     calls = []
     real = engine.reduce_axes_grid
@@ -70,7 +81,7 @@ def _partials(var, axis, index, fold, monkeypatch):
         calls.append(1)
     monkeypatch.setattr(engine, "reduce_axes_grid", spy)
     a = Active(var, axis=axis)
-    a.method = "mean"
+    a.method = method
     got = {}
 
     def raw(ctx, st, fin, n, shape):
@@ -122,7 +133,11 @@ def test_fold_matches_two_step(gpu, dtype, masked, case, monkeypatch):
     f1, r1, n1 = _partials(var, axis, index, True, monkeypatch)
     f0, r0, n0 = _partials(var, axis, index, False, monkeypatch)
     assert n1 == 1 and n0 == 0            # the fold ran, then the two-step path
-    assert f1.tobytes() == f0.tobytes()
+    _same_final(f1, f0)
+    for method in ("min", "max"):         # the two-step path's min / max records
+        g1, _, _ = _partials(var, axis, index, True, monkeypatch, method)
+        g0, _, _ = _partials(var, axis, index, False, monkeypatch, method)
+        _same_final(g1, g0, method)
     # and the result against NumPy's masked mean of the selection
     sel = data[index]
     m = np.ma.masked_equal(sel, var.attrs["_FillValue"][0]) if masked else np.ma.MaskedArray(sel)
@@ -148,7 +163,7 @@ def test_fold_shuffled_matches_two_step(gpu, dtype, case, monkeypatch):
     # case 11's 20-element runs are not whole 16-element shuffled load units:
     # the fold refuses and the two-step (generic kernel) path runs
     assert n1 == (0 if case == 11 else 1) and n0 == 0
-    assert f1.tobytes() == f0.tobytes()
+    _same_final(f1, f0)
     rng = np.random.default_rng(case * 7 + len(dtype))
     plain, _ = _variable(shape, chunks, dtype, rng, True, nan=(case in (0, 16)), shuffle=False)
     fp, rp, _ = _partials(plain, axis, index, True, monkeypatch)
@@ -170,7 +185,7 @@ def test_fold_refuses_long_rows(gpu, monkeypatch):
     f, r, n = _partials(var, (2,), np.s_[...], True, monkeypatch)
     assert n == 0
     f0, r0, _ = _partials(var, (2,), np.s_[...], False, monkeypatch)
-    assert f.tobytes() == f0.tobytes()
+    _same_final(f, f0)
 
 
 def test_fold_refuses_too_few_workgroups(gpu, monkeypatch):
@@ -214,7 +229,12 @@ def test_lean_fold_matches_split_fold(gpu, dtype, case, lean, monkeypatch):
     f_two, _, n_two = _partials(var, axis, index, False, monkeypatch)
     assert n_lean == 1 and n_split == 1 and n_two == 0
     assert f_lean.tobytes() == f_split.tobytes()
-    assert f_lean.tobytes() == f_two.tobytes()
+    _same_final(f_lean, f_two)
+    for method in ("min", "max"):         # the two-step path's min / max records
+        monkeypatch.setenv("PYAS_FOLD_LEAN", lean)
+        g_lean, _, _ = _partials(var, axis, index, True, monkeypatch, method)
+        g_two, _, _ = _partials(var, axis, index, False, monkeypatch, method)
+        _same_final(g_lean, g_two, method)
 
 
 def _rewrite(var, data):
