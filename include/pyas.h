@@ -395,15 +395,21 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
                           const pyas_grid *grid, uint32_t combine_flags, pyas_partial *out,
                           void *stream);
 /* combine_flags of pyas_reduce_axes_grid: NumPy's sign of a zero min (MIN)
- * or max (MAX), fused into the fold.  Valid only where both reductions NumPy
- * runs are elementwise, which the caller checks: the chunks' innermost dim
- * in memory and the `out` array's innermost dim (active.py:594) are kept
- * dims, so storage.py:99-100 and active.py:594 let every later zero win.
- * Each lane then tracks its outputs' last zero (layer order, then row order)
- * and writes that zero's sign to a zero result: pyas_tie_chunk_flags and
- * pyas_tie_grid are not needed.  Float dtypes; PYAS_ENOTSUP (nothing
- * launched) when the geometry takes a kernel other than the lean column
- * fold -- fold without the flag and run the zero-sign passes then. */
+ * or max (MAX), fused into the fold, so pyas_tie_chunk_flags and
+ * pyas_tie_grid are not needed.  The caller checks that the chunks are
+ * C-ordered (NumPy reduces chunk[sel] in memory order, storage.py:99-100);
+ * the library derives both NumPy calls from the geometry:
+ *  - lean column fold (innermost dim kept): valid where both reductions are
+ *    elementwise (the chunks' innermost non-1 dim and the `out` array's,
+ *    active.py:594, are kept) -- every later zero wins, and each lane tracks
+ *    its outputs' last zero (layer order, then row order);
+ *  - LDS row fold (modes 4-6, each output row one contiguous call): the
+ *    context's tie rule (pyas_ctx_set_tie_rule) keys the zeros of a row
+ *    whose min/max is a zero, and the row's sign is keyed at its layer's
+ *    position in the `out` array's call (MIN or MAX, not both).
+ * Float dtypes; PYAS_ENOTSUP (nothing launched) when the geometry takes
+ * another fold kernel, a reduction the kernel cannot key, or no rule is set:
+ * fold without the flag and run the zero-sign passes then. */
 #define PYAS_FOLD_ZERO_SIGN_MIN 0x100u
 #define PYAS_FOLD_ZERO_SIGN_MAX 0x200u
 

@@ -824,7 +824,7 @@ class Active:
         g.chunk_out_offsets = abuf.ptr
         fin = DeviceBuffer(ctx, max(n_final, 1) * _lib.PARTIAL_NBYTES)
         folded = fused = False
-        zs_ok = self._elementwise_sign(axes)
+        zs_ok = self._fold_sign_ok(axes)
         if (_AXES_FOLD and lo == 0 and hi == n_all and not plan.batch.sel
                 and self._whole_chunk_grid(tables, final_shape, axes)):
             try:   # one launch: chunk layers folded inside the reduction kernel
@@ -870,27 +870,24 @@ class Active:
         ctx.synchronize(st)
         return final
 
-    def _elementwise_sign(self, axes) -> bool:
-        """Whether NumPy's zero sign of this partial-axis query is "the last
-        zero wins" at both levels: the chunks are C-ordered with their
-        innermost dim kept (storage.py:99-100 reduces elementwise), and so is
-        the `out` array's innermost dim (active.py:594).  Then the in-kernel
-        fold can track it (PYAS_FOLD_ZERO_SIGN_*), if this host's NumPy rule
-        is known at all."""
+    def _fold_sign_ok(self, axes) -> bool:
+        """Whether the fold may fuse NumPy's zero sign of this partial-axis
+        query (PYAS_FOLD_ZERO_SIGN_*): a float variable with C-ordered chunks
+        (storage.py:99-100 then reduces each chunk in the memory order the
+        kernels assume) and this host's NumPy rule known.  The library
+        refuses (ENOTSUP) the geometries its fold kernels cannot key."""
         ds = self.ds
-        nd = ds.ndim
-        if ds.dtype.kind != "f" or getattr(ds, "order", "C") != "C" or (nd - 1) in axes:
-            return False
-        if ds.chunks[nd - 1] < 2:
+        if ds.dtype.kind != "f" or getattr(ds, "order", "C") != "C":
             return False
         ctx = get_context(self.device)
         return bool(getattr(ctx, "tie_signs_exact", {}).get("f4" if ds.dtype.itemsize == 4 else "f8"))
 
     def _fold(self, ctx, st, plan, g, fin_ptr, zs_ok) -> bool:
         """pyas_reduce_axes_grid, with NumPy's zero sign fused in when the
-        query allows it (min/max of a float variable, elementwise at both
-        levels) and the lean column fold takes the geometry.  Returns
-        whether the sign was fused (else the zero-sign passes run)."""
+        query allows it (min/max of a float variable, _fold_sign_ok) and the
+        fold kernel the geometry takes can key it (the lean column fold with
+        both reductions elementwise, or the LDS row fold).  Returns whether
+        the sign was fused (else the zero-sign passes run)."""
         which = self._tie_which() if zs_ok else 0
         if which:
             try:

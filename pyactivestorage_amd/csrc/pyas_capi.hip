@@ -1132,9 +1132,44 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
     if (fg.n_cols * x.d.bpc < min_blocks / 4)
         return fail(PYAS_ENOTSUP, "in-kernel layer fold: %lld workgroups are too few to fill the device",
                     (long long)(fg.n_cols * x.d.bpc));
-    if (fg.zs && !fg.lean)
-        return fail(PYAS_ENOTSUP, "the zero sign is fused into the lean column fold only (this geometry takes "
-                                  "another kernel)");
+    if (fg.zs) {
+        // level 2: the `out` array (C-ordered, active.py:512) reduced over the
+        // chunk-grid dims -- its call is the trailing reduced group
+        // (zerosign.grid_lr)
+        int64_t lr2 = 1;
+        for (int d = batch->ndim - 1; d >= 0; --d) {
+            const bool red = (axes_mask >> d) & 1u;
+            const int64_t ext = red ? g->n_coords[d] : g->out_extent[d];
+            if (ext == 1) continue;
+            if (!red) break;
+            lr2 *= ext;
+        }
+        if (fg.lean) {
+            // the lean fold tracks "the last zero wins": both reductions
+            // elementwise (the chunk's innermost non-1 dim kept, lr2 == 1)
+            bool inner_kept = false;
+            for (int d = batch->ndim - 1; d >= 0; --d) {
+                if (batch->chunk_shape[d] == 1) continue;
+                inner_kept = !((axes_mask >> d) & 1u);
+                break;
+            }
+            if (!inner_kept || lr2 != 1)
+                return fail(PYAS_ENOTSUP, "zero sign in the lean column fold: a reduction is not elementwise");
+        } else if (x.d.mode >= 4) {
+            // LDS row layout: each output row (RI elements, RO == KI == 1) is
+            // one contiguous NumPy call; the rule comes from the context
+            const pyas::TieRule *t = tie_of(ctx, batch->dtype);
+            if (!t) return fail(PYAS_ENOTSUP, "zero sign in the row fold: no tie rule set for this dtype");
+            if (fg.zs == 3u) return fail(PYAS_ENOTSUP, "zero sign in the row fold: min or max, not both");
+            if (x.d.RI - 1 >= t->piece || lr2 >= (int64_t(1) << 31))
+                return fail(PYAS_ENOTSUP, "zero sign in the row fold: call longer than NumPy's buffer");
+            fg.t = *t;
+            fg.c2 = grid_call(*t, lr2);
+        } else {
+            return fail(PYAS_ENOTSUP, "the zero sign is fused into the lean column and the row folds only (this "
+                                      "geometry takes k_axes_fold)");
+        }
+    }
     x.axes = axes_mask;
     x.out = out;
     x.shuf = shuf;

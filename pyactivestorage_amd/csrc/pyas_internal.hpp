@@ -83,16 +83,8 @@ struct AxesArgs {
 // per-thread fold (k_combine_grid) for every layer count
 constexpr uint32_t kCombineThreadOnly = 1u << 31;
 constexpr int kLeanMaxB = 8;         // k_axes_fold_lean: layers of a split column's second half (LDS sums)
+struct FoldGrid;                     // below, after the tie structs it carries
 
-struct FoldGrid {
-    int64_t n_coords[PYAS_MAX_DIMS];  // chunk coordinates per dim (chunk n = C-order position)
-    int64_t ostride[PYAS_MAX_DIMS];   // final-output element strides (kept dims)
-    int64_t n_layers, n_cols;         // chunks along the reduced dims / kept dims
-    uint32_t flags;                   // PYAS_COMBINE_*
-    int32_t lean;                     // column layout: k_axes_fold_lean (split 1, rows % 4 == 0),
-                                      // 1 = one lane per column item, 2 = layers split over two
-    uint32_t zs;                      // k_axes_fold_lean: NumPy's zero sign fused for min (1) / max (2)
-};
 
 struct InflateArgs {
     const uint8_t *src;
@@ -154,6 +146,17 @@ struct TieCall {
     uint32_t block;                   // acc: kept dims of NumPy's copied first buffer fill
     int64_t lr, npr;                  // call length (1: elementwise), pieces per call
     int64_t n_copy;                   // acc: runs of that fill (contiguous calls), 0: none
+};
+struct FoldGrid {
+    int64_t n_coords[PYAS_MAX_DIMS];  // chunk coordinates per dim (chunk n = C-order position)
+    int64_t ostride[PYAS_MAX_DIMS];   // final-output element strides (kept dims)
+    int64_t n_layers, n_cols;         // chunks along the reduced dims / kept dims
+    uint32_t flags;                   // PYAS_COMBINE_*
+    int32_t lean;                     // column layout: k_axes_fold_lean (split 1, rows % 4 == 0),
+                                      // 1 = one lane per column item, 2 = layers split over two
+    uint32_t zs;                      // NumPy's zero sign fused for min (1) / max (2)
+    TieRule t;                        // zs in k_axes_fold_row: the host's rule,
+    TieCall c2;                       //   and the `out` array's call (level 2)
 };
 struct TieChunkArgs {
     ReduceArgs r;

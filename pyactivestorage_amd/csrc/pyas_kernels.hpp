@@ -2734,6 +2734,43 @@ __global__ __launch_bounds__(kBlock) void k_axes_shuf_slab(AxesArgs a) {
     }
 }
 
+// NumPy's zero sign (defined with the tie passes below; key layout there)
+constexpr uint64_t kTieWNone = ~0ull;
+constexpr int kTieOffBits = 24;
+constexpr uint32_t kTieRemRank = 127;
+__device__ __forceinline__ void tie_keys(int64_t e, uint64_t sg, const TieCall &c, const TieRule &t, bool lanes,
+                                         uint64_t &k1, uint64_t &w, uint64_t &ka);
+__device__ __forceinline__ int tie_finalize(uint64_t k1, uint64_t w, uint64_t ka, const TieCall &c,
+                                            const TieRule &t);
+
+// tie_keys of a zero at position e of ONE contiguous call of a row's m + 1
+// elements (the seed e = 0, then m elements; m < piece, so one row): 32-bit
+// keys, W without its row field.  nv = m - m % L (L = lanes, a power of 2).
+__device__ __forceinline__ void row_tie_keys(uint32_t e, uint32_t sg, uint32_t nv, uint32_t L,
+                                             const uint8_t *rank, uint32_t &k1, uint32_t &w) {
+    if (e == 0) {
+        k1 = k1 > (2u | sg) ? k1 : (2u | sg);
+        w = w < sg ? w : sg;
+        return;
+    }
+    const uint32_t off = e - 1;
+    const bool vec = off < nv;
+    const uint32_t rk = vec ? (uint32_t)rank[off & (L - 1)] : kTieRemRank;
+    const uint32_t x1 = (!vec || rk == 0) ? (((e + 1) << 1) | sg) : 0u;
+    const uint32_t xw = (rk << 25) | ((((1u << kTieOffBits) - 1) - off) << 1) | sg;
+    k1 = x1 > k1 ? x1 : k1;
+    w = xw < w ? xw : w;
+}
+
+// tie_finalize of row_tie_keys' keys (at least one zero seen)
+__device__ __forceinline__ uint32_t row_tie_sign(uint32_t k1, uint32_t w) {
+    if (k1 == 0) return w & 1u;
+    if (w == 0xFFFFFFFFu) return k1 & 1u;
+    const uint32_t e1 = (k1 >> 1) - 1;
+    const uint32_t ew = w < 2 ? 0u : 1u + (((1u << kTieOffBits) - 1) - ((w >> 1) & ((1u << kTieOffBits) - 1)));
+    return ew > e1 ? (w & 1u) : (k1 & 1u);
+}
+
 // Whole-chunk box query, LDS row layout (modes 4/5/6), chunk layers folded
 // in the kernel (pyas_reduce_axes_grid).  Block (col, j), wave w owns the
 // output tiles j*4 + w, + 4*bpc, ... of kept-dims chunk column `col`; for
@@ -2742,11 +2779,24 @@ __global__ __launch_bounds__(kBlock) void k_axes_shuf_slab(AxesArgs a) {
 // does, then merges the partial store_group would write into a running WAcc
 // (k_combine_grid's merge, same rounding).  Bit-identical to k_axes_dense +
 // k_combine_grid; the next layer's tile is loaded while this one is folded.
-template <typename T, bool SHUF, bool BSWAP, int MASKED, int H>
+// ZS (g.zs = which: 1 min, 2 max): NumPy's sign of a zero min/max fused in.
+// Each output row of a chunk is ONE contiguous reduce call of NumPy's
+// (storage.py:99-100 over a C-ordered chunk whose trailing reduced group is
+// the row; tie rule g.t): when a layer's row min/max is a zero, the row's
+// H lanes key its zeros from the tile still in LDS (row_tie_keys), and the
+// row's winning sign is keyed at position l of the `out` array's call g.c2
+// (active.py:594, tie_keys); the output's zero min/max takes the sign those
+// level-2 keys give.  Zero-free layers cost one ballot.
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int H, bool ZS>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes_fold_row(AxesArgs a, FoldGrid g) {
     constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
     constexpr int UL = 16 / H / VPL > 0 ? 16 / H / VPL : 1;   // load units per lane per tile
     __shared__ uint4 tile[(kBlock / kWave) * RPW * kRowLdsStride];
+    __shared__ uint8_t s_rank[ZS ? 64 : 1];
+    if constexpr (ZS) {
+        if (threadIdx.x < 64) s_rank[threadIdx.x] = g.t.rank[threadIdx.x];
+        __syncthreads();
+    }
     const AxesDense &d = a.d;
     const ReduceArgs &r = a.r;
     const int64_t col = blockIdx.x / d.bpc;
@@ -2814,6 +2864,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
         const int64_t nvec = (d.KO - o0 < RPW ? d.KO - o0 : RPW) * V;
         WAcc<T> wacc;
         wacc.init();
+        uint64_t zk1 = 0, zkw = kTieWNone;   // ZS: level-2 keys of the row's zero layers
         load(layer_base(0), o0, nvec);
         for (int64_t l = 0; l < g.n_layers; ++l) {
 #pragma unroll
@@ -2834,13 +2885,54 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
             }
             if constexpr (!MASKED) acc.count += (uint32_t)(VH * N);
             uint32_t cnt, nan;
-            group_reduce(acc, H, cnt, nan);
+            group_reduce(acc, H, cnt, nan);   // every lane of the row holds the row's result
+            if constexpr (ZS) {
+                const T v = (g.zs & 1u) ? acc.mn : acc.mx;
+                const bool z = cnt > 0 && !nan && v == (T)0;
+                if (__ballot(z)) {
+                    const uint32_t L = (uint32_t)g.t.lanes, m = (uint32_t)d.RI - 1u, nv = m & ~(L - 1u);
+                    uint32_t k1 = 0, kw = 0xFFFFFFFFu;
+                    if (z) {
+                        // a masked zero never makes the min/max a zero (value
+                        // rules: zeros are masked all or none), so every zero keys
+                        for (int i = 0; i < VH; ++i) {
+                            T x[N];
+                            unpack16<T, BSWAP>(row[i], x);
+#pragma unroll
+                            for (int k = 0; k < N; ++k)
+                                if (x[k] == (T)0)
+                                    row_tie_keys((uint32_t)((h * VH + i) * N + k), __builtin_signbit(x[k]) ? 1u : 0u,
+                                                 nv, L, s_rank, k1, kw);
+                        }
+                    }
+#pragma unroll
+                    for (int mm = H / 2; mm >= 1; mm >>= 1) {   // the row's H lanes
+                        const uint32_t o1 = __shfl_xor(k1, mm), ow = __shfl_xor(kw, mm);
+                        k1 = o1 > k1 ? o1 : k1;
+                        kw = ow < kw ? ow : kw;
+                    }
+                    if (z && h == 0) {
+                        uint64_t x1, xw, xa;
+                        tie_keys(l, row_tie_sign(k1, kw), g.c2, g.t, true, x1, xw, xa);
+                        zk1 = x1 > zk1 ? x1 : zk1;
+                        zkw = xw < zkw ? xw : zkw;
+                    }
+                }
+            }
             if (h == 0) {
                 pyas_partial pp;
                 store_group(acc, cnt, nan, &pp);
                 merge(wacc, pp, round);
             }
             wave_sync_lds();
+        }
+        if constexpr (ZS) {
+            if (h == 0 && wacc.count > 0 && (zk1 != 0 || zkw != kTieWNone)) {
+                const int sg = tie_finalize(zk1, zkw, 0, g.c2, g.t);
+                const T zz = sg == 1 ? -(T)0 : (T)0;
+                if ((g.zs & 1u) && wacc.mn == (T)0) wacc.mn = zz;
+                if ((g.zs & 2u) && wacc.mx == (T)0) wacc.mx = zz;
+            }
         }
         if (h == 0 && o0 + rw < d.KO) {
             int64_t loc = o0 + rw, f = 0;   // kept-dims index in the chunk -> final element
@@ -2937,9 +3029,7 @@ __global__ __launch_bounds__(kBlock) void k_select(SelectArgs a) {
 //                         (the seed: sign alone; none: kTieWNone)
 //   K1, strided loop    : (call + 1) << 33 | remainder << 32 | acc priority << 25 | off << 1 | sign
 //                         (the seed: 2 | sign)
-constexpr uint64_t kTieWNone = ~0ull;
-constexpr int kTieOffBits = 24;
-constexpr uint32_t kTieRemRank = 127;
+// (kTieWNone, kTieOffBits, kTieRemRank: defined above k_axes_fold_row)
 
 // Call structure (zerosign.call_structure): cnt/vstride per dim in elements,
 // perm = iteration order (outer -> inner).  lr = 1: elementwise calls.  A
@@ -3845,27 +3935,34 @@ hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hip
     return hipGetLastError();
 }
 
-template <typename T, bool SHUF, int H>
+template <typename T, bool SHUF, int H, bool ZS>
 static void launch_fold_row_s(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
     const dim3 blk(kBlock);
     const int mm = mask_mode(a.r.mask, masked);
     if (a.bswap) {
-        if (mm) hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, true, kMaskAll, H>), gr, blk, 0, st, a, g);
-        else hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, true, 0, H>), gr, blk, 0, st, a, g);
+        if (mm) hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, true, kMaskAll, H, ZS>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, true, 0, H, ZS>), gr, blk, 0, st, a, g);
     } else if (mm == kMaskRange) {
-        hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, kMaskRange, H>), gr, blk, 0, st, a, g);
+        hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, kMaskRange, H, ZS>), gr, blk, 0, st, a, g);
     } else if (mm == kMaskNoEq1) {
-        hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, kMaskNoEq1, H>), gr, blk, 0, st, a, g);
+        hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, kMaskNoEq1, H, ZS>), gr, blk, 0, st, a, g);
     } else {
-        if (mm) hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, kMaskAll, H>), gr, blk, 0, st, a, g);
-        else hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, 0, H>), gr, blk, 0, st, a, g);
+        if (mm) hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, kMaskAll, H, ZS>), gr, blk, 0, st, a, g);
+        else hipLaunchKernelGGL((k_axes_fold_row<T, SHUF, false, 0, H, ZS>), gr, blk, 0, st, a, g);
     }
 }
 
 template <typename T, int H>
 static void launch_fold_row(const AxesArgs &a, const FoldGrid &g, bool masked, dim3 gr, hipStream_t st) {
-    if (a.shuf) launch_fold_row_s<T, true, H>(a, g, masked, gr, st);
-    else launch_fold_row_s<T, false, H>(a, g, masked, gr, st);
+    if constexpr (TT<T>::kind == 0) {   // signed zeros: floats only
+        if (g.zs) {
+            if (a.shuf) launch_fold_row_s<T, true, H, true>(a, g, masked, gr, st);
+            else launch_fold_row_s<T, false, H, true>(a, g, masked, gr, st);
+            return;
+        }
+    }
+    if (a.shuf) launch_fold_row_s<T, true, H, false>(a, g, masked, gr, st);
+    else launch_fold_row_s<T, false, H, false>(a, g, masked, gr, st);
 }
 
 template <typename T, bool SHUF, bool ZS>

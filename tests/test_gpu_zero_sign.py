@@ -306,11 +306,68 @@ def test_fused_fold_sign(gpu, dt, lean, kind, monkeypatch):
                     _same_bytes(want, act[...], (axis, "replay"))
             active_mod.release_resident(var)
         assert calls and all(calls), calls   # the lean kernel took every query with the fusion
-        monkeypatch.setattr(active_mod.Active, "_elementwise_sign", lambda self, axes: False)
+        monkeypatch.setattr(active_mod.Active, "_fold_sign_ok", lambda self, axes: False)
         for axis in ((0,), (1,)):
             want = _reference_active(a, chunks, (slice(None),) * 3, axis, kind, missing, data_of)
             act = Active(var, axis=axis)
             act.method = kind
             _same_bytes(want, act[...], (axis, "passes"))
+    finally:
+        gpu.set_fold_min_blocks(0)
+
+
+ROW_FOLD_CASES = [   # (shape, chunks, axis): each output row of a chunk one contiguous NumPy call
+    ((32, 64, 128), (16, 32, 32), (2,)),     # the innermost dim; `out` call over 4 layers
+    ((32, 64, 128), (16, 4, 8), (1, 2)),     # a two-dim trailing group (32); `out` call of 16 x 16
+    ((32, 64, 128), (1, 16, 32), (0, 2)),    # extent-1 reduced dim; `out`: 32 runs of 4 layers
+    ((32, 32, 4), (16, 16, 1), (1,)),        # extent-1 kept innermost dim: `out` elementwise
+]
+
+
+@pytest.mark.parametrize("dt", ["<f4", ">f4", "<f8"])
+@pytest.mark.parametrize("row_lds", ["1", "2", "4"])
+@pytest.mark.parametrize("dens", [0.4, 0.03])
+@pytest.mark.parametrize("kind", ["min", "max"])
+@pytest.mark.parametrize("case", range(len(ROW_FOLD_CASES)))
+def test_fused_row_fold_sign(gpu, dt, row_lds, dens, kind, case, monkeypatch):
+    """PYAS_FOLD_ZERO_SIGN_* in the LDS row fold (k_axes_fold_row, 1, 2 or 4
+    lanes per row): each row whose min/max is a zero is keyed by the host's
+    NumPy rule from the tile in LDS, and its sign at its layer's position in
+    the `out` array's call.  Bytes equal active.py's combine over
+    storage.py's results and the zero-sign passes' (the fusion refused)."""
+    if tie_rule(dt) is None:
+        pytest.skip("no NumPy tie rule derived on this host")
+    monkeypatch.setenv("PYAS_ROW_LDS", row_lds)
+    gpu.set_fold_min_blocks(1)
+    try:
+        shape, chunks, axis = ROW_FOLD_CASES[case]
+        rng = np.random.default_rng(case * 31 + len(dt) + int(row_lds) + int(dens * 100) + len(kind))
+        a = _chunk(rng, shape, np.dtype(dt), "min0" if kind == "min" else "max0", dens=dens, n_fill=60)
+        attrs = {"_FillValue": np.array([-999.0], dtype=dt)}
+        missing = (np.dtype(dt).type(-999.0), None, None, None)
+        var, data = _variable(a, chunks, attrs)
+        data_of = lambda cc: data[var.chunk_index[cc][0]: var.chunk_index[cc][0] + var.chunk_index[cc][1]]
+        calls = []
+        real = active_mod.Active._fold
+
+        def spy(self, *args):
+            fused = real(self, *args)
+            calls.append(fused)
+            return fused
+        monkeypatch.setattr(active_mod.Active, "_fold", spy)
+        want = _reference_active(a, chunks, (slice(None),) * 3, axis, kind, missing, data_of)
+        for resident in (False, True):
+            act = Active(var, axis=axis, resident=resident)
+            act.method = kind
+            _same_bytes(want, act[...], (axis, resident, "fused"))
+            if resident:   # the cached replay folds with the fusion again
+                act.method = kind
+                _same_bytes(want, act[...], (axis, "replay"))
+        active_mod.release_resident(var)
+        assert calls and all(calls), calls   # the row kernel took the fusion every time
+        monkeypatch.setattr(active_mod.Active, "_fold_sign_ok", lambda self, axes: False)
+        act = Active(var, axis=axis)
+        act.method = kind
+        _same_bytes(want, act[...], (axis, "passes"))
     finally:
         gpu.set_fold_min_blocks(0)
