@@ -3411,8 +3411,8 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
 #pragma unroll
             for (int j = 0; j < PYAS_MAX_DIMS; ++j) {
                 if (j < nk) {
-                    const uint32_t kcj = S.kc[j], q = oo / kcj, k = oo - q * kcj;
-                    oo = q;
+                    const uint32_t kcj = S.kc[j], q = j + 1 < nk ? oo / kcj : 0u, k = oo - q * kcj;
+                    oo = q;   // (the last kept slot needs no division: oo < its count)
                     if ((S.kin >> j) & 1u) bidx += (int64_t)k * S.kbw[j];
                     else beyond |= k != 0;
                     const int64_t idx = S.ksp[j] != 0 ? (int64_t)S.kst[j] + (int64_t)k * S.ksp[j]
@@ -3442,8 +3442,8 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
 #pragma unroll
                     for (int i = 0; i < PYAS_MAX_DIMS; ++i) {
                         if (i < nr) {
-                            const uint32_t q = rr / rc[i], k = rr - q * rc[i];
-                            rr = q;
+                            const uint32_t q = i + 1 < nr ? rr / rc[i] : 0u, k = rr - q * rc[i];
+                            rr = q;   // (the last slot needs no division: rr < its count)
                             const int64_t idx = rsp[i] != 0 ? (int64_t)rst[i] + (int64_t)k * rsp[i]
                                                             : (int64_t)r.pool[(int64_t)rst[i] + k];
                             o[j].mem += idx * rcs[i];
