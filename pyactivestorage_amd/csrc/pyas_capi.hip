@@ -1163,8 +1163,18 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
             if (fg.zs == 3u) return fail(PYAS_ENOTSUP, "zero sign in the row fold: min or max, not both");
             if (x.d.RI - 1 >= t->piece || lr2 >= (int64_t(1) << 31))
                 return fail(PYAS_ENOTSUP, "zero sign in the row fold: call longer than NumPy's buffer");
+            if (x.d.RI > 64) return fail(PYAS_ENOTSUP, "zero sign in the row fold: rows over 64 elements");
             fg.t = *t;
             fg.c2 = grid_call(*t, lr2);
+            // the row call's positions as bit masks: e = 0 the seed, then
+            // m = RI - 1 elements, the first nv in L lanes, the rest remainder
+            const int64_t m = x.d.RI - 1, L = t->lanes, nv = m - m % L;
+            for (int64_t e = nv + 1; e < x.d.RI; ++e) fg.zrow_rem |= uint64_t(1) << e;
+            for (int64_t e = 1; e <= nv; ++e) {
+                const int r = t->rank[(e - 1) % L];
+                fg.zrow_cm[r] |= uint64_t(1) << e;
+                if (r == 0) fg.zrow_top |= uint64_t(1) << e;
+            }
         } else {
             return fail(PYAS_ENOTSUP, "the zero sign is fused into the lean column and the row folds only (this "
                                       "geometry takes k_axes_fold)");

@@ -156,7 +156,9 @@ struct FoldGrid {
                                       // 1 = one lane per column item, 2 = layers split over two
     uint32_t zs;                      // NumPy's zero sign fused for min (1) / max (2)
     TieRule t;                        // zs in k_axes_fold_row: the host's rule,
-    TieCall c2;                       //   and the `out` array's call (level 2)
+    TieCall c2;                       //   the `out` array's call (level 2), and masks over a
+    uint64_t zrow_rem, zrow_top;      //   row's positions e (RI <= 64): remainder, top-priority lane,
+    uint64_t zrow_cm[64];             //   lane-rank classes (zrow_cm[r]: the lane of rank r)
 };
 struct TieChunkArgs {
     ReduceArgs r;

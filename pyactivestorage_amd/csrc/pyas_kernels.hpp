@@ -2582,7 +2582,8 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_STREAM_WAVES) void k_axes_c
 // rows of its output columns ki = lane + 64 q from LDS in 4-row groups,
 // exactly col_rows_ring's arithmetic (same groups, order and counts), so the
 // partials equal dense_col's bit for bit.  The next slab's plane loads are
-// in flight (registers) while the current one is reduced from LDS.  Waves
+// issued piece by piece as this slab's pieces are transposed (one rolling
+// register buffer), and are in flight while it is reduced from LDS.  Waves
 // are persistent: wave gw of TW takes units (chunk, ko) gw, gw + TW, ...
 // (adjacent waves read adjacent slabs).  Round 3's dword-plane walks ran this
 // geometry at 58 % of 8 TB/s: their loads are 64-B pieces of 4 rows.
@@ -2608,35 +2609,53 @@ __global__ __launch_bounds__(kBlock) void k_axes_shuf_slab(AxesArgs a) {
     const T *tv = reinterpret_cast<const T *>(tile);
     MaskT<T> mk;
     mk.init(r.mask);
+    // One rolling register buffer: as soon as piece m of a slab has been
+    // transposed into LDS, the next slab's piece m is loaded into the same
+    // registers, so a wave keeps (MM - 1) x ES loads in flight through the
+    // transposes and all MM x ES of the next slab through the reduction.
+    // (Round 4's first form issued the next slab only after the whole
+    // transpose, leaving the wave without loads in flight meanwhile.)
     uint4 pl[MM][ES];
-    bool al = true;
-    // issue the plane loads of sub-slab s of unit u (16-B pieces; AL per chunk)
-    auto load = [&](int64_t u, int64_t s) {
+    // wave-uniform base of sub-slab s of unit u (scalar registers) and its
+    // alignment; a lane adds its 16-B offset and an immediate per piece
+    auto slab_base = [&](int64_t u, int64_t s) {
         const int64_t c = u / d.KO, ko = u - c * d.KO;
-        const uint8_t *base = r.data + sload(r.offsets + c);
-        al = ((((uintptr_t)base) | (uint64_t)n) & 15) == 0;    // wave-uniform
-        const int64_t e0 = (ko * RI + s * RB) * KI + 16 * lane;
+        return r.data + sload(r.offsets + c) + (ko * RI + s * RB) * KI;
+    };
+    const uint32_t lo = 16u * (uint32_t)lane;
+    // piece m's ES plane loads (pieces m >= M re-read piece 0, never used:
+    // every path issues the same loads, so each wait leaves exactly the
+    // younger ones in flight)
+    // (one load form for aligned and unaligned chunks: a branch per piece
+    // made the compiler's waits drain every load in flight)
+    auto load_piece = [&](const uint8_t *sb, int m) {
+        const int mm = m < M ? m : 0;
 #pragma unroll
-        for (int m = 0; m < MM; ++m) {
-            if (m < M) {
-#pragma unroll
-                for (int b = 0; b < ES; ++b) {
-                    const uint8_t *q = base + b * n + e0 + m * 1024;
-                    pl[m][b] = al ? ld16<true>(q) : ld16<false>(q);
-                }
-            }
-        }
+        for (int b = 0; b < ES; ++b) pl[m][b] = ld16<false>(sb + b * n + lo + mm * 1024);
     };
     TileAcc<T> acc[KPL];
 #pragma unroll
     for (int q = 0; q < KPL; ++q) acc[q].init();
     int64_t u = gw, s = 0;
-    if (u < units) load(u, 0);
+    if (u < units) {
+        const uint8_t *sb0 = slab_base(u, 0);
+#pragma unroll
+        for (int m = 0; m < MM; ++m) load_piece(sb0, m);
+    }
     while (u < units) {   // wave-uniform
-        // plane bytes -> plain elements (raw byte order) -> LDS
+        const int64_t cu = u, cs = s;
+        if (++s == NS) {
+            s = 0;
+            u += TW;
+        }
+        // the next sub-slab (past the last unit: this one again, never used)
+        const uint8_t *sbn = u < units ? slab_base(u, s) : slab_base(cu, cs);
+        // plane bytes -> plain elements (raw byte order) -> LDS, piece by
+        // piece (pieces m >= M too: rows past RB of the tile, never read --
+        // no branch, so the waits stay exact)
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
-            if (m < M) {
+            {
                 uint4 v[ES];
                 if constexpr (ES == 4) {
 #pragma unroll
@@ -2656,24 +2675,24 @@ __global__ __launch_bounds__(kBlock) void k_axes_shuf_slab(AxesArgs a) {
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        uint32_t lo[4], hi[4];
-                        transpose4(word(pl[m][0], j), word(pl[m][1], j), word(pl[m][2], j), word(pl[m][3], j), lo);
-                        transpose4(word(pl[m][4], j), word(pl[m][5], j), word(pl[m][6], j), word(pl[m][7], j), hi);
-                        v[2 * j] = make_uint4(lo[0], hi[0], lo[1], hi[1]);
-                        v[2 * j + 1] = make_uint4(lo[2], hi[2], lo[3], hi[3]);
+                        uint32_t lo4[4], hi4[4];
+                        transpose4(word(pl[m][0], j), word(pl[m][1], j), word(pl[m][2], j), word(pl[m][3], j), lo4);
+                        transpose4(word(pl[m][4], j), word(pl[m][5], j), word(pl[m][6], j), word(pl[m][7], j), hi4);
+                        v[2 * j] = make_uint4(lo4[0], hi4[0], lo4[1], hi4[1]);
+                        v[2 * j + 1] = make_uint4(lo4[2], hi4[2], lo4[3], hi4[3]);
                     }
                 }
 #pragma unroll
                 for (int b = 0; b < ES; ++b) tile[(m * 64 + lane) * ES + b] = v[b];
             }
+            // piece m of the next sub-slab, into the freed registers; the
+            // scheduling fences keep the pieces' loads in this order (the
+            // scheduler would otherwise regroup them and the waits with them)
+            __builtin_amdgcn_sched_barrier(0);
+            load_piece(sbn, m);
+            __builtin_amdgcn_sched_barrier(0);
         }
         wave_sync_lds();
-        const int64_t cu = u, cs = s;
-        if (++s == NS) {
-            s = 0;
-            u += TW;
-        }
-        if (u < units) load(u, s);   // the next slab's loads fly while this one is reduced
         // rows of this sub-slab, output columns ki = lane + 64 q, 4-row groups
         int64_t rr = 0;
         for (; rr + 4 <= RB; rr += 4) {
@@ -2743,33 +2762,7 @@ __device__ __forceinline__ void tie_keys(int64_t e, uint64_t sg, const TieCall &
 __device__ __forceinline__ int tie_finalize(uint64_t k1, uint64_t w, uint64_t ka, const TieCall &c,
                                             const TieRule &t);
 
-// tie_keys of a zero at position e of ONE contiguous call of a row's m + 1
-// elements (the seed e = 0, then m elements; m < piece, so one row): 32-bit
-// keys, W without its row field.  nv = m - m % L (L = lanes, a power of 2).
-__device__ __forceinline__ void row_tie_keys(uint32_t e, uint32_t sg, uint32_t nv, uint32_t L,
-                                             const uint8_t *rank, uint32_t &k1, uint32_t &w) {
-    if (e == 0) {
-        k1 = k1 > (2u | sg) ? k1 : (2u | sg);
-        w = w < sg ? w : sg;
-        return;
-    }
-    const uint32_t off = e - 1;
-    const bool vec = off < nv;
-    const uint32_t rk = vec ? (uint32_t)rank[off & (L - 1)] : kTieRemRank;
-    const uint32_t x1 = (!vec || rk == 0) ? (((e + 1) << 1) | sg) : 0u;
-    const uint32_t xw = (rk << 25) | ((((1u << kTieOffBits) - 1) - off) << 1) | sg;
-    k1 = x1 > k1 ? x1 : k1;
-    w = xw < w ? xw : w;
-}
-
-// tie_finalize of row_tie_keys' keys (at least one zero seen)
-__device__ __forceinline__ uint32_t row_tie_sign(uint32_t k1, uint32_t w) {
-    if (k1 == 0) return w & 1u;
-    if (w == 0xFFFFFFFFu) return k1 & 1u;
-    const uint32_t e1 = (k1 >> 1) - 1;
-    const uint32_t ew = w < 2 ? 0u : 1u + (((1u << kTieOffBits) - 1) - ((w >> 1) & ((1u << kTieOffBits) - 1)));
-    return ew > e1 ? (w & 1u) : (k1 & 1u);
-}
+__device__ __forceinline__ int msb64(uint64_t v) { return 63 - __builtin_clzll(v); }   // v != 0
 
 // Whole-chunk box query, LDS row layout (modes 4/5/6), chunk layers folded
 // in the kernel (pyas_reduce_axes_grid).  Block (col, j), wave w owns the
@@ -2782,21 +2775,21 @@ __device__ __forceinline__ uint32_t row_tie_sign(uint32_t k1, uint32_t w) {
 // ZS (g.zs = which: 1 min, 2 max): NumPy's sign of a zero min/max fused in.
 // Each output row of a chunk is ONE contiguous reduce call of NumPy's
 // (storage.py:99-100 over a C-ordered chunk whose trailing reduced group is
-// the row; tie rule g.t): when a layer's row min/max is a zero, the row's
-// H lanes key its zeros from the tile still in LDS (row_tie_keys), and the
-// row's winning sign is keyed at position l of the `out` array's call g.c2
-// (active.py:594, tie_keys); the output's zero min/max takes the sign those
-// level-2 keys give.  Zero-free layers cost one ballot.
+// the row; tie rule g.t).  When a layer's row min/max is a zero, the row's H
+// lanes build its zero mask Z (bit e: element e is a zero) from the tile
+// still in LDS, and the winner follows from the host's masks of the row's
+// positions (the K1/W keys of tie_keys, evaluated on bits): the last
+// remainder zero if any; else the later of the last seed/top-lane zero (K1)
+// and, unless the seed is a zero, the last zero of the lowest lane rank
+// class holding one (W).  The winner's sign is read back from LDS and keyed
+// at position l of the `out` array's call g.c2 (active.py:594, tie_keys);
+// the output's zero min/max takes the sign those level-2 keys give.
+// Zero-free layers cost one ballot.
 template <typename T, bool SHUF, bool BSWAP, int MASKED, int H, bool ZS>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes_fold_row(AxesArgs a, FoldGrid g) {
     constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
     constexpr int UL = 16 / H / VPL > 0 ? 16 / H / VPL : 1;   // load units per lane per tile
     __shared__ uint4 tile[(kBlock / kWave) * RPW * kRowLdsStride];
-    __shared__ uint8_t s_rank[ZS ? 64 : 1];
-    if constexpr (ZS) {
-        if (threadIdx.x < 64) s_rank[threadIdx.x] = g.t.rank[threadIdx.x];
-        __syncthreads();
-    }
     const AxesDense &d = a.d;
     const ReduceArgs &r = a.r;
     const int64_t col = blockIdx.x / d.bpc;
@@ -2890,30 +2883,47 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
                 const T v = (g.zs & 1u) ? acc.mn : acc.mx;
                 const bool z = cnt > 0 && !nan && v == (T)0;
                 if (__ballot(z)) {
-                    const uint32_t L = (uint32_t)g.t.lanes, m = (uint32_t)d.RI - 1u, nv = m & ~(L - 1u);
-                    uint32_t k1 = 0, kw = 0xFFFFFFFFu;
+                    uint64_t Z = 0;
                     if (z) {
                         // a masked zero never makes the min/max a zero (value
-                        // rules: zeros are masked all or none), so every zero keys
+                        // rules: zeros are masked all or none), so every zero counts
                         for (int i = 0; i < VH; ++i) {
                             T x[N];
                             unpack16<T, BSWAP>(row[i], x);
 #pragma unroll
                             for (int k = 0; k < N; ++k)
-                                if (x[k] == (T)0)
-                                    row_tie_keys((uint32_t)((h * VH + i) * N + k), __builtin_signbit(x[k]) ? 1u : 0u,
-                                                 nv, L, s_rank, k1, kw);
+                                Z |= (uint64_t)(x[k] == (T)0 ? 1u : 0u) << ((h * VH + i) * N + k);
                         }
                     }
 #pragma unroll
-                    for (int mm = H / 2; mm >= 1; mm >>= 1) {   // the row's H lanes
-                        const uint32_t o1 = __shfl_xor(k1, mm), ow = __shfl_xor(kw, mm);
-                        k1 = o1 > k1 ? o1 : k1;
-                        kw = ow < kw ? ow : kw;
-                    }
-                    if (z && h == 0) {
+                    for (int mm = H / 2; mm >= 1; mm >>= 1) Z |= shfl_xor(Z, mm);   // the row's H lanes
+                    if (z && h == 0 && Z) {
+                        int e;
+                        const uint64_t rem = Z & g.zrow_rem;
+                        if (rem) {
+                            e = msb64(rem);   // K1 at the last remainder zero; W is never later
+                        } else {
+                            const uint64_t sig = Z & (g.zrow_top | 1u);
+                            const int e1 = sig ? msb64(sig) : -1;
+                            int ew = -1;
+                            if (!(Z & 1u)) {   // (a zero seed is W itself, at 0)
+                                for (int rk = 0; rk < g.t.lanes; ++rk) {
+                                    const uint64_t cz = Z & g.zrow_cm[rk];
+                                    if (cz) {
+                                        ew = msb64(cz);
+                                        break;
+                                    }
+                                }
+                            }
+                            e = ew > e1 ? ew : e1;
+                        }
+                        T xe[N];
+                        unpack16<T, BSWAP>(t[rw * kRowLdsStride + e / N], xe);
+                        T we = xe[0];
+#pragma unroll
+                        for (int k = 1; k < N; ++k) we = (e % N) == k ? xe[k] : we;
                         uint64_t x1, xw, xa;
-                        tie_keys(l, row_tie_sign(k1, kw), g.c2, g.t, true, x1, xw, xa);
+                        tie_keys(l, __builtin_signbit(we) ? 1u : 0u, g.c2, g.t, true, x1, xw, xa);
                         zk1 = x1 > zk1 ? x1 : zk1;
                         zkw = xw < zkw ? xw : zkw;
                     }
