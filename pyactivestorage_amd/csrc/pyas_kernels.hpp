@@ -2775,16 +2775,19 @@ __device__ __forceinline__ int msb64(uint64_t v) { return 63 - __builtin_clzll(v
 // ZS (g.zs = which: 1 min, 2 max): NumPy's sign of a zero min/max fused in.
 // Each output row of a chunk is ONE contiguous reduce call of NumPy's
 // (storage.py:99-100 over a C-ordered chunk whose trailing reduced group is
-// the row; tie rule g.t).  When a layer's row min/max is a zero, the row's H
-// lanes build its zero mask Z (bit e: element e is a zero) from the tile
-// still in LDS, and the winner follows from the host's masks of the row's
-// positions (the K1/W keys of tie_keys, evaluated on bits): the last
-// remainder zero if any; else the later of the last seed/top-lane zero (K1)
-// and, unless the seed is a zero, the last zero of the lowest lane rank
-// class holding one (W).  The winner's sign is read back from LDS and keyed
-// at position l of the `out` array's call g.c2 (active.py:594, tie_keys);
-// the output's zero min/max takes the sign those level-2 keys give.
-// Zero-free layers cost one ballot.
+// the row; tie rule g.t).  When a layer's row min/max is a zero, the row's
+// lane 0 finds the winning zero from the tile still in LDS, by the host's
+// masks of the row's positions (the K1/W keys of tie_keys, evaluated on
+// bits): the last remainder zero if any (read backwards from the row's end:
+// one or two vectors on zero-heavy data); else, from the row's whole zero
+// mask, the later of the last seed/top-lane zero (K1) and, unless the seed
+// is a zero, the last zero of the lowest lane-rank class holding one (W).
+// The winner's sign is read back from LDS and keyed at position l of the
+// `out` array's call g.c2 (active.py:594; the position's keys are
+// wave-uniform, worked out once per layer); the output's zero min/max takes
+// the sign those level-2 keys give.  Zero-free layers cost one ballot.
+// (Building the zero mask in the main pass instead cost every min/max query
+// 21 %: C3 (2,) 0.70 -> 0.85 ms.)
 template <typename T, bool SHUF, bool BSWAP, int MASKED, int H, bool ZS>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes_fold_row(AxesArgs a, FoldGrid g) {
     constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
@@ -2880,29 +2883,51 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
             uint32_t cnt, nan;
             group_reduce(acc, H, cnt, nan);   // every lane of the row holds the row's result
             if constexpr (ZS) {
+                // level-2 keys of position l with sign 0 (wave-uniform: scalar)
+                uint64_t lk1, lkw, lka;
+                tie_keys(l, 0u, g.c2, g.t, true, lk1, lkw, lka);
                 const T v = (g.zs & 1u) ? acc.mn : acc.mx;
-                const bool z = cnt > 0 && !nan && v == (T)0;
-                if (__ballot(z)) {
-                    uint64_t Z = 0;
-                    if (z) {
-                        // a masked zero never makes the min/max a zero (value
-                        // rules: zeros are masked all or none), so every zero counts
-                        for (int i = 0; i < VH; ++i) {
-                            T x[N];
-                            unpack16<T, BSWAP>(row[i], x);
+                // lane 0 of a row whose min/max is a zero finds the winning
+                // zero e from the tile (a masked zero never makes the min/max
+                // a zero -- value rules mask zeros all or none -- so every
+                // zero element counts)
+                bool open = cnt > 0 && !nan && v == (T)0 && h == 0;
+                if (__ballot(open)) {
+                    const uint4 *trow = t + rw * kRowLdsStride;
+                    int e = -1;
+                    // fast path: the last remainder zero, if any, wins (K1; W
+                    // is never later) -- the remainder's vectors, last first
+                    const int vlo = g.zrow_rem ? (int)(__builtin_ctzll(g.zrow_rem) / N) : V;
+                    for (int vi = V - 1; vi >= vlo && __ballot(open); --vi) {
+                        if (open) {
+                            T xe[N];
+                            unpack16<T, BSWAP>(trow[vi], xe);
+                            uint32_t m4 = 0;
 #pragma unroll
-                            for (int k = 0; k < N; ++k)
-                                Z |= (uint64_t)(x[k] == (T)0 ? 1u : 0u) << ((h * VH + i) * N + k);
+                            for (int k = 0; k < N; ++k) m4 |= (xe[k] == (T)0 ? 1u : 0u) << k;
+                            m4 &= (uint32_t)(g.zrow_rem >> (vi * N)) & ((1u << N) - 1u);
+                            if (m4) {
+                                e = vi * N + (31 - __builtin_clz(m4));
+                                open = false;
+                            }
                         }
                     }
+                    // no remainder zero: the row's zero mask Z, then the later
+                    // of the last seed/top-lane zero (K1) and, unless the seed
+                    // is a zero, the last zero of the lowest lane-rank class
+                    // holding one (W)
+                    if (__ballot(open)) {
+                        uint64_t Z = 0;
+                        if (open) {
+                            for (int vi = 0; vi < V; ++vi) {
+                                T xe[N];
+                                unpack16<T, BSWAP>(trow[vi], xe);
 #pragma unroll
-                    for (int mm = H / 2; mm >= 1; mm >>= 1) Z |= shfl_xor(Z, mm);   // the row's H lanes
-                    if (z && h == 0 && Z) {
-                        int e;
-                        const uint64_t rem = Z & g.zrow_rem;
-                        if (rem) {
-                            e = msb64(rem);   // K1 at the last remainder zero; W is never later
-                        } else {
+                                for (int k = 0; k < N; ++k)
+                                    Z |= (uint64_t)(xe[k] == (T)0 ? 1u : 0u) << (vi * N + k);
+                            }
+                        }
+                        if (open && Z) {
                             const uint64_t sig = Z & (g.zrow_top | 1u);
                             const int e1 = sig ? msb64(sig) : -1;
                             int ew = -1;
@@ -2917,13 +2942,15 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
                             }
                             e = ew > e1 ? ew : e1;
                         }
+                    }
+                    if (e >= 0) {
                         T xe[N];
-                        unpack16<T, BSWAP>(t[rw * kRowLdsStride + e / N], xe);
+                        unpack16<T, BSWAP>(trow[e / N], xe);
                         T we = xe[0];
 #pragma unroll
                         for (int k = 1; k < N; ++k) we = (e % N) == k ? xe[k] : we;
-                        uint64_t x1, xw, xa;
-                        tie_keys(l, __builtin_signbit(we) ? 1u : 0u, g.c2, g.t, true, x1, xw, xa);
+                        const uint64_t sg = __builtin_signbit(we) ? 1u : 0u;
+                        const uint64_t x1 = lk1 ? (lk1 | sg) : 0u, xw = lkw | sg;
                         zk1 = x1 > zk1 ? x1 : zk1;
                         zkw = xw < zkw ? xw : zkw;
                     }
@@ -3358,7 +3385,8 @@ __device__ void tie_setup(const TieChunkArgs &a, int64_t c, TieSetup &S) {
 template <typename T, int G>
 __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
     constexpr int NG = kBlock / G;
-    constexpr int V = G == kWave ? 4 : 1;     // elements per lane per step
+    constexpr int V = G == kWave ? 4 : 1;     // elements per lane per step (8 measured slower:
+                                              // C3 full min 34.7 -> 47.6 us at 50 % zeros)
     constexpr int NW = kBlock / kWave;
     __shared__ TieSetup setups[NW];
     __shared__ uint8_t rank[64], arank[64];

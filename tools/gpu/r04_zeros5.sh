@@ -1,6 +1,6 @@
-# round 4: zero-mask keying in the fused row-fold sign; rolling-buffer slab loads
+# round 4: row-fold sign: remainder scan first, full mask only without a remainder zero
 set -o pipefail
-O=gpurun_out/r04/zeros3
+O=gpurun_out/r04/zeros5
 mkdir -p $O
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -12,6 +12,3 @@ timeout -k 10 300 python -u tools/bench_zeros.py --zeros 0.02 --axes none,0,2 --
 (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/zt -o run -- \
    python3 $R/tools/bench_zeros.py --zeros 0.5 --axes none,0,2 --reps 5 > $R/$O/zeros50_prof.log 2>&1) || exit 1
 cp $(find /tmp/zt -name '*kernel_stats.csv' | head -n 1) $O/zeros50_kernel_stats.csv
-timeout -k 10 300 python -u tools/bench_axes.py --shuffle --rec sum > $O/axes_shuf_rec.json 2> $O/axes_shuf_rec.err || exit 1
-PYAS_SHUF_SLAB=0 timeout -k 10 300 python -u tools/bench_axes.py --shuffle --rec sum --only 1 > $O/axes_shuf_rec_noslab.json 2> $O/axes_shuf_rec_noslab.err || exit 1
-timeout -k 10 300 python -u tools/bench_axes.py --rec sum > $O/axes_plain_rec.json 2> $O/axes_plain_rec.err || exit 1
