@@ -219,6 +219,19 @@ typedef struct {
 int pyas_tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
                     const pyas_tie_geom *geom, uint32_t axes_mask, uint32_t which,
                     const int64_t *out_offsets, pyas_partial *partials, void *stream);
+/* Level 1 of a FULL reduction (every dim reduced, one partial per chunk, the
+ * chunks at positions layer_base + c of the `out` array's call of length lr,
+ * active.py:594), done only where it can matter: which zero the level-2 keys
+ * pick depends on positions alone, so a pick pass keys the zero partials
+ * with sign 0, and only the chunk holding the K1 winner and the chunk
+ * holding the W winner are scanned (pyas_tie_chunks' scan, one wave each).
+ * pyas_tie_segments over the same partials then gives the same result as
+ * after pyas_tie_chunks over every chunk (a group of ranks: each rank's keys
+ * name its own two chunks, and the exchange picks among them).  Replaces
+ * pyas_tie_chunks for storage.py:99-100 + active.py:594 full reductions. */
+int pyas_tie_chunks_total(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask,
+                          const pyas_tie_geom *geom, uint32_t which, pyas_partial *partials,
+                          int64_t layer_base, int64_t lr, void *stream);
 /* Level 1 for a result folded without per-chunk partials
  * (pyas_reduce_axes_grid): when any of the n_final partials in `final_`
  * has a zero min/max (which: 1 or 2), write one byte per chunk output to

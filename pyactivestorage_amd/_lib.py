@@ -161,6 +161,8 @@ SIGNATURES = {
     "pyas_ctx_set_tie_rule": [_vp, _i32, ctypes.POINTER(TieRule)],
     "pyas_tie_chunks": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(TieGeom), _u32, _u32,
                         _vp, _vp, _vp],
+    "pyas_tie_chunks_total": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(TieGeom), _u32,
+                              _vp, _i64, _i64, _vp],
     "pyas_tie_chunk_flags": [_vp, ctypes.POINTER(Batch), ctypes.POINTER(Mask), ctypes.POINTER(TieGeom), _u32,
                              _u32, _vp, _vp, _i64, _vp, _vp],
     "pyas_tie_grid": [_vp, _i32, ctypes.POINTER(Grid), _vp, _vp, _i64, _u32, _vp, _vp, _vp],

@@ -674,7 +674,9 @@ class Active:
         min/max of a float variable the chunk partials are kept so that a
         zero extreme gets NumPy's sign: per chunk over its elements
         (storage.py:99-100, pyas_tie_chunks), then over the per-chunk values
-        in the `out` array's C order (active.py:594, pyas_tie_segments).
+        in the `out` array's C order (active.py:594, pyas_tie_segments);
+        level 1 scans only the two chunks level 2 can pick
+        (pyas_tie_chunks_total).
         Under a group the plan holds this rank's chunks, the first at
         position ``layer_base`` of the ``n_layers`` in the query, and the
         level-2 keys go to ``keys`` (a host list) for pyas_tie_finalize
@@ -684,8 +686,10 @@ class Active:
         if which:
             ctx, dt = plan.ctx, self.ds.dtype
             n_all = plan.n_chunks if n_layers is None else int(n_layers)
-            engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, plan.tie_geom(), (1 << self.ds.ndim) - 1,
-                              which, None, plan.chunk_partials.ptr, st)
+            # level 1 only on the chunks the level-2 keys can pick (positions
+            # decide which zero wins; the two candidates' signs are then exact)
+            engine.tie_chunks_total(ctx, plan.batch, plan.mask_up.struct, plan.tie_geom(), which,
+                                    plan.chunk_partials.ptr, int(layer_base), max(n_all, 1), st)
             kbuf = None
             if keys is not None:
                 kbuf = DeviceBuffer(ctx, 16)

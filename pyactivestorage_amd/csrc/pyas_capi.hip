@@ -372,6 +372,16 @@ const pyas::TieRule *tie_of(const pyas_ctx *ctx, int32_t dtype) {
     return t.lanes ? &t : nullptr;
 }
 
+pyas::TieCall grid_call(const pyas::TieRule &t, int64_t lr) {
+    pyas::TieCall c;
+    c.acc = 0;
+    c.block = 0;
+    c.n_copy = 0;
+    c.lr = lr < 1 ? 1 : lr;
+    c.npr = (c.lr + t.piece - 1) / t.piece;
+    return c;
+}
+
 int check_geom(const pyas_tie_geom *g, int ndim) {
     if (!g) return fail(PYAS_EINVAL, "tie geometry is NULL");
     uint32_t seen = 0;
@@ -385,9 +395,12 @@ int check_geom(const pyas_tie_geom *g, int ndim) {
 }
 
 // Level 1 shared by pyas_tie_chunks / pyas_tie_chunk_flags.
+// pick (full reductions): device keys of pyas_tie_chunks_total's pick pass;
+// only the two chunks they name are scanned, one workgroup.
 int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, const pyas_tie_geom *geom,
                uint32_t axes_mask, uint32_t which, const int64_t *out_offsets, pyas_partial *partials,
-               uint8_t *flags, const uint32_t *gate, hipStream_t st) {
+               uint8_t *flags, const uint32_t *gate, hipStream_t st, const uint64_t *pick = nullptr,
+               int64_t pick_base = 0, int64_t pick_lr = 1) {
     pyas::TieChunkArgs a;
     std::memset(&a, 0, sizeof(a));
     int es;
@@ -425,6 +438,7 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
         const int g = atoi(e_group);
         if (g == 1 || g == 16 || g == pyas::kWave) group = g;
     }
+    if (pick) group = pyas::kWave;   // the picked chunks: a wave each
     a.group = group;
     a.n_chunks = batch->n_chunks;
     a.cpw = (kept == 1 && group == pyas::kWave) ? pyas::kBlock / pyas::kWave : 1;
@@ -438,7 +452,14 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
     a.parts = partials;
     a.flags = flags;
     a.gate = gate;
-    const int64_t grid = (batch->n_chunks + a.cpw - 1) / a.cpw;   // a workgroup per chunk (or per cpw)
+    int64_t grid = (batch->n_chunks + a.cpw - 1) / a.cpw;   // a workgroup per chunk (or per cpw)
+    if (pick) {
+        if (kept != 1 || a.cpw < 2) return fail(PYAS_EINVAL, "the picked tie scan needs a full reduction");
+        a.pick = pick;
+        a.pick_call = grid_call(*t, pick_lr);
+        a.pick_base = pick_base;
+        grid = 1;
+    }
     if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "tie grid too large");
     PYAS_HIP(hipSetDevice(ctx->device));
     PYAS_HIP(pyas::launch_tie_chunks(batch->dtype, a, grid, st));
@@ -469,16 +490,6 @@ int tie_scratch(pyas_ctx *ctx, void *stream, size_t bytes, void **out) {
         PYAS_HIP(hipFree(old));
     }
     return PYAS_OK;
-}
-
-pyas::TieCall grid_call(const pyas::TieRule &t, int64_t lr) {
-    pyas::TieCall c;
-    c.acc = 0;
-    c.block = 0;
-    c.n_copy = 0;
-    c.lr = lr < 1 ? 1 : lr;
-    c.npr = (c.lr + t.piece - 1) / t.piece;
-    return c;
 }
 
 // Level 2: one wave per (output, layer slice); several slices per output
@@ -525,6 +536,30 @@ int pyas_tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mas
     if (!partials && batch && batch->n_chunks > 0) return fail(PYAS_EINVAL, "partials is NULL");
     return tie_chunks(ctx, batch, mask, geom, axes_mask, which, out_offsets, partials, nullptr, nullptr,
                       (hipStream_t)stream);
+}
+
+int pyas_tie_chunks_total(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, const pyas_tie_geom *geom,
+                          uint32_t which, pyas_partial *partials, int64_t layer_base, int64_t lr, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (!batch) return fail(PYAS_EINVAL, "batch is NULL");
+    if ((which & ~PYAS_TIE_REC) != 1u && (which & ~PYAS_TIE_REC) != 2u)
+        return fail(PYAS_EINVAL, "which must be 1 (min) or 2 (max), optionally | PYAS_TIE_REC");
+    if (layer_base < 0 || lr < 1) return fail(PYAS_EINVAL, "layer_base < 0 or lr < 1");
+    const pyas::TieRule *t = tie_of(ctx, batch->dtype);
+    if (!t || batch->n_chunks == 0) return PYAS_OK;
+    if (!partials) return fail(PYAS_EINVAL, "partials is NULL");
+    void *p = nullptr;
+    int rc = tie_scratch(ctx, stream, 16, &p);
+    if (rc) return rc;
+    uint64_t *keys = (uint64_t *)p;
+    hipStream_t st = (hipStream_t)stream;
+    PYAS_HIP(hipSetDevice(ctx->device));
+    PYAS_HIP(hipMemsetAsync(keys, 0, 8, st));
+    PYAS_HIP(hipMemsetAsync(keys + 1, 0xff, 8, st));
+    PYAS_HIP(pyas::launch_tie_pick(batch->dtype, partials, batch->n_chunks, which, layer_base, grid_call(*t, lr), *t,
+                                   keys, st));
+    return tie_chunks(ctx, batch, mask, geom, (1u << batch->ndim) - 1u, which, nullptr, partials, nullptr, nullptr,
+                      st, keys, layer_base, lr);
 }
 
 int pyas_tie_chunk_flags(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, const pyas_tie_geom *geom,

@@ -173,6 +173,9 @@ struct TieChunkArgs {
     int64_t n_chunks;
     int32_t cpw;                      // chunks per workgroup: 1, or a wave per chunk (one output each)
     int32_t group;                    // lanes per output: 1, 16 or 64 (k_tie_scan)
+    const uint64_t *pick;             // non-NULL (full reductions): only the chunks of the level-2
+    TieCall pick_call;                //   K1 / W keys pick[0] / pick[1] (positions pick_base + c
+    int64_t pick_base;                //   of the `out` call pick_call), a wave each
 };
 struct TieGridArgs {
     pyas_grid g;                      // kind 0: layers from the grid tables
@@ -194,6 +197,9 @@ template <typename T>
 hipError_t launch_tie_gate_t(const pyas_partial *fin, int64_t n, uint32_t which, uint32_t *gate, hipStream_t st);
 template <typename T>
 hipError_t launch_tie_grid_t(const TieGridArgs &a, hipStream_t st);
+template <typename T>
+hipError_t launch_tie_pick_t(const pyas_partial *parts, int64_t n, uint32_t which, int64_t base, const TieCall &call,
+                             const TieRule &t, uint64_t *keys, hipStream_t st);
 template <typename T>
 hipError_t launch_tie_finalize_t(const uint64_t *keys, int64_t n_out, int32_t n_sets, const TieCall &call,
                                  const TieRule &t, uint32_t which, pyas_partial *fin, hipStream_t st);
@@ -223,6 +229,8 @@ hipError_t launch_tie_chunks(int dtype, const TieChunkArgs &a, int64_t grid, hip
 hipError_t launch_tie_gate(int dtype, const pyas_partial *fin, int64_t n, uint32_t which, uint32_t *gate,
                            hipStream_t st);
 hipError_t launch_tie_grid(int dtype, const TieGridArgs &a, hipStream_t st);
+hipError_t launch_tie_pick(int dtype, const pyas_partial *parts, int64_t n, uint32_t which, int64_t base,
+                           const TieCall &call, const TieRule &t, uint64_t *keys, hipStream_t st);
 hipError_t launch_tie_finalize(int dtype, const uint64_t *keys, int64_t n_out, int32_t n_sets, const TieCall &call,
                                const TieRule &t, uint32_t which, pyas_partial *fin, hipStream_t st);
 hipError_t launch_format(int dtype, const pyas_partial *in, int64_t n, int32_t method, void *values,

@@ -150,6 +150,12 @@ hipError_t launch_tie_grid(int dtype, const TieGridArgs &a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
+hipError_t launch_tie_pick(int dtype, const pyas_partial *parts, int64_t n, uint32_t which, int64_t base,
+                           const TieCall &call, const TieRule &t, uint64_t *keys, hipStream_t st) {
+    PYAS_DISPATCH_T(dtype, return launch_tie_pick_t<T>(parts, n, which, base, call, t, keys, st));
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_tie_finalize(int dtype, const uint64_t *keys, int64_t n_out, int32_t n_sets, const TieCall &call,
                                const TieRule &t, uint32_t which, pyas_partial *fin, hipStream_t st) {
     PYAS_DISPATCH_T(dtype, return launch_tie_finalize_t<T>(keys, n_out, n_sets, call, t, which, fin, st));

@@ -3166,6 +3166,16 @@ __device__ __forceinline__ void tie_keys(int64_t e, uint64_t sg, const TieCall &
     w = (row1 << 32) | ((uint64_t)rank << 25) | ((uint64_t)(((int64_t)1 << kTieOffBits) - 1 - off) << 1) | sg;
 }
 
+// Reduced position of the zero behind a contiguous call's W key.
+__device__ __forceinline__ int64_t tie_w_pos(uint64_t w, const TieCall &c, const TieRule &t) {
+    if (w < 2) return 0;
+    const int64_t row = (int64_t)(w >> 32) - 1;
+    const int64_t off = (((int64_t)1 << kTieOffBits) - 1) - (int64_t)((w >> 1) & ((1u << kTieOffBits) - 1));
+    const int64_t q = row / c.npr, k = row - q * c.npr;
+    const int64_t s0 = (q == 0 && k == 0) ? 1 : k * (int64_t)t.piece;
+    return q * c.lr + s0 + off;
+}
+
 // Sign bit from an output's combined keys; -1 when it holds no zero.
 __device__ __forceinline__ int tie_finalize(uint64_t k1, uint64_t w, uint64_t ka, const TieCall &c,
                                             const TieRule &t) {
@@ -3174,15 +3184,7 @@ __device__ __forceinline__ int tie_finalize(uint64_t k1, uint64_t w, uint64_t ka
     if (k1 == 0) return (int)(w & 1u);
     if (w == kTieWNone) return (int)(k1 & 1u);
     const int64_t e1 = (int64_t)(k1 >> 1) - 1;
-    int64_t ew = 0;
-    if (w >= 2) {
-        const int64_t row = (int64_t)(w >> 32) - 1;
-        const int64_t off = (((int64_t)1 << kTieOffBits) - 1) - (int64_t)((w >> 1) & ((1u << kTieOffBits) - 1));
-        const int64_t q = row / c.npr, k = row - q * c.npr;
-        const int64_t s0 = (q == 0 && k == 0) ? 1 : k * (int64_t)t.piece;
-        ew = q * c.lr + s0 + off;
-    }
-    return ew > e1 ? (int)(w & 1u) : (int)(k1 & 1u);
+    return tie_w_pos(w, c, t) > e1 ? (int)(w & 1u) : (int)(k1 & 1u);
 }
 
 template <typename T>
@@ -3402,10 +3404,16 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
     int slot;
     if (a.cpw > 1) {   // one output per chunk, a wave per chunk (host: G == kWave)
         c = (int64_t)blockIdx.x * a.cpw + wv;
+        if (a.pick) {      // only the chunks the level-2 keys can pick: wave 0 K1's, wave 1 W's
+            const uint64_t k1 = a.pick[0], kw = a.pick[1];
+            const int64_t c1 = k1 ? (int64_t)(k1 >> 1) - 1 - a.pick_base : -1;
+            const int64_t cw = kw != kTieWNone ? tie_w_pos(kw, a.pick_call, a.t) - a.pick_base : -1;
+            c = wv == 0 ? c1 : (wv == 1 && cw != c1) ? cw : -1;
+        }
         o_first = 0;
         o_step = 1;
         slot = wv;
-        if (c < a.n_chunks && lane == 0) tie_setup(a, c, setups[slot]);
+        if (c >= 0 && c < a.n_chunks && lane == 0) tie_setup(a, c, setups[slot]);
     } else {
         c = blockIdx.x;
         o_first = grp;
@@ -3414,7 +3422,7 @@ __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
         if (threadIdx.x == 0) tie_setup(a, c, setups[0]);
     }
     __syncthreads();
-    if (c >= a.n_chunks) return;   // wave-uniform
+    if (c < 0 || c >= a.n_chunks) return;   // wave-uniform
     const TieSetup &S = setups[slot];
     const int rec = tie_rec(a.which);
     const int64_t n_out = S.n_out, R = S.R;
@@ -3562,6 +3570,42 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
         v = o < v ? o : v;
     }
     return v;
+}
+
+// Level-2 keys by position alone of a full reduction's chunk partials
+// (positions base + l of the `out` call; which zero wins does not depend on
+// the signs): keys[0] = max K1, keys[1] = min W over the zero partials, one
+// atomic each per workgroup.  The winner is one of the two chunks, so only
+// they need the level-1 scan (pyas_tie_chunks_total).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_tie_pick(const pyas_partial *parts, int64_t n, uint32_t which,
+                                                     int64_t base, TieCall call, TieRule t, uint64_t *keys) {
+    __shared__ uint64_t s1[kBlock / kWave], sw[kBlock / kWave];
+    const int rec = tie_rec(which);
+    uint64_t k1 = 0, kw = kTieWNone;
+    for (int64_t l = (int64_t)blockIdx.x * kBlock + threadIdx.x; l < n; l += (int64_t)gridDim.x * kBlock) {
+        if (!tie_zero<T>(part_at<T>(parts, l, rec), which)) continue;
+        uint64_t x1, xw, xa;
+        tie_keys(base + l, 0u, call, t, true, x1, xw, xa);
+        k1 = x1 > k1 ? x1 : k1;
+        kw = xw < kw ? xw : kw;
+    }
+    k1 = wave_max_u64(k1);
+    kw = wave_min_u64(kw);
+    const int w = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        s1[w] = k1;
+        sw[w] = kw;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < kBlock / kWave; ++i) {
+            k1 = s1[i] > k1 ? s1[i] : k1;
+            kw = sw[i] < kw ? sw[i] : kw;
+        }
+        if (k1) atomicMax(reinterpret_cast<unsigned long long *>(keys), (unsigned long long)k1);
+        if (kw != kTieWNone) atomicMin(reinterpret_cast<unsigned long long *>(keys + 1), (unsigned long long)kw);
+    }
 }
 
 // Level 2 (active.py:594 over the `out` array): one wave per (final output,
@@ -3732,6 +3776,20 @@ hipError_t launch_tie_gate_t(const pyas_partial *fin, int64_t n, uint32_t which,
         int64_t blocks = (n + kBlock - 1) / kBlock;
         blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
         hipLaunchKernelGGL((k_tie_gate<T>), dim3((unsigned)blocks), dim3(kBlock), 0, st, fin, n, which, gate);
+        return hipGetLastError();
+    }
+}
+
+template <typename T>
+hipError_t launch_tie_pick_t(const pyas_partial *parts, int64_t n, uint32_t which, int64_t base, const TieCall &call,
+                             const TieRule &t, uint64_t *keys, hipStream_t st) {
+    if constexpr (TT<T>::kind != 0) {
+        return hipSuccess;
+    } else {
+        int64_t blocks = (n + kBlock - 1) / kBlock;
+        blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+        hipLaunchKernelGGL((k_tie_pick<T>), dim3((unsigned)blocks), dim3(kBlock), 0, st, parts, n, which, base,
+                           call, t, keys);
         return hipGetLastError();
     }
 }
@@ -4181,6 +4239,8 @@ hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, vo
     template hipError_t launch_tie_gate_t<T>(const pyas_partial *, int64_t, uint32_t, uint32_t *,  \
                                              hipStream_t);                                       \
     template hipError_t launch_tie_grid_t<T>(const TieGridArgs &, hipStream_t);                   \
+    template hipError_t launch_tie_pick_t<T>(const pyas_partial *, int64_t, uint32_t, int64_t,     \
+                                             const TieCall &, const TieRule &, uint64_t *, hipStream_t); \
     template hipError_t launch_tie_finalize_t<T>(const uint64_t *, int64_t, int32_t, const TieCall &, \
                                                  const TieRule &, uint32_t, pyas_partial *, hipStream_t);
 #define PYAS_INSTANTIATE_PART2(T)                                                              \

@@ -95,6 +95,17 @@ def tie_chunks(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, geom: _lib.TieG
                "pyas_tie_chunks")
 
 
+def tie_chunks_total(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, geom: _lib.TieGeom, which: int,
+                     partials_ptr, layer_base: int, lr: int, stream) -> None:
+    """Level 1 of a full reduction where it can matter (pyas_tie_chunks_total):
+    only the two chunks the level-2 keys can pick are scanned, so
+    tie_segments afterwards gives what tie_chunks over every chunk would."""
+    _lib.check(ctx.lib.pyas_tie_chunks_total(ctx.handle, ctypes.byref(batch), ctypes.byref(mask),
+                                             ctypes.byref(geom), int(which), partials_ptr, int(layer_base),
+                                             int(lr), stream),
+               "pyas_tie_chunks_total")
+
+
 def tie_chunk_flags(ctx: Context, batch: _lib.Batch, mask: _lib.Mask, geom: _lib.TieGeom, axes_mask: int,
                     which: int, out_offsets_ptr, final_ptr, n_final: int, flags_ptr, stream) -> None:
     """Per chunk output: zero held / NumPy's sign, when a final min/max is a

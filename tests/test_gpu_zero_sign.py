@@ -371,3 +371,29 @@ def test_fused_row_fold_sign(gpu, dt, row_lds, dens, kind, case, monkeypatch):
         _same_bytes(want, act[...], (axis, "passes"))
     finally:
         gpu.set_fold_min_blocks(0)
+
+
+@pytest.mark.parametrize("dt", ["<f4", ">f4", "<f8"])
+@pytest.mark.parametrize("dens", [0.5, 0.02, 0.0005])
+@pytest.mark.parametrize("kind", ["min", "max"])
+def test_full_reduction_pick(gpu, dt, dens, kind):
+    """pyas_tie_chunks_total: Active full min/max scans only the two chunks
+    the level-2 keys can pick (K1's and W's, by position alone).  Dense,
+    sparse and very sparse zeros over 256 chunks, against active.py's
+    combine over storage.py's per-chunk results, sign bit included."""
+    if tie_rule(dt) is None:
+        pytest.skip("no NumPy tie rule derived on this host")
+    rng = np.random.default_rng(int(dens * 10000) + len(dt) + len(kind))
+    shape, chunks = (64, 64, 64), (16, 8, 8)
+    a = _chunk(rng, shape, np.dtype(dt), "min0" if kind == "min" else "max0", dens=dens, n_fill=30)
+    attrs = {"_FillValue": np.array([-999.0], dtype=dt)}
+    missing = (np.dtype(dt).type(-999.0), None, None, None)
+    var, data = _variable(a, chunks, attrs)
+    data_of = lambda cc: data[var.chunk_index[cc][0]: var.chunk_index[cc][0] + var.chunk_index[cc][1]]
+    for q in QUERIES[:2]:
+        want = _reference_active(a, chunks, q, (0, 1, 2), kind, missing, data_of)
+        for resident in (False, True):
+            act = Active(var, resident=resident)
+            act.method = kind
+            _same_bytes(want, act[q], (q, resident))
+        active_mod.release_resident(var)

@@ -1,4 +1,4 @@
-# round 4: row-fold sign: remainder scan first, full mask only without a remainder zero
+# round 4: row-fold sign remainder scan first; full-reduction tie scan only on the two picked chunks
 set -o pipefail
 O=gpurun_out/r04/zeros5
 mkdir -p $O
