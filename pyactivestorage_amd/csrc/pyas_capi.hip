@@ -1199,6 +1199,8 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
             if (x.d.RI - 1 >= t->piece || lr2 >= (int64_t(1) << 31))
                 return fail(PYAS_ENOTSUP, "zero sign in the row fold: call longer than NumPy's buffer");
             if (x.d.RI > 64) return fail(PYAS_ENOTSUP, "zero sign in the row fold: rows over 64 elements");
+            if (t->lanes & (t->lanes - 1))
+                return fail(PYAS_ENOTSUP, "zero sign in the row fold: a lane count that is not a power of two");
             fg.t = *t;
             fg.c2 = grid_call(*t, lr2);
             // the row call's positions as bit masks: e = 0 the seed, then
@@ -1208,8 +1210,10 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
             for (int64_t e = 1; e <= nv; ++e) {
                 const int r = t->rank[(e - 1) % L];
                 fg.zrow_cm[r] |= uint64_t(1) << e;
+                fg.zrow_vec |= uint64_t(1) << e;
                 if (r == 0) fg.zrow_top |= uint64_t(1) << e;
             }
+            for (int64_t b = 0; b * L < 64; ++b) fg.zrow_rep |= uint64_t(1) << (b * L);
         } else {
             return fail(PYAS_ENOTSUP, "the zero sign is fused into the lean column and the row folds only (this "
                                       "geometry takes k_axes_fold)");

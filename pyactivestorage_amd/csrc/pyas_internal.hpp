@@ -158,6 +158,7 @@ struct FoldGrid {
     TieRule t;                        // zs in k_axes_fold_row: the host's rule,
     TieCall c2;                       //   the `out` array's call (level 2), and masks over a
     uint64_t zrow_rem, zrow_top;      //   row's positions e (RI <= 64): remainder, top-priority lane,
+    uint64_t zrow_vec, zrow_rep;      //   all lane positions, lane 0's positions (from e = 1),
     uint64_t zrow_cm[64];             //   lane-rank classes (zrow_cm[r]: the lane of rank r)
 };
 struct TieChunkArgs {

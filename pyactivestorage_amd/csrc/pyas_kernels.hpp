@@ -2764,6 +2764,38 @@ __device__ __forceinline__ int tie_finalize(uint64_t k1, uint64_t w, uint64_t ka
 
 __device__ __forceinline__ int msb64(uint64_t v) { return 63 - __builtin_clzll(v); }   // v != 0
 
+// A position's place in a contiguous call, stepped one position at a time
+// (l = q * lr + k * piece + kpos): tie_keys(l, sign 0) without a division,
+// for a walk over consecutive positions (the fold's layers).
+struct TiePos {
+    uint32_t q = 0, k = 0, pos = 0, kpos = 0;
+    __device__ void next(const TieCall &c, const TieRule &t) {
+        if (++pos == (uint32_t)c.lr) {
+            pos = kpos = k = 0;
+            ++q;
+        } else if (++kpos == (uint32_t)t.piece) {
+            kpos = 0;
+            ++k;
+        }
+    }
+    __device__ void keys(int64_t l, const TieCall &c, const TieRule &t, uint64_t &k1, uint64_t &w) const {
+        if (l == 0) {   // the seed
+            k1 = 2u;
+            w = 0u;
+            return;
+        }
+        const uint32_t P = (uint32_t)t.piece, lr = (uint32_t)c.lr, L = (uint32_t)t.lanes;
+        const uint32_t s0 = (q == 0 && k == 0) ? 1u : k * P;
+        const uint32_t e1 = (k + 1) * P < lr ? (k + 1) * P : lr;
+        const uint32_t m = e1 - s0, off = pos - s0;
+        const bool vec = off < (m & ~(L - 1u));
+        const uint32_t rk = vec ? (uint32_t)t.rank[off & (L - 1u)] : kTieRemRank;
+        k1 = (!vec || rk == 0) ? (((uint64_t)l + 1) << 1) : 0u;
+        w = (((uint64_t)q * (uint64_t)c.npr + k + 1) << 32) | ((uint64_t)rk << 25) |
+            ((uint64_t)(((uint32_t)1 << kTieOffBits) - 1 - off) << 1);
+    }
+};
+
 // Whole-chunk box query, LDS row layout (modes 4/5/6), chunk layers folded
 // in the kernel (pyas_reduce_axes_grid).  Block (col, j), wave w owns the
 // output tiles j*4 + w, + 4*bpc, ... of kept-dims chunk column `col`; for
@@ -2789,10 +2821,29 @@ __device__ __forceinline__ int msb64(uint64_t v) { return 63 - __builtin_clzll(v
 // (Building the zero mask in the main pass instead cost every min/max query
 // 21 %: C3 (2,) 0.70 -> 0.85 ms.)
 template <typename T, bool SHUF, bool BSWAP, int MASKED, int H, bool ZS>
-__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes_fold_row(AxesArgs a, FoldGrid g) {
+// (ZS with two lanes per row: held to 128 VGPRs, the non-ZS kernel's 4 waves
+// per SIMD, except the all-rules mask mode, which would spill)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ZS && H == 2 && MASKED != kMaskAll ? 4 : 1, 8)))
+void k_axes_fold_row(AxesArgs a, FoldGrid g) {
     constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
     constexpr int UL = 16 / H / VPL > 0 ? 16 / H / VPL : 1;   // load units per lane per tile
     __shared__ uint4 tile[(kBlock / kWave) * RPW * kRowLdsStride];
+    // ZS: lane-class sets -> rank sets, per byte of the class set (entries
+    // 256 h + byte: the ranks of lanes 8 h + i for the byte's bits i), and
+    // rank -> lane
+    __shared__ uint16_t s_pt[ZS ? 512 : 1];
+    __shared__ uint8_t s_ord[ZS ? 64 : 1];
+    if constexpr (ZS) {
+        for (int x = threadIdx.x; x < 512; x += kBlock) {
+            const int hh = x >> 8, byte = x & 255;
+            uint32_t m = 0;
+            for (int i = 0; i < 8; ++i)
+                if (((byte >> i) & 1) && 8 * hh + i < g.t.lanes) m |= 1u << g.t.rank[8 * hh + i];
+            s_pt[x] = (uint16_t)m;
+        }
+        if ((int)threadIdx.x < g.t.lanes) s_ord[g.t.rank[threadIdx.x]] = (uint8_t)threadIdx.x;
+        __syncthreads();
+    }
     const AxesDense &d = a.d;
     const ReduceArgs &r = a.r;
     const int64_t col = blockIdx.x / d.bpc;
@@ -2830,6 +2881,8 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
     mk.init(r.mask);
     const bool round = (g.flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
     const int V = (int)(d.RI / N), VH = V / H;
+    // ZS: the row's first vector holding a remainder position (V: none)
+    const int vrem = ZS && g.zrow_rem ? (int)(__builtin_ctzll(g.zrow_rem) / N) : V;
     const int lane = threadIdx.x & (kWave - 1), rw = lane / H, h = lane - rw * H;
     uint4 *t = tile + (threadIdx.x / kWave) * RPW * kRowLdsStride;
     const int64_t wave = j * (kBlock / kWave) + threadIdx.x / kWave;
@@ -2861,6 +2914,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
         WAcc<T> wacc;
         wacc.init();
         uint64_t zk1 = 0, zkw = kTieWNone;   // ZS: level-2 keys of the row's zero layers
+        TiePos l2;                           // ZS: layer l's place in the `out` call
         load(layer_base(0), o0, nvec);
         for (int64_t l = 0; l < g.n_layers; ++l) {
 #pragma unroll
@@ -2883,67 +2937,87 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
             uint32_t cnt, nan;
             group_reduce(acc, H, cnt, nan);   // every lane of the row holds the row's result
             if constexpr (ZS) {
-                // level-2 keys of position l with sign 0 (wave-uniform: scalar)
-                uint64_t lk1, lkw, lka;
-                tie_keys(l, 0u, g.c2, g.t, true, lk1, lkw, lka);
                 const T v = (g.zs & 1u) ? acc.mn : acc.mx;
-                // lane 0 of a row whose min/max is a zero finds the winning
-                // zero e from the tile (a masked zero never makes the min/max
-                // a zero -- value rules mask zeros all or none -- so every
-                // zero element counts)
-                bool open = cnt > 0 && !nan && v == (T)0 && h == 0;
-                if (__ballot(open)) {
+                // the rows whose min/max is a zero find their winning zero e
+                // from the tile, all H lanes of a row together (a masked zero
+                // never makes the min/max a zero -- value rules mask zeros all
+                // or none -- so every zero element counts)
+                const bool zrow = cnt > 0 && !nan && v == (T)0;   // the row's H lanes agree
+                if (__ballot(zrow)) {
                     const uint4 *trow = t + rw * kRowLdsStride;
                     int e = -1;
-                    // fast path: the last remainder zero, if any, wins (K1; W
-                    // is never later) -- the remainder's vectors, last first
-                    const int vlo = g.zrow_rem ? (int)(__builtin_ctzll(g.zrow_rem) / N) : V;
-                    for (int vi = V - 1; vi >= vlo && __ballot(open); --vi) {
-                        if (open) {
+                    if (zrow) {
+                        // the last remainder zero, if any, wins (K1; W is never
+                        // later): lane h reads remainder vectors vlo + h, + H, ...
+                        int er = -1;
+                        for (int vi = vrem + h; vi < V; vi += H) {
                             T xe[N];
                             unpack16<T, BSWAP>(trow[vi], xe);
                             uint32_t m4 = 0;
 #pragma unroll
                             for (int k = 0; k < N; ++k) m4 |= (xe[k] == (T)0 ? 1u : 0u) << k;
                             m4 &= (uint32_t)(g.zrow_rem >> (vi * N)) & ((1u << N) - 1u);
-                            if (m4) {
-                                e = vi * N + (31 - __builtin_clz(m4));
-                                open = false;
-                            }
+                            if (m4) er = vi * N + (31 - __builtin_clz(m4));
                         }
+#pragma unroll
+                        for (int mm = H / 2; mm >= 1; mm >>= 1) {
+                            const int o = __shfl_xor(er, mm);
+                            er = o > er ? o : er;
+                        }
+                        e = er;
                     }
-                    // no remainder zero: the row's zero mask Z, then the later
-                    // of the last seed/top-lane zero (K1) and, unless the seed
-                    // is a zero, the last zero of the lowest lane-rank class
-                    // holding one (W)
-                    if (__ballot(open)) {
+                    // no remainder zero: the row's zero mask Z (lane h: its VH
+                    // vectors), then the later of the last seed/top-lane zero
+                    // (K1) and, unless the seed is a zero, the last zero of the
+                    // lowest lane-rank class holding one (W)
+                    const bool slow = zrow && e < 0;
+                    if (__ballot(slow)) {
                         uint64_t Z = 0;
-                        if (open) {
-                            for (int vi = 0; vi < V; ++vi) {
+                        if (slow) {
+                            for (int i = 0; i < VH; ++i) {
                                 T xe[N];
-                                unpack16<T, BSWAP>(trow[vi], xe);
+                                unpack16<T, BSWAP>(row[i], xe);
 #pragma unroll
                                 for (int k = 0; k < N; ++k)
-                                    Z |= (uint64_t)(xe[k] == (T)0 ? 1u : 0u) << (vi * N + k);
+                                    Z |= (uint64_t)(xe[k] == (T)0 ? 1u : 0u) << ((h * VH + i) * N + k);
                             }
                         }
-                        if (open && Z) {
+#pragma unroll
+                        for (int mm = H / 2; mm >= 1; mm >>= 1) Z |= shfl_xor(Z, mm);
+                        if (slow && h == 0 && Z) {
                             const uint64_t sig = Z & (g.zrow_top | 1u);
                             const int e1 = sig ? msb64(sig) : -1;
                             int ew = -1;
-                            if (!(Z & 1u)) {   // (a zero seed is W itself, at 0)
-                                for (int rk = 0; rk < g.t.lanes; ++rk) {
-                                    const uint64_t cz = Z & g.zrow_cm[rk];
-                                    if (cz) {
-                                        ew = msb64(cz);
-                                        break;
+                            const uint64_t Zv = Z & g.zrow_vec;   // the zeros in the lanes
+                            if (!(Z & 1u) && Zv) {   // (a zero seed is W itself, at 0)
+                                const int L = g.t.lanes;
+                                if (L <= 16) {
+                                    // the lane classes holding a zero (bit j: lane j),
+                                    // through the rank tables: the lowest rank's class
+                                    uint32_t C = 0;
+                                    for (int b = 0; 1 + b * L < 64; ++b)
+                                        C |= (uint32_t)(Zv >> (1 + b * L)) & ((1u << L) - 1u);
+                                    const uint32_t P = (uint32_t)s_pt[C & 0xFFu] | (uint32_t)s_pt[256 + (C >> 8)];
+                                    const int j = s_ord[__builtin_ctz(P)];
+                                    ew = msb64(Zv & (g.zrow_rep << (1 + j)));
+                                } else {
+                                    for (int rk = 0; rk < L; ++rk) {
+                                        const uint64_t cz = Z & g.zrow_cm[rk];
+                                        if (cz) {
+                                            ew = msb64(cz);
+                                            break;
+                                        }
                                     }
                                 }
                             }
                             e = ew > e1 ? ew : e1;
                         }
                     }
-                    if (e >= 0) {
+                    // level-2 keys of position l (sign 0; wave-uniform, from
+                    // the incremental position state: no division)
+                    uint64_t lk1, lkw;
+                    l2.keys(l, g.c2, g.t, lk1, lkw);
+                    if (zrow && h == 0 && e >= 0) {
                         T xe[N];
                         unpack16<T, BSWAP>(trow[e / N], xe);
                         T we = xe[0];
@@ -2955,6 +3029,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
                         zkw = xw < zkw ? xw : zkw;
                     }
                 }
+                l2.next(g.c2, g.t);
             }
             if (h == 0) {
                 pyas_partial pp;
