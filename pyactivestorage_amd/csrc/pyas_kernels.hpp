@@ -2821,10 +2821,9 @@ struct TiePos {
 // (Building the zero mask in the main pass instead cost every min/max query
 // 21 %: C3 (2,) 0.70 -> 0.85 ms.)
 template <typename T, bool SHUF, bool BSWAP, int MASKED, int H, bool ZS>
-// (ZS with two lanes per row: held to 128 VGPRs, the non-ZS kernel's 4 waves
-// per SIMD, except the all-rules mask mode, which would spill)
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(ZS && H == 2 && MASKED != kMaskAll ? 4 : 1, 8)))
-void k_axes_fold_row(AxesArgs a, FoldGrid g) {
+// (Holding the ZS kernel to 128 VGPRs, the non-ZS kernel's 4 waves per SIMD,
+// made it slower: C3 (2,) 0.77 -> 1.0-1.06 ms, profiles/r04/zeros7.)
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes_fold_row(AxesArgs a, FoldGrid g) {
     constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
     constexpr int UL = 16 / H / VPL > 0 ? 16 / H / VPL : 1;   // load units per lane per tile
     __shared__ uint4 tile[(kBlock / kWave) * RPW * kRowLdsStride];
