@@ -432,7 +432,11 @@ int tie_chunks(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask *mask, co
         if (batch->chunk_shape[d] != 1) inner_kept = ((axes_mask >> d) & 1u) ? 0 : 1;
     }
     // (a full reduction: a wave per chunk, four chunks per workgroup)
-    int group = kept == 1 ? pyas::kWave : inner_kept == 1 ? 1 : red >= 1024 ? pyas::kWave : 16;
+    // short calls (< 256 reduced elements, e.g. C3 (2,): 64) take a lane per
+    // output too, 4 positions per step: a group of 16 per output walked the
+    // chunk's 4096 outputs 4 at a time per wave, one chain of dependent loads
+    // each (13 ms per C3 query at 50 % zeros)
+    int group = kept == 1 ? pyas::kWave : inner_kept == 1 ? 1 : red >= 1024 ? pyas::kWave : red >= 256 ? 16 : 1;
     const char *e_group = getenv("PYAS_TIE_GROUP");   // per call: tests force each layout
     if (e_group && *e_group) {
         const int g = atoi(e_group);

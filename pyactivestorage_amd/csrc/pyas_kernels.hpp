@@ -3461,8 +3461,8 @@ __device__ void tie_setup(const TieChunkArgs &a, int64_t c, TieSetup &S) {
 template <typename T, int G>
 __global__ __launch_bounds__(kBlock) void k_tie_scan(TieChunkArgs a) {
     constexpr int NG = kBlock / G;
-    constexpr int V = G == kWave ? 4 : 1;     // elements per lane per step (8 measured slower:
-                                              // C3 full min 34.7 -> 47.6 us at 50 % zeros)
+    constexpr int V = G == 16 ? 1 : 4;        // elements per lane per step (8 measured slower for
+                                              // a wave: C3 full min 34.7 -> 47.6 us at 50 % zeros)
     constexpr int NW = kBlock / kWave;
     __shared__ TieSetup setups[NW];
     __shared__ uint8_t rank[64], arank[64];

@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--axes", default="none,0,2", help="comma list of 'none' or one axis (0/1/2)")
     ap.add_argument("--method", default="min")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--index", default="",
+                    help="a hyperslab, e.g. '1:1023' for every dim (cuts the edge chunks: the "
+                         "two-step path and its zero-sign passes instead of the fold)")
     a = ap.parse_args()
     import torch
     from pyactivestorage_amd.active import Active, release_resident
@@ -70,18 +73,22 @@ def main():
         attrs = {"_FillValue": np.array([-999.0], dtype=np.float32)}
         var = ChunkedVariable(name="zeros", shape=(n,) * 3, chunks=(c,) * 3, dtype=np.float32,
                               chunk_index=index, attrs=attrs, filename=path, filter_pipeline=None)
+        index = Ellipsis
+        if a.index:
+            lo, hi = (int(x) for x in a.index.split(":"))
+            index = (slice(lo, hi),) * 3
         for ax in a.axes.split(","):
             axis = None if ax == "none" else (int(ax),)
             act = Active(var, resident=True)
             getattr(act, a.method)(axis=axis)
-            r = act[...]                    # loads the chunks into HBM
-            act[...]
+            r = act[index]                  # loads the chunks into HBM
+            act[index]
             times = []
             for _ in range(a.reps):
                 getattr(act, a.method)(axis=axis)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                r = act[...]
+                r = act[index]
                 times.append(time.perf_counter() - t0)
             arr = np.ma.getdata(r)
             zero = arr == 0
@@ -93,7 +100,8 @@ def main():
     finally:
         if os.path.exists(path):
             os.unlink(path)
-    print(json.dumps({"workload": f"Active({a.method}, resident) over {n}^3 f32, 64^3 chunks, "
+    print(json.dumps({"workload": f"Active({a.method}, resident) over {n}^3 f32, 64^3 chunks"
+                                  f"{', index [' + a.index + ']^3' if a.index else ''}, "
                                   f"{a.zeros:.0%} of elements +-0.0, rest in [1, 1000)",
                       "results": res}))
 
