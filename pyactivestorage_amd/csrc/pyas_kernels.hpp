@@ -380,6 +380,60 @@ __device__ void run_rows(const ReduceArgs &a, const uint8_t *base, const Sel &s,
     }
 }
 
+// run_rows for runs at any alignment and of any length (a hyperslab cutting
+// an f32 row at element 1: [1:64] of a 64-element row).  Work items are
+// (outer index, group j of N consecutive positions of the run); a group
+// wholly inside the tile is one 16-B load at its element address (unaligned
+// global loads are allowed), a short group (the run's last, or one cut by
+// the tile's range [e0, e1)) reads its elements one by one.  The positions
+// taken are exactly [e0, e1), so the caller's unmasked count holds.
+template <typename T, bool BSWAP, int MASKED>
+__device__ void run_rows_any(const ReduceArgs &a, const uint8_t *base, const Sel &s, int k, int64_t L,
+                             int64_t e0, int64_t e1, TileAcc<T> &acc, const MaskT<T> &mk) {
+    constexpr int N = 16 / sizeof(T);
+    const int64_t Vr = (L + N - 1) / N;               // groups per run
+    const int64_t r0 = e0 / L, r1 = (e1 + L - 1) / L;  // runs touching [e0, e1)
+    const int64_t g0 = r0 * Vr, g1 = r1 * Vr;
+    const int64_t cut0 = e0 - r0 * L, cut1 = e1 - (r1 - 1) * L;   // first run from, last run to
+    Sel rs = s;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+        if (d == k) rs.cnt[d] = (int32_t)Vr;
+        else if (d > k) rs.cnt[d] = 1;
+    }
+    const uint32_t dm = (2u << k) - 1u;               // dims 0..k
+    int64_t inner0 = 0;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+        if (d == k) inner0 = (int64_t)s.start[d] * a.cstride[d];
+    RadixCounter rc;
+    rc.init(rs, a.ndim, dm, (uint64_t)(g0 + threadIdx.x), (uint64_t)kBlock);
+    for (int64_t g = g0 + threadIdx.x; g < g1; g += kBlock) {
+        int64_t mem = inner0;
+        int64_t j = 0;
+#pragma unroll
+        for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+            if (d < k) mem += sel_index(s, a.pool, d, rc.idx[d]) * a.cstride[d];
+            else if (d == k) j = rc.idx[d];
+        }
+        const int64_t lo = j * N, hi = lo + N < L ? lo + N : L;
+        int64_t elo = lo, ehi = hi;
+        if (g < g0 + Vr && cut0 > elo) elo = cut0;
+        if (g >= g1 - Vr && cut1 < ehi) ehi = cut1;
+        if (ehi - elo == N) {
+            uint4 r;
+            __builtin_memcpy(&r, base + (mem + lo) * (int64_t)sizeof(T), 16);
+            consume16<T, BSWAP, MASKED, false>(r, acc, mk);
+        } else {
+            for (int64_t i = elo; i < ehi; ++i) {
+                const T v = load_plain<T, BSWAP>(base, mem + i);
+                acc.template add_n<1, MASKED, false>(&v, mk);
+            }
+        }
+        rc.advance();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // combines (fixed order)
 // ---------------------------------------------------------------------------
@@ -698,9 +752,17 @@ __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
                     }
                 }
             }
+            // any unit-step innermost partial dim, no shuffle or tables: runs
+            // of L contiguous elements at any alignment (run_rows_any)
+            bool runs = !SHUF && !(a.tab.on[0] || a.tab.on[1]) && k >= 0;
+#pragma unroll
+            for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+                if (d == k && s.step[d] != 1) runs = false;
             if (k < 0 || (L * ES) % 16 != 0) rows = false;
             if (rows) {
                 run_rows<T, BSWAP, MASKED>(a, base, s, k, L, e0, e1, acc, mk);
+            } else if (runs) {
+                run_rows_any<T, BSWAP, MASKED>(a, base, s, k, L, e0, e1, acc, mk);
             } else {
                 generic = true;
                 run_generic<T, SHUF, BSWAP, MASKED>(a, base, s, e0, e1, acc, mk);
