@@ -408,29 +408,47 @@ __device__ void run_rows_any(const ReduceArgs &a, const uint8_t *base, const Sel
         if (d == k) inner0 = (int64_t)s.start[d] * a.cstride[d];
     RadixCounter rc;
     rc.init(rs, a.ndim, dm, (uint64_t)(g0 + threadIdx.x), (uint64_t)kBlock);
-    for (int64_t g = g0 + threadIdx.x; g < g1; g += kBlock) {
-        int64_t mem = inner0;
-        int64_t j = 0;
+    // U items per lane per step: their 16-B loads are issued together
+    constexpr int U = 4;
+    for (int64_t g = g0 + threadIdx.x; g < g1; g += U * kBlock) {
+        int64_t at[U], elo[U], ehi[U];
+        bool full[U];
 #pragma unroll
-        for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
-            if (d < k) mem += sel_index(s, a.pool, d, rc.idx[d]) * a.cstride[d];
-            else if (d == k) j = rc.idx[d];
+        for (int u = 0; u < U; ++u) {
+            const int64_t gu = g + (int64_t)u * kBlock;
+            int64_t mem = inner0, j = 0;
+#pragma unroll
+            for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+                if (d < k) mem += sel_index(s, a.pool, d, rc.idx[d]) * a.cstride[d];
+                else if (d == k) j = rc.idx[d];
+            }
+            const int64_t lo = j * N, hi = lo + N < L ? lo + N : L;
+            elo[u] = lo;
+            ehi[u] = gu < g1 ? hi : lo;   // past the tile: nothing
+            if (gu < g0 + Vr && cut0 > elo[u]) elo[u] = cut0;
+            if (gu >= g1 - Vr && cut1 < ehi[u]) ehi[u] = cut1;
+            if (ehi[u] < elo[u]) ehi[u] = elo[u];
+            at[u] = mem + lo;
+            full[u] = ehi[u] - elo[u] == N;
+            elo[u] += mem;
+            ehi[u] += mem;
+            if (gu < g1) rc.advance();
         }
-        const int64_t lo = j * N, hi = lo + N < L ? lo + N : L;
-        int64_t elo = lo, ehi = hi;
-        if (g < g0 + Vr && cut0 > elo) elo = cut0;
-        if (g >= g1 - Vr && cut1 < ehi) ehi = cut1;
-        if (ehi - elo == N) {
-            uint4 r;
-            __builtin_memcpy(&r, base + (mem + lo) * (int64_t)sizeof(T), 16);
-            consume16<T, BSWAP, MASKED, false>(r, acc, mk);
-        } else {
-            for (int64_t i = elo; i < ehi; ++i) {
-                const T v = load_plain<T, BSWAP>(base, mem + i);
-                acc.template add_n<1, MASKED, false>(&v, mk);
+        uint4 r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (full[u]) __builtin_memcpy(&r[u], base + at[u] * (int64_t)sizeof(T), 16);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (full[u]) {
+                consume16<T, BSWAP, MASKED, false>(r[u], acc, mk);
+            } else {
+                for (int64_t i = elo[u]; i < ehi[u]; ++i) {   // a short group: element by element
+                    const T v = load_plain<T, BSWAP>(base, i);
+                    acc.template add_n<1, MASKED, false>(&v, mk);
+                }
             }
         }
-        rc.advance();
     }
 }
 
