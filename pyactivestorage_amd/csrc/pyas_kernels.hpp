@@ -406,44 +406,64 @@ __device__ void run_rows_any(const ReduceArgs &a, const uint8_t *base, const Sel
 #pragma unroll
     for (int d = 0; d < PYAS_MAX_DIMS; ++d)
         if (d == k) inner0 = (int64_t)s.start[d] * a.cstride[d];
+    // the digits of item g (dims 0..k-1, then the group j at dim k) and its
+    // run's memory offset, both stepped by kBlock items per iteration without
+    // multiplies: ud[d] = the offset of one index of dim d (< k), incu/cntu
+    // = ud times the digit's increment / count (32-bit: chunks < 2^31 elems)
     RadixCounter rc;
     rc.init(rs, a.ndim, dm, (uint64_t)(g0 + threadIdx.x), (uint64_t)kBlock);
+    int32_t ud[PYAS_MAX_DIMS], incu[PYAS_MAX_DIMS], cntu[PYAS_MAX_DIMS];
+    int64_t mem64 = inner0;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+        ud[d] = d < k ? (int32_t)((int64_t)s.step[d] * a.cstride[d]) : 0;
+        incu[d] = (int32_t)rc.inc[d] * ud[d];
+        cntu[d] = (int32_t)rc.cnt[d] * ud[d];
+        if (d < k) mem64 += sel_index(s, a.pool, d, rc.idx[d]) * a.cstride[d];
+    }
+    int32_t mem = (int32_t)mem64;
     // U items per lane per step: their 16-B loads are issued together
     constexpr int U = 4;
     for (int64_t g = g0 + threadIdx.x; g < g1; g += U * kBlock) {
-        int64_t at[U], elo[U], ehi[U];
+        int32_t at[U], elo[U], ehi[U];
         bool full[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t gu = g + (int64_t)u * kBlock;
-            int64_t mem = inner0, j = 0;
+            int32_t j = 0;
 #pragma unroll
-            for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
-                if (d < k) mem += sel_index(s, a.pool, d, rc.idx[d]) * a.cstride[d];
-                else if (d == k) j = rc.idx[d];
-            }
-            const int64_t lo = j * N, hi = lo + N < L ? lo + N : L;
-            elo[u] = lo;
-            ehi[u] = gu < g1 ? hi : lo;   // past the tile: nothing
-            if (gu < g0 + Vr && cut0 > elo[u]) elo[u] = cut0;
-            if (gu >= g1 - Vr && cut1 < ehi[u]) ehi[u] = cut1;
-            if (ehi[u] < elo[u]) ehi[u] = elo[u];
+            for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+                if (d == k) j = (int32_t)rc.idx[d];
+            const int32_t lo = j * N, hi = lo + N < L ? lo + N : (int32_t)L;
+            int32_t el = lo, eh = gu < g1 ? hi : lo;   // past the tile: nothing
+            if (gu < g0 + Vr && cut0 > el) el = (int32_t)cut0;
+            if (gu >= g1 - Vr && cut1 < eh) eh = (int32_t)cut1;
+            if (eh < el) eh = el;
             at[u] = mem + lo;
-            full[u] = ehi[u] - elo[u] == N;
-            elo[u] += mem;
-            ehi[u] += mem;
-            if (gu < g1) rc.advance();
+            full[u] = eh - el == N;
+            elo[u] = mem + el;
+            ehi[u] = mem + eh;
+            // next item: kBlock further (carry-propagating, offset kept in step)
+            uint32_t carry = 0;
+#pragma unroll
+            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+                const uint32_t x = rc.idx[d] + rc.inc[d] + carry;
+                const uint32_t c2 = x >= rc.cnt[d] ? 1u : 0u;
+                rc.idx[d] = c2 ? x - rc.cnt[d] : x;
+                mem += incu[d] + (carry ? ud[d] : 0) - (c2 ? cntu[d] : 0);
+                carry = c2;
+            }
         }
         uint4 r[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (full[u]) __builtin_memcpy(&r[u], base + at[u] * (int64_t)sizeof(T), 16);
+            if (full[u]) __builtin_memcpy(&r[u], base + (int64_t)at[u] * (int64_t)sizeof(T), 16);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (full[u]) {
                 consume16<T, BSWAP, MASKED, false>(r[u], acc, mk);
             } else {
-                for (int64_t i = elo[u]; i < ehi[u]; ++i) {   // a short group: element by element
+                for (int32_t i = elo[u]; i < ehi[u]; ++i) {   // a short group: element by element
                     const T v = load_plain<T, BSWAP>(base, i);
                     acc.template add_n<1, MASKED, false>(&v, mk);
                 }
@@ -772,10 +792,12 @@ __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
             }
             // any unit-step innermost partial dim, no shuffle or tables: runs
             // of L contiguous elements at any alignment (run_rows_any)
-            bool runs = !SHUF && !(a.tab.on[0] || a.tab.on[1]) && k >= 0;
+            bool runs = !SHUF && !(a.tab.on[0] || a.tab.on[1]) && k >= 0 && a.chunk_elems < (int64_t(1) << 31);
 #pragma unroll
-            for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+            for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
                 if (d == k && s.step[d] != 1) runs = false;
+                if (d < k && s.step[d] == 0) runs = false;   // an index list: the generic walk
+            }
             if (k < 0 || (L * ES) % 16 != 0) rows = false;
             if (rows) {
                 run_rows<T, BSWAP, MASKED>(a, base, s, k, L, e0, e1, acc, mk);
