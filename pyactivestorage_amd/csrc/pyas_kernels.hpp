@@ -454,19 +454,32 @@ __device__ void run_rows_any(const ReduceArgs &a, const uint8_t *base, const Sel
                 carry = c2;
             }
         }
+        // every load of the step is issued before anything is consumed: a
+        // short group (nearly every step has some: one per run) loads its
+        // elements at clamped addresses beside the 16-B loads (a dependent
+        // load per element made the step wait on each)
         uint4 r[U];
+        T xs[U][N];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (full[u]) __builtin_memcpy(&r[u], base + (int64_t)at[u] * (int64_t)sizeof(T), 16);
+        for (int u = 0; u < U; ++u) {
+            if (full[u]) {
+                __builtin_memcpy(&r[u], base + (int64_t)at[u] * (int64_t)sizeof(T), 16);
+            } else if (ehi[u] > elo[u]) {
+#pragma unroll
+                for (int t = 0; t < N; ++t) {
+                    const int32_t i = elo[u] + t < ehi[u] ? elo[u] + t : ehi[u] - 1;
+                    xs[u][t] = load_plain<T, BSWAP>(base, i);
+                }
+            }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (full[u]) {
                 consume16<T, BSWAP, MASKED, false>(r[u], acc, mk);
             } else {
-                for (int32_t i = elo[u]; i < ehi[u]; ++i) {   // a short group: element by element
-                    const T v = load_plain<T, BSWAP>(base, i);
-                    acc.template add_n<1, MASKED, false>(&v, mk);
-                }
+#pragma unroll
+                for (int t = 0; t < N; ++t)
+                    if (elo[u] + t < ehi[u]) acc.template add_n<1, MASKED, false>(&xs[u][t], mk);
             }
         }
     }
