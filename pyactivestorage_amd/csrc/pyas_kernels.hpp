@@ -3092,13 +3092,20 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
                     if (__ballot(slow)) {
                         uint64_t Z = 0;
                         if (slow) {
+                            // the lane's zero bits shifted in (its first element
+                            // ends up highest), then reversed to element order at
+                            // the lane's offset: one shift-or per element
+                            using ZT = typename std::conditional<H == 1, uint64_t, uint32_t>::type;
+                            ZT zl = 0;
                             for (int i = 0; i < VH; ++i) {
                                 T xe[N];
                                 unpack16<T, BSWAP>(row[i], xe);
 #pragma unroll
-                                for (int k = 0; k < N; ++k)
-                                    Z |= (uint64_t)(xe[k] == (T)0 ? 1u : 0u) << ((h * VH + i) * N + k);
+                                for (int k = 0; k < N; ++k) zl = (ZT)((zl << 1) | (xe[k] == (T)0 ? 1u : 0u));
                             }
+                            const int J = VH * N;
+                            if constexpr (H == 1) Z = __builtin_bitreverse64(zl) >> (64 - J);
+                            else Z = (uint64_t)(__builtin_bitreverse32(zl) >> (32 - J)) << (h * J);
                         }
 #pragma unroll
                         for (int mm = H / 2; mm >= 1; mm >>= 1) Z |= shfl_xor(Z, mm);
