@@ -2377,9 +2377,12 @@ __device__ __forceinline__ void col_walk_layers(const AxesDense &d, int64_t n, c
 // sum is stored at sink[(layer - l0) * sstride + k * IB] instead of being
 // added to w[k].sum (the second half of a split column, added in order by
 // the first half's lane).
-// ZS: zs[k] tracks output k's last zero in (layer, row) order -- 0 none, 1
-// +0.0, 2 -0.0 (the elementwise rule both NumPy reductions follow when the
-// innermost dim is kept; k_axes_fold_lean writes it to a zero min/max).
+// ZS: zs[k] tracks output k's last zero in (layer, row) order: the word of
+// that zero holding its sign bit, kZsNone while none (the elementwise rule
+// both NumPy reductions follow when the innermost dim is kept;
+// k_axes_fold_lean writes it to a zero min/max).
+constexpr uint32_t kZsNone = 1u;   // no zero seen (a zero's sign word is 0 or 0x80000000)
+
 template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int DEPTH, bool SINK, bool NT, bool ZS,
           typename LB>
 __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t off0, int64_t l0,
@@ -2421,8 +2424,17 @@ __device__ __forceinline__ void lean_walk(const AxesDense &d, int64_t n, int64_t
                 T x[N];
                 unpack16<T, BSWAP>(buf[u], x);
 #pragma unroll
-                for (int k = 0; k < N; ++k)
-                    if (x[k] == (T)0) zs[k] = __builtin_signbit(x[k]) ? 2u : 1u;
+                for (int k = 0; k < N; ++k) {   // a compare and a select per element
+                    uint32_t hi;                   // the word holding the sign bit
+                    if constexpr (sizeof(T) == 4) {
+                        __builtin_memcpy(&hi, &x[k], 4);
+                    } else {
+                        uint64_t b;
+                        __builtin_memcpy(&b, &x[k], 8);
+                        hi = (uint32_t)(b >> 32);
+                    }
+                    zs[k] = x[k] == (T)0 ? hi : zs[k];
+                }
             }
         };
         col_walk_layers<T, SHUF, BSWAP, MASKED, AL, DEPTH, NT, 1>(d, n, &off0, l0, n_layers, mk, layer_base, acc,
@@ -2526,7 +2538,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         w[k].init();
-        zs[k] = 0;
+        zs[k] = kZsNone;
     }
     // AL_ / NT_: compile-time aligned walk / non-temporal plane loads
     auto walk = [&](auto al_c, auto nt_c) {
@@ -2579,15 +2591,15 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LEAN_WAVES) void k_axes_fol
             w[k].count += (int64_t)s_cnt[k * IB + il];
             if constexpr (ZS) {   // the second half's layers come later
                 const uint32_t z2 = s_zs[k * IB + il];
-                zs[k] = z2 ? z2 : zs[k];
+                zs[k] = z2 != kZsNone ? z2 : zs[k];
             }
         }
     }
     if constexpr (ZS) {
 #pragma unroll
         for (int k = 0; k < N; ++k) {
-            const T z = zs[k] == 2u ? -(T)0 : (T)0;
-            if (zs[k] && w[k].count > 0) {
+            const T z = (zs[k] >> 31) ? -(T)0 : (T)0;
+            if (zs[k] != kZsNone && w[k].count > 0) {
                 if ((g.zs & 1u) && w[k].mn == (T)0) w[k].mn = z;
                 if ((g.zs & 2u) && w[k].mx == (T)0) w[k].mx = z;
             }
