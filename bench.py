@@ -77,9 +77,10 @@ def parse(argv=None):
     p.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                    help="weak: each GPU adds its own slab of the variable (dim 0); "
                         "strong: one variable of the config's shape split across GPUs")
-    p.add_argument("--extra", default="c4,c5",
+    p.add_argument("--extra", default="c4,c5,c3_slab,c3_stride",
                    help="comma list of configs also measured at this N with strong scaling "
-                        "(reported under 'extra'; 'none' to skip)")
+                        "(reported under 'extra'; 'none' to skip); c3_slab / c3_stride: the "
+                        "reference's query shapes through Active on C3 (N=1 only)")
     p.add_argument("--extra-steps", type=int, default=20)
     p.add_argument("--cpu-chunks", type=int, default=4096,
                    help="chunks in the CPU-baseline sample (0 = skip)")
@@ -639,6 +640,117 @@ def run_config(env, name, scaling, steps, warmup, args, full_check=False):
     return rep, achieved
 
 
+# The reference's own query shapes at C3 size (tests/unit/test_active_axis.py:30-39:
+# ragged hyperslabs, strides and index lists x axis subsets), each an
+# Active.__getitem__ on resident chunks (active.py:487-516 -> storage.py:95).
+def _list64():
+    return np.sort(np.random.default_rng(7).choice(1024, size=64, replace=False))
+
+
+ACTIVE_EXTRAS = {
+    # name: [(label, index builder, axis, method)]
+    "c3_slab": [
+        ("[1:1023]^3", lambda: (slice(1, 1023),) * 3, None, "mean"),
+        ("[1:1023]^3", lambda: (slice(1, 1023),) * 3, None, "min"),
+        ("[0:1023]^3", lambda: (slice(0, 1023),) * 3, None, "mean"),
+        ("[4:1020]^3", lambda: (slice(4, 1020),) * 3, None, "mean"),
+        ("[1:1023]^3", lambda: (slice(1, 1023),) * 3, (0,), "mean"),
+        ("[1:1023]^3", lambda: (slice(1, 1023),) * 3, (2,), "mean"),
+        ("[1:1023]^3", lambda: (slice(1, 1023),) * 3, (0,), "min"),
+        ("[1:1023]^3", lambda: (slice(1, 1023),) * 3, (2,), "min"),
+    ],
+    "c3_stride": [
+        ("[:, 0:1024:3, :]", lambda: (slice(None), slice(0, 1024, 3), slice(None)), None, "mean"),
+        ("[:, :, 0:1024:4]", lambda: (slice(None), slice(None), slice(0, 1024, 4)), None, "mean"),
+        ("[:, list64, :]", lambda: (slice(None), _list64(), slice(None)), None, "mean"),
+        ("[:, 0:1024:3, :]", lambda: (slice(None), slice(0, 1024, 3), slice(None)), (0,), "mean"),
+        ("[:, :, 0:1024:4]", lambda: (slice(None), slice(None), slice(0, 1024, 4)), (1,), "mean"),
+    ],
+}
+
+
+def _dim_indices(ix, n):
+    """Selected indices of one dim (slice or index array), sorted unique."""
+    if isinstance(ix, slice):
+        return np.arange(n)[ix]
+    return np.unique(np.asarray(ix))
+
+
+def selected_and_touched(index, shape, chunks, es, line=128):
+    """Selected bytes of an orthogonal index, and the bytes of the 128-B
+    lines they touch (chunk rows line-aligned: the innermost chunk extent
+    times the itemsize is a multiple of `line`)."""
+    per = [_dim_indices(ix, n) for ix, n in zip(index, shape)]
+    sel = int(np.prod([len(p) for p in per])) * es
+    rows = int(np.prod([len(p) for p in per[:-1]]))
+    inner, ci = per[-1], chunks[-1]
+    assert (ci * es) % line == 0
+    lines = len(np.unique((inner // ci) * (ci * es // line) + (inner % ci) * es // line))
+    return sel, rows * lines * line
+
+
+def run_active_extra(env, name, steps, warmup):
+    """The reference's query shapes on C3 (ACTIVE_EXTRAS[name]): an
+    ``Active(resident=True)`` query per step over the C3 variable held in HBM
+    (attach_resident: no file), timed end to end (planning, launches, the
+    combine, the result copy; the repeated query replays its cached plan).
+    ``frac`` is on the selected bytes; for strides also on the touched
+    128-B lines (the bytes HBM must deliver)."""
+    torch, dev, rank = env["torch"], env["dev"], env["rank"]
+    from pyactivestorage_amd.active import Active, attach_resident, release_resident
+    from pyactivestorage_amd.synthetic import chunk_major_device
+    from pyactivestorage_amd.variable import ChunkedVariable
+    cfg = CONFIGS["c3"]
+    dt = np.dtype(cfg["dtype"])
+    shape, chunks = cfg["shape"], cfg["chunks"]
+    data, offsets, _ = chunk_major_device(torch, shape, chunks, dt, dev, fill=FILL, fill_frac=0.01,
+                                          seed=0, shuffle=False)
+    torch.cuda.synchronize()
+    grid = [s // c for s, c in zip(shape, chunks)]
+    cb = int(np.prod(chunks)) * dt.itemsize
+    index = {co: (int(offsets[k]), cb) for k, co in enumerate(np.ndindex(*grid))}
+    attrs = {"_FillValue": np.array([FILL], dtype=dt), "valid_min": np.array([VMIN], dtype=dt),
+             "valid_max": np.array([VMAX], dtype=dt)}
+    var = ChunkedVariable(name=name, shape=shape, chunks=chunks, dtype=dt, chunk_index=index, attrs=attrs,
+                          filename=None, filter_pipeline=None)
+    attach_resident(var, data.data_ptr(), device=dev.index or 0, owner=data)
+    out = []
+    try:
+        for label, mk, axis, method in ACTIVE_EXTRAS[name]:
+            ix = mk()
+            act = Active(var, resident=True, device=dev.index or 0)
+            for _ in range(max(warmup, 1)):
+                getattr(act, method)(axis=axis)   # a query's method lasts one __getitem__
+                act[ix]
+            times = []
+            for _ in range(steps):
+                getattr(act, method)(axis=axis)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                act[ix]
+                times.append(time.perf_counter() - t0)
+            ms = float(np.median(times)) * 1e3
+            sel, touched = selected_and_touched(ix, shape, chunks, dt.itemsize)
+            rep = {"index": label, "axis": list(axis) if axis else None, "method": method,
+                   "ms_per_step": round(ms, 4), "ms_min": round(min(times) * 1e3, 4),
+                   "selected_bytes": sel, "GBps": round(sel / (ms * 1e-3) / 1e9, 1),
+                   "frac": round(sel / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            if touched != sel:
+                rep["touched_line_bytes"] = touched
+                rep["frac_touched_lines"] = round(touched / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            out.append(rep)
+    finally:
+        release_resident(var)
+        del data
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return {"config": name, "workload": "Active(resident) queries over C3 (1024^3 f32, 64^3 chunks, "
+                                        "_FillValue + valid_min/valid_max), end to end per query",
+            "steps": steps, "queries": out,
+            "frac_basis": "selected bytes / median query time / 8 TB/s; strides also on the 128-B "
+                          "lines they touch"}
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -750,6 +862,10 @@ def main():
     extra = {}
     names = [] if args.extra in ("", "none") else [c.strip() for c in args.extra.split(",")]
     for name in names:
+        if name in ACTIVE_EXTRAS:
+            if world == 1:   # single-GPU query shapes (the N-rank curve is the head + C4/C5)
+                extra[name] = run_active_extra(env, name, args.extra_steps, args.warmup)
+            continue
         if name not in CONFIGS:
             raise SystemExit(f"bench.py: unknown --extra config {name!r}")
         rep, _ = run_config(env, name, "strong", args.extra_steps, args.warmup, args)

@@ -349,12 +349,28 @@ int pyas_combine_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
  * the global total, identical on every device; out[k][1 + j] the total of
  * device j.  mask may be NULL (unmasked) or hold one mask per device.
  * Asynchronous like every launch: synchronise streams[k] before reading.
+ * Bounded wait: with the environment variable PYAS_SHARD_TIMEOUT_MS set to
+ * a number >= 0 the call instead waits for the exchange up to that many
+ * milliseconds, polling the streams and ncclCommGetAsyncError; on expiry or
+ * an RCCL error it aborts the device list's communicators (ncclCommAbort),
+ * drops them from the cache and returns PYAS_EDEVICE naming the devices that
+ * had not finished.
+ * Thread safety: calls on the same device list are serialised from group
+ * start to group end (RCCL allows one group on a communicator at a time);
+ * pyas_shard_release waits for a call still using a set.
+ * Zero sign: a float min/max whose result is a zero keeps the sign the
+ * device reduction gives; storage.py/active.py's +0.0/-0.0 rule is applied
+ * by the per-device path (pyas_tie_chunks_total + pyas_tie_finalize) and by
+ * pyactivestorage_amd.distributed, not by this entry.
+ * RCCL is resolved from the process first (an RCCL already mapped, e.g.
+ * torch's), then librccl.so.1.
  * The multi-process equivalent (one process per GPU) is
  * pyactivestorage_amd.distributed over torch.distributed. */
 int pyas_reduce_sharded(pyas_ctx *const *ctx, const pyas_batch *const *per_dev,
                         const pyas_mask *const *mask, int32_t ndev, uint32_t combine_flags,
                         pyas_partial *const *out, void *const *streams);
-/* Destroy the cached RCCL communicators of pyas_reduce_sharded. */
+/* Destroy the cached RCCL communicators of pyas_reduce_sharded (waits for a
+ * call still using them). */
 int pyas_shard_release(void);
 
 /* Segmented fixed-order combine: out[s] = fold of in[index[k]] for k in

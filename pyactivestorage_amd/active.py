@@ -31,6 +31,8 @@ import concurrent.futures
 import os
 import threading
 
+import warnings
+
 import numpy as np
 
 from . import _lib, engine, selection, zerosign
@@ -148,6 +150,39 @@ def release_resident(variable) -> None:
         store["buf"].free()
 
 
+class _External:
+    """A device buffer owned by the caller (attach_resident): never freed here."""
+
+    def __init__(self, ptr, owner):
+        self.ptr = int(ptr)
+        self.owner = owner          # keeps the caller's allocation alive
+
+    def free(self):
+        self.owner = None
+
+
+def attach_resident(variable, ptr, device: int = 0, owner=None) -> None:
+    """Register chunks already decoded in HBM as ``variable``'s resident copy:
+    ``ptr`` holds every chunk of the variable's grid in C order, one slot of
+    ``ceil(chunk_bytes / 256) * 256`` bytes each, in the variable's dtype
+    and byte order (variables without filters only).  Resident-mode queries on
+    ``variable`` then read only HBM, as if an earlier query had loaded every
+    chunk (a producer on the GPU handing its output to the reduction without
+    a trip through a file).  ``owner`` (e.g. the torch tensor behind ``ptr``)
+    is kept alive until :func:`release_resident`."""
+    ds = variable
+    if ds.filter_pipeline:
+        raise NotImplementedError("attach_resident: variables with a filter pipeline")
+    grid = tuple(-(-s // c) for s, c in zip(ds.shape, ds.chunks))
+    n_all = int(np.prod(grid))
+    with _RESIDENT_LOCK:
+        if getattr(ds, "_pyas_resident", None) is not None:
+            raise ValueError("the variable already has a resident copy (release_resident first)")
+        ds._pyas_resident = {"device": int(device), "buf": _External(ptr, owner),
+                             "state": np.full(n_all, _LOADED, dtype=np.int8), "users": 0,
+                             "released": False}
+
+
 def _unhold(store) -> None:
     """A query that used ``store`` has finished (its stream is synchronised)."""
     with _RESIDENT_LOCK:
@@ -171,6 +206,15 @@ def _pipeline_groups(sizes, n_groups):
     edges = np.unique(np.concatenate([[0], np.minimum(cuts, z.size), [z.size]]))
     return [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:]) if b > a]
 
+
+
+def _sign_fallback(err):
+    """A zero-sign pass the device cannot run for this query (e.g. 2^31 or
+    more reduced elements per output: its scan keys are 32-bit).  The
+    reduction itself is complete; only the sign of a zero min/max is then
+    the device reduction's rather than NumPy's (storage.py:99-100)."""
+    warnings.warn(f"the sign of a zero min/max is not NumPy's for this query ({err})",
+                  RuntimeWarning, stacklevel=3)
 
 class Active:
     """GPU-backed ``Active`` over one chunked variable."""
@@ -688,8 +732,14 @@ class Active:
             n_all = plan.n_chunks if n_layers is None else int(n_layers)
             # level 1 only on the chunks the level-2 keys can pick (positions
             # decide which zero wins; the two candidates' signs are then exact)
-            engine.tie_chunks_total(ctx, plan.batch, plan.mask_up.struct, plan.tie_geom(), which,
-                                    plan.chunk_partials.ptr, int(layer_base), max(n_all, 1), st)
+            try:
+                engine.tie_chunks_total(ctx, plan.batch, plan.mask_up.struct, plan.tie_geom(), which,
+                                        plan.chunk_partials.ptr, int(layer_base), max(n_all, 1), st)
+            except NotImplementedError as e:
+                if keys is not None:
+                    raise
+                _sign_fallback(e)
+                return plan.read_total(st)
             kbuf = None
             if keys is not None:
                 kbuf = DeviceBuffer(ctx, 16)
@@ -725,8 +775,14 @@ class Active:
             engine.tie_grid(ctx, dt, rec["g"], None, t["flags"].ptr, t["lr"], which, rec["fin"].ptr, keys_ptr, st)
         else:   # per-chunk partials: compact records of the method (pyas_reduce_axes_ex)
             pw = which | (_lib.TIE_REC if rec.get("rec") else 0)
-            engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, geom, rec["axes_mask"], pw,
-                              rec["obuf"].ptr, rec["parts"].ptr, st)
+            try:
+                engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, geom, rec["axes_mask"], pw,
+                                  rec["obuf"].ptr, rec["parts"].ptr, st)
+            except NotImplementedError as e:
+                if keys_ptr is not None:
+                    raise
+                _sign_fallback(e)
+                return
             engine.tie_grid(ctx, dt, rec["g"], rec["parts"].ptr, None, t["lr"], pw, rec["fin"].ptr, keys_ptr,
                             st)
 

@@ -177,6 +177,11 @@ int prepare(const pyas_ctx *ctx, const pyas_batch *b, const pyas_mask *m, pyas::
     a.pool = b->index_pool;
     a.ndim = b->ndim;
     a.chunk_elems = elems;
+    {   // PYAS_SPANS (per call: tests and benches switch it): 0 off, 2 also the
+        // aligned runs run_rows streams, unset / 1 the default
+        const char *e = getenv("PYAS_SPANS");
+        a.spans = e && *e ? atoi(e) : 1;
+    }
     int64_t stride = 1;
     for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
         if (d < b->ndim) {
@@ -1003,6 +1008,17 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
     dense_geometry(x.d, batch, axes_mask, es, shuf ? es : 1, x.r.tab.on[0] || x.r.tab.on[1]);
     // Fully selected chunks go to k_axes_dense, the rest to k_reduce_axes
     // (each kernel skips the other's chunks); sel == NULL means all full.
+    // With selections, the dense launch also takes the cut chunks whose box
+    // covers at least half the chunk (cut_eligible: a hyperslab's edges),
+    // read whole with the box applied per row / element; the reduced
+    // positions' bit map must fit LDS.  PYAS_AXES_CUTS=0 leaves every cut
+    // chunk to k_reduce_axes.
+    {
+        const char *e = getenv("PYAS_AXES_CUTS");   // per call: tests and benches switch it
+        x.cuts = batch->sel && x.d.mode != 0 && !(e && *e == '0') &&
+                 x.d.RO * x.d.RI <= 32 * (int64_t)pyas::kCutMapWords &&
+                 x.r.chunk_elems < (int64_t(1) << 31);   // 32-bit index arithmetic
+    }
     // Streamed column layout (k_axes_col_stream): every chunk whole, one
     // lane per item column (split 1), rows in whole 4-row groups; each
     // workgroup walks cpb chunks as one ring of loads.  Measured on C3
@@ -1194,6 +1210,10 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
             }
             if (!inner_kept || lr2 != 1)
                 return fail(PYAS_ENOTSUP, "zero sign in the lean column fold: a reduction is not elementwise");
+            // the sign is NumPy's only where a tie rule was derived and
+            // validated for this dtype on this host (pyas.h: ENOTSUP otherwise)
+            if (!tie_of(ctx, batch->dtype))
+                return fail(PYAS_ENOTSUP, "zero sign in the lean column fold: no tie rule set for this dtype");
         } else if (x.d.mode >= 4) {
             // LDS row layout: each output row (RI elements, RO == KI == 1) is
             // one contiguous NumPy call; the rule comes from the context

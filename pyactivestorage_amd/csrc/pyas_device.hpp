@@ -345,6 +345,41 @@ template <typename T> struct TileAcc {
         if constexpr (TT<T>::kind == 0) return g != g;
         else return false;
     }
+    // N values of which only those whose bit is set in `sel` are selected
+    // (run_spans' in-span predicate, the dense kernels' cut chunks).  CNT:
+    // 0 the caller counts (unmasked tiles), 1 per-lane counts, 2 ballot
+    // counts (converged code only).  Returns whether this lane must run
+    // check_nan on its selected values.
+    template <int N, int MASKED, int CNT = (MASKED ? 2 : 0)>
+    __device__ __forceinline__ bool add_pred(const T *x, uint32_t sel, const MaskT<T> &mk) {
+        using G = typename GroupSum<T>::type;
+        constexpr int GS = N < 4 ? N : 4;
+        bool bad = false;
+#pragma unroll
+        for (int k0 = 0; k0 < N; k0 += GS) {
+            G g = 0;
+#pragma unroll
+            for (int k = k0; k < k0 + GS; ++k) {
+                const T v = x[k];
+                bool ok = ((sel >> k) & 1u) != 0;
+                if constexpr (MASKED) ok = ok && !mk.template masked_m<MASKED>(v);
+                if constexpr (TT<T>::kind == 0) {
+                    const T y = ok ? v : (T)__builtin_nan("");
+                    mn = tmin(mn, y);
+                    mx = tmax(mx, y);
+                } else {
+                    mn = tmin(mn, ok ? v : TT<T>::highest());
+                    mx = tmax(mx, ok ? v : TT<T>::lowest());
+                }
+                g += ok ? (G)v : (G)0;
+                if constexpr (CNT == 2) ucount += (uint32_t)__builtin_popcountll(__ballot(ok));
+                else if constexpr (CNT == 1) count += ok ? 1u : 0u;
+            }
+            sum += (S)g;
+            if constexpr (TT<T>::kind == 0) bad |= g != g;
+        }
+        return bad;
+    }
     // one element with an externally computed mask bit (generic path)
     __device__ __forceinline__ void add_one(T v, bool is_masked) {
         if constexpr (TT<T>::kind == 0) nan |= (v != v);

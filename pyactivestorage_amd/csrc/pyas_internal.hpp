@@ -23,6 +23,7 @@ struct ReduceArgs {
     int64_t chunk_elems;
     int64_t tpc;                      // tiles (workgroups) per chunk
     int32_t ndim;
+    int32_t spans;                    // run_spans: 0 off, 1 cut chunks run_rows cannot stream, 2 every cut chunk
     pyas_mask mask;
     MaskTab tab;
     pyas_partial *out;                // one partial per workgroup (tile b of chunk b / tpc)
@@ -43,6 +44,7 @@ struct FinishArgs {
     uint32_t flags;                   // PYAS_COMBINE_*
 };
 
+constexpr int kCutMapWords = 512;   // cut chunks' reduced-position bit map in LDS (16384 positions; + 1 pad word)
 constexpr int kAxesLds = 8192;   // reduced-index offsets kept in LDS (int32, 32 KiB)
 
 // Dense partial-axis geometry (k_axes_dense): the chunk dims merged into
@@ -75,6 +77,7 @@ struct AxesArgs {
     int32_t split;                    // column layout: splits of the reduced range
     bool vec;                         // geometry admits 16-B vector walks (kernel re-checks per chunk)
     int32_t rec;                      // per-chunk outputs: 0 pyas_partial, else a PYAS_REC_* record
+    bool cuts;                        // dense launch also takes cut chunks (box, >= half the chunk)
 };
 
 // pyas_reduce_axes_grid: the chunk layers of a whole-chunk box query folded

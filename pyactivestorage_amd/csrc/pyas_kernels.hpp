@@ -20,6 +20,21 @@
 
 namespace pyas {
 
+// Debug progress marks (tools/dbg harnesses only: -DPYAS_DBG): each thread
+// writes its last mark to host-mapped memory the host can poll while a
+// kernel runs.  Empty in the library build.
+#ifdef PYAS_DBG
+__device__ int *pyas_dbg_mark;
+#define PYAS_MARK(v)                                                                              \
+    do {                                                                                          \
+        if (pyas_dbg_mark)                                                                        \
+            __hip_atomic_store(pyas_dbg_mark + blockIdx.x * kBlock + threadIdx.x, (int)(v),        \
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                      \
+    } while (0)
+#else
+#define PYAS_MARK(v) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // vector un-shuffle: 16 consecutive elements from ES byte planes
 // ---------------------------------------------------------------------------
@@ -487,6 +502,307 @@ __device__ void run_rows_any(const ReduceArgs &a, const uint8_t *base, const Sel
     }
 }
 
+// 16 bytes at any element-aligned address (AL: 16-B aligned -> one load)
+template <bool AL>
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+    if constexpr (AL) {
+        return ldg16(reinterpret_cast<const uint4 *>(p));
+    } else {
+        uint4 r;
+        __builtin_memcpy(&r, p, 16);
+        return r;
+    }
+}
+
+// One byte-plane piece of a shuffled vector: W bytes at q (AL: W-aligned)
+#ifndef PYAS_PLANE_NT
+#define PYAS_PLANE_NT 1   // plane pieces loaded non-temporal (0: plain loads, a tuning variant)
+#endif
+template <typename W, bool AL, bool NT = true>
+__device__ __forceinline__ W ldp(const uint8_t *q) {
+    if constexpr (AL && NT && PYAS_PLANE_NT) {
+        return __builtin_nontemporal_load(reinterpret_cast<const W *>(q));
+    } else if constexpr (AL) {
+        return *reinterpret_cast<const W *>(q);
+    } else {
+        W r;
+        __builtin_memcpy(&r, q, sizeof(W));
+        return r;
+    }
+}
+
+// 16 bytes = N = 16/ES consecutive elements of the plain layout, addressed
+// by `p` in the plain layout of the chunk at `base` (n elements).  With SHUF
+// the chunk is HDF5-shuffled (byte b of element e at b*n + e), so those
+// elements are N consecutive bytes of each of the ES byte planes: ES loads
+// of N bytes (f32: 4 dwords, 256 contiguous bytes per plane per wave),
+// reassembled into the plain bytes with v_perm; the caller's unpack16 then
+// applies the byte order as for plain chunks.  AL: see ldv_aligned.
+// NT = false: plain loads for the plane pieces (the lean fold's walk over
+// rows whose plane pieces share 128-B lines, measured faster there).
+template <typename T, bool SHUF, bool AL, bool NT = true>
+__device__ __forceinline__ uint4 ldv(const uint8_t *base, const uint8_t *p, int64_t n) {
+    constexpr int ES = sizeof(T);
+    if constexpr (!SHUF || ES == 1) {
+        return ld16<AL>(p);
+    } else {
+        const uint8_t *q = base + ((uint64_t)(p - base) / ES);
+        if constexpr (ES == 4) {          // 4 planes x 4 bytes
+            uint32_t w[4], e[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) w[b] = ldp<uint32_t, AL, NT>(q + b * n);
+            transpose4(w[0], w[1], w[2], w[3], e);
+            return make_uint4(e[0], e[1], e[2], e[3]);
+        } else if constexpr (ES == 2) {   // 2 planes x 8 bytes
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 a = ldp<u32x2, AL, NT>(q), b = ldp<u32x2, AL, NT>(q + n);
+            return make_uint4(perm(b.x, a.x, 0x05010400u), perm(b.x, a.x, 0x07030602u),
+                              perm(b.y, a.y, 0x05010400u), perm(b.y, a.y, 0x07030602u));
+        } else {                          // 8 planes x 2 bytes
+            uint32_t h[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) h[b] = ldp<uint16_t, AL, NT>(q + b * n);
+            const uint32_t x01 = h[0] | (h[1] << 16), x23 = h[2] | (h[3] << 16);
+            const uint32_t x45 = h[4] | (h[5] << 16), x67 = h[6] | (h[7] << 16);
+            return make_uint4(perm(x23, x01, 0x06040200u), perm(x67, x45, 0x06040200u),
+                              perm(x23, x01, 0x07050301u), perm(x67, x45, 0x07050301u));
+        }
+    }
+}
+
+// Whether ldv<T, SHUF, true> may be used on the chunk at `base` of n elements:
+// plain: base 16-B aligned; shuffled: every plane piece W = 16/ES-aligned
+// (vector offsets are multiples of N elements in every dense layout).
+template <typename T, bool SHUF>
+__device__ __forceinline__ bool ldv_aligned(const uint8_t *base, int64_t n) {
+    constexpr int ES = sizeof(T), N = 16 / ES;
+    if constexpr (!SHUF || ES == 1) return ((uintptr_t)base & 15) == 0;
+    else return (((uintptr_t)base | (uint64_t)n) & (N - 1)) == 0;
+}
+
+// A load unit of the row layouts: VPL = (SHUF ? ES : 1) consecutive 16-B
+// vectors of the plain layout.  Shuffled, that is 16 consecutive elements =
+// one 16-B load from each of the ES byte planes (a wave reads 1 KiB of a
+// plane per instruction when its lanes' units are adjacent), transposed
+// into ES plain vectors with v_perm; the caller's unpack16 applies the byte
+// order as for plain chunks.  AL: see ldu_aligned.
+template <typename T, bool SHUF>
+struct Unit {
+    static constexpr int VPL = (SHUF && sizeof(T) > 1) ? (int)sizeof(T) : 1;
+};
+
+template <typename T, bool SHUF, bool AL>
+__device__ __forceinline__ void ldu(const uint8_t *base, const uint8_t *p, int64_t n,
+                                    uint4 v[Unit<T, SHUF>::VPL]) {
+    constexpr int ES = sizeof(T);
+    if constexpr (Unit<T, SHUF>::VPL == 1) {
+        v[0] = ld16<AL>(p);
+    } else {
+        const uint8_t *q = base + ((uint64_t)(p - base) / ES);
+        uint4 pl[ES];
+#pragma unroll
+        for (int b = 0; b < ES; ++b) pl[b] = ld16<AL>(q + b * n);
+        if constexpr (ES == 4) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t e[4];
+                transpose4(word(pl[0], j), word(pl[1], j), word(pl[2], j), word(pl[3], j), e);
+                v[j] = make_uint4(e[0], e[1], e[2], e[3]);
+            }
+        } else if constexpr (ES == 2) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t a0 = word(pl[0], 2 * j), b0 = word(pl[1], 2 * j);
+                const uint32_t a1 = word(pl[0], 2 * j + 1), b1 = word(pl[1], 2 * j + 1);
+                v[j] = make_uint4(perm(b0, a0, 0x05010400u), perm(b0, a0, 0x07030602u),
+                                  perm(b1, a1, 0x05010400u), perm(b1, a1, 0x07030602u));
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                uint32_t lo[4], hi[4];
+                transpose4(word(pl[0], w), word(pl[1], w), word(pl[2], w), word(pl[3], w), lo);
+                transpose4(word(pl[4], w), word(pl[5], w), word(pl[6], w), word(pl[7], w), hi);
+                v[2 * w] = make_uint4(lo[0], hi[0], lo[1], hi[1]);
+                v[2 * w + 1] = make_uint4(lo[2], hi[2], lo[3], hi[3]);
+            }
+        }
+    }
+}
+
+// Whether ldu<T, SHUF, true> may be used on the chunk at `base` of n
+// elements (unit offsets are multiples of 16 elements when shuffled).
+template <typename T, bool SHUF>
+__device__ __forceinline__ bool ldu_aligned(const uint8_t *base, int64_t n) {
+    if constexpr (Unit<T, SHUF>::VPL == 1) return ((uintptr_t)base & 15) == 0;
+    else return (((uintptr_t)base | (uint64_t)n) & 15) == 0;
+}
+
+// ---------------------------------------------------------------------------
+// spans with a per-lane predicate (cut chunks of hyperslabs, strides, lists)
+// ---------------------------------------------------------------------------
+// A selection is read as spans: the dims < kk are enumerated (each selected
+// index tuple is one span, any step or an index list), the dims >= kk are
+// inside the span: a run of `ext` chunk elements starting `m_in` elements
+// into the span's outer row, of which those at multiples of `istep` are
+// selected (istep > 1 only for a strided innermost dim).  When every span
+// starts at the same offset `off` from a 16-B boundary (16-element boundary
+// when shuffled), a span is G aligned groups and a lane keeps ONE group
+// position j for the whole tile: its in-span predicate (which of its group's
+// elements are selected) is computed once, and every group is one aligned
+// 16-B load (ES plane loads when shuffled) -- no element loads, no per-item
+// bookkeeping beyond the span address.  The groups at either end of a span
+// read a few unselected bytes of the same 16-B line; those never cross a
+// page (a page boundary is 16-B aligned) and sit in 128-B lines the span's
+// own bytes already fetch.
+struct SpanPlan {
+    int kk;              // dims < kk: enumerated; dims >= kk: inside a span
+    int32_t m_in;        // memory offset of a span's first element in its outer row
+    int32_t ext;         // memory extent of a span (elements)
+    int32_t istep;       // in-span step (1, or the innermost dim's |step|)
+    int32_t off;         // elements from the group boundary to a span's first element
+    int32_t G, P;        // aligned groups per span; spans per block pass (P * G <= kBlock)
+    int64_t nspans;      // spans in the chunk's selection
+    int64_t per_span;    // selected elements per span
+};
+
+template <typename T, bool SHUF>
+__device__ __forceinline__ bool span_plan(const ReduceArgs &a, const uint8_t *base, const Sel &s,
+                                          SpanPlan &sp) {
+    constexpr int ES = sizeof(T);
+    constexpr bool SH = SHUF && ES > 1;
+    constexpr int NU = SH ? 16 : 16 / ES;   // elements per aligned group
+    if (a.tab.on[0] || a.tab.on[1] || a.chunk_elems >= (int64_t(1) << 31)) return false;
+    if (SH && ((((uintptr_t)base) | (uint64_t)a.chunk_elems) & 15) != 0) return false;
+    // innermost dim that is not whole
+    int k = -1;
+#pragma unroll
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d)
+        if (d < a.ndim && k < 0 &&
+            !(s.step[d] == 1 && s.start[d] == 0 && (int64_t)s.cnt[d] == a.shape[d]))
+            k = d;
+    if (k < 0) return false;
+    int64_t cs_k = 1, sk = 1, st_k = 0, cn_k = 1;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+        if (d == k) { cs_k = a.cstride[d]; sk = s.step[d]; st_k = s.start[d]; cn_k = s.cnt[d]; }
+    if (sk < 0) { st_k += (cn_k - 1) * sk; sk = -sk; }   // same elements, ascending
+    // three span forms (written as selects: a branch-per-form version of this
+    // lost the `ext` of the last form at -O1 and above, ROCm 7.2 hipcc)
+    const bool run = sk == 1;                             // a run of whole inner rows
+    const bool strided = !run && sk > 1 && k == a.ndim - 1;   // strided innermost dim
+    // otherwise: a list, or strided with inner rows -> dim k enumerated too
+    sp.kk = (run || strided) ? k : k + 1;
+    const int64_t m_in = run ? st_k * cs_k : strided ? st_k : 0;
+    const int64_t ext = run ? cn_k * cs_k : strided ? (cn_k - 1) * sk + 1 : cs_k;
+    sp.m_in = (int32_t)m_in;
+    sp.ext = (int32_t)ext;
+    sp.istep = strided ? (int32_t)sk : 1;
+    sp.per_span = run ? cn_k * cs_k : strided ? cn_k : cs_k;
+    // every span must start at the same offset from a group boundary
+    int64_t m0 = sp.m_in, nsp = 1;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+        if (d < sp.kk) {
+            nsp *= s.cnt[d];
+            if (s.cnt[d] > 0) m0 += sel_index(s, a.pool, d, 0) * a.cstride[d];
+            if (s.cnt[d] > 1) {
+                const int64_t delta = (s.step[d] != 0 ? (int64_t)s.step[d] : 1) * a.cstride[d];
+                if (SH ? (delta & 15) != 0 : ((delta * ES) & 15) != 0) return false;
+            }
+        }
+    }
+    sp.nspans = nsp;
+    sp.off = SH ? (int32_t)(m0 & 15) : (int32_t)((((uintptr_t)base + (uint64_t)(m0 * ES)) & 15) / ES);
+    const int64_t G = (sp.off + (int64_t)sp.ext + NU - 1) / NU;
+    if (G < 1 || G > kBlock) return false;
+    sp.G = (int32_t)G;
+    sp.P = (int32_t)(kBlock / G);
+    return true;
+}
+
+// Spans [q0, q1) of the chunk at `base` (plan sp).  Lane tid reads group
+// j = tid % G of spans tid / G + P*i; U groups per lane in flight.  Counts:
+// masked tiles count through ballots, unmasked ones are counted by the caller
+// ((q1 - q0) * per_span).
+template <typename T, bool SHUF, bool BSWAP, int MASKED>
+__device__ void run_spans(const ReduceArgs &a, const uint8_t *base, const Sel &s, const SpanPlan &sp,
+                          int64_t q0, int64_t q1, TileAcc<T> &acc, const MaskT<T> &mk) {
+    constexpr int ES = sizeof(T);
+    constexpr bool SH = SHUF && ES > 1;
+    constexpr int N = 16 / ES;                // elements per plain 16-B vector
+    constexpr int VPL = SH ? ES : 1;          // plain vectors per group
+    constexpr int NU = N * VPL;               // elements per group
+    const int tid = threadIdx.x;
+    const int p = tid / sp.G, j = tid - p * sp.G;
+    uint32_t bits = 0;                        // this lane's selected group elements
+    if (p < sp.P) {
+#pragma unroll
+        for (int t = 0; t < NU; ++t) {
+            const int32_t x = j * NU - sp.off + t;
+            if (x >= 0 && x < sp.ext && x % sp.istep == 0) bits |= 1u << t;
+        }
+    }
+    const uint32_t dm = (1u << sp.kk) - 1u;
+    RadixCounter rc;
+    rc.init(s, a.ndim, dm, (uint64_t)(q0 + p), (uint64_t)sp.P);
+    // span-independent part of a group's address (elements; may be -off < 0)
+    const int32_t gofs = j * NU - sp.off + sp.m_in;
+    const int64_t nit = (q1 - q0 + sp.P - 1) / sp.P;
+    // groups in flight per lane: 4, or 8 plain vectors' worth when shuffled
+    // (f64: one group = 8 vectors; 4 of them took k_reduce_u to ~300 VGPRs)
+    constexpr int U = VPL == 1 ? 4 : (8 / VPL > 0 ? 8 / VPL : 1);
+    int64_t q = q0 + p;
+    for (int64_t it = 0; it < nit; it += U) {
+        uint4 r[U][VPL];
+        bool on[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            on[u] = bits != 0 && q < q1;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) r[u][v] = make_uint4(0u, 0u, 0u, 0u);
+            if (on[u]) {
+                int32_t mem = gofs;
+#pragma unroll
+                for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+                    if (d < sp.kk) mem += (int32_t)sel_index(s, a.pool, d, rc.idx[d]) * (int32_t)a.cstride[d];
+                if constexpr (SH) {
+                    ldu<T, true, true>(base, base + (int64_t)mem * ES, a.chunk_elems, r[u]);
+                } else {
+                    r[u][0] = ldg16(reinterpret_cast<const uint4 *>(base + (int64_t)mem * ES));
+                }
+            }
+            rc.advance();
+            q += sp.P;
+        }
+        bool bad = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t b = on[u] ? bits : 0u;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+                T x[N];
+                unpack16<T, BSWAP>(r[u][v], x);
+                bad |= acc.template add_pred<N, MASKED>(x, b >> (v * N), mk);
+            }
+        }
+        if (__builtin_expect(__ballot(bad) != 0, 0)) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t b = on[u] ? bits : 0u;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v) {
+                    T x[N];
+                    unpack16<T, BSWAP>(r[u][v], x);
+#pragma unroll
+                    for (int t = 0; t < N; ++t)
+                        if ((b >> (v * N + t)) & 1u) acc.template check_nan<1>(&x[t]);
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // combines (fixed order)
 // ---------------------------------------------------------------------------
@@ -717,6 +1033,70 @@ __global__ __launch_bounds__(kBlock) void k_finish(FinishArgs f) {
     if (threadIdx.x == 0) store_wpartial(f.total, tot);
 }
 
+// Is the selection one contiguous run of chunk memory?  (innermost non-full
+// dim has unit step; every dim outside it picks one index; no mask tables)
+// *m0 = the memory index of its first element.
+__device__ __forceinline__ bool sel_contiguous(const ReduceArgs &a, const Sel &s, int64_t *m0) {
+    bool contig = !(a.tab.on[0] || a.tab.on[1]);
+    bool seen_partial = false;
+    int64_t m = 0;
+#pragma unroll
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+        if (d < a.ndim) {
+            const bool full = s.step[d] == 1 && s.start[d] == 0 && (int64_t)s.cnt[d] == a.shape[d];
+            if (seen_partial) {
+                if (s.cnt[d] > 1) contig = false;
+            } else if (!full) {
+                seen_partial = true;
+                if (s.cnt[d] > 1 && s.step[d] != 1) contig = false;
+            }
+            if (s.cnt[d] > 0) m += sel_index(s, a.pool, d, 0) * a.cstride[d];
+        }
+    }
+    *m0 = m;
+    return contig;
+}
+
+// Rows of 16-B vectors (run_rows)?  No shuffle or tables, unit-step
+// innermost partial dim *k, every run (*L elements) 16-B aligned.
+template <typename T, bool SHUF>
+__device__ __forceinline__ bool rows_aligned(const ReduceArgs &a, const uint8_t *base, const Sel &s,
+                                             int *kp, int64_t *Lp) {
+    constexpr int64_t ES = sizeof(T);
+    int k = -1;
+    int64_t L = 1;
+    bool rows = !SHUF && !(a.tab.on[0] || a.tab.on[1]) && ((uintptr_t)base & 15) == 0;
+#pragma unroll
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+        if (d < a.ndim) {
+            if (k < 0) {
+                const bool full = s.step[d] == 1 && s.start[d] == 0 && (int64_t)s.cnt[d] == a.shape[d];
+                if (!full) {
+                    k = d;
+                    if (s.step[d] != 1) rows = false;
+                    if (((int64_t)s.start[d] * a.cstride[d] * ES) % 16 != 0) rows = false;
+                    L *= s.cnt[d];
+                } else {
+                    L *= a.shape[d];
+                }
+            } else if ((a.cstride[d] * ES) % 16 != 0) {
+                rows = false;  // an outer dim whose rows start unaligned
+            }
+        }
+    }
+    if (k < 0 || (L * ES) % 16 != 0) rows = false;
+    *kp = k;
+    *Lp = L;
+    return rows;
+}
+
+// The predicate stream (run_spans) for cut chunks; ReduceArgs::spans picks
+// where it runs at run time (1: not on chunks whose aligned runs run_rows
+// streams); PYAS_SPANS=0 builds it out.
+#ifndef PYAS_SPANS
+#define PYAS_SPANS 1
+#endif
+
 // ---------------------------------------------------------------------------
 // the hot kernel
 // ---------------------------------------------------------------------------
@@ -751,60 +1131,39 @@ __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
     int64_t total = 1;
 #pragma unroll
     for (int d = 0; d < PYAS_MAX_DIMS; ++d) total *= (int64_t)s.cnt[d];
+#if PYAS_SPANS
+    // cut chunks whose spans fit one block pass: the predicate stream,
+    // tiled by whole spans (unless the selection is one contiguous run,
+    // which run_plain / run_shuffled stream at the whole-chunk rate)
+    int64_t m0s = 0;
+    int ks = -1;
+    int64_t Ls = 1;
+    if (a.spans && total > 0 && !sel_contiguous(a, s, &m0s)) {
+        SpanPlan sp;
+        if (span_plan<T, SHUF>(a, base, s, sp) && (a.spans == 2 || !rows_aligned<T, SHUF>(a, base, s, &ks, &Ls))) {
+            const int64_t per = (sp.nspans + a.tpc - 1) / a.tpc;
+            const int64_t q0 = t * per, q1 = q0 + per < sp.nspans ? q0 + per : sp.nspans;
+            if (q0 < q1) run_spans<T, SHUF, BSWAP, MASKED>(a, base, s, sp, q0, q1, acc, mk);
+            tile_finish(acc, (!MASKED && q0 < q1) ? (uint64_t)((q1 - q0) * sp.per_span) : 0u, tout);
+            return;
+        }
+    }
+#endif
     int64_t per = (total + a.tpc - 1) / a.tpc;
     per = (per + 63) & ~(int64_t)63;
     const int64_t e0 = t * per, e1 = e0 + per < total ? e0 + per : total;
     bool generic = false;
     if (e0 < e1) {
-        // Is the selection one contiguous run of chunk memory?  (innermost
-        // non-full dim has unit step; every dim outside it picks one index)
-        bool contig = !(a.tab.on[0] || a.tab.on[1]);
-        bool seen_partial = false;
         int64_t m0 = 0;
-#pragma unroll
-        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-            if (d < a.ndim) {
-                const bool full = s.step[d] == 1 && s.start[d] == 0 && (int64_t)s.cnt[d] == a.shape[d];
-                if (seen_partial) {
-                    if (s.cnt[d] > 1) contig = false;
-                } else if (!full) {
-                    seen_partial = true;
-                    if (s.cnt[d] > 1 && s.step[d] != 1) contig = false;
-                }
-                if (s.cnt[d] > 0) m0 += sel_index(s, a.pool, d, 0) * a.cstride[d];
-            }
-        }
-        if (contig) {
+        if (sel_contiguous(a, s, &m0)) {
             if constexpr (SHUF && sizeof(T) > 1)
                 run_shuffled<T, BSWAP, MASKED>(base, a.chunk_elems, m0 + e0, m0 + e1, acc, mk);
             else
                 run_plain<T, BSWAP, MASKED>(base, m0 + e0, m0 + e1, acc, mk);
         } else {
-            // rows of 16-B vectors?  (no shuffle/tables, unit-step innermost
-            // partial dim k, everything 16-B aligned)
-            constexpr int64_t ES = sizeof(T);
             int k = -1;
             int64_t L = 1;
-            bool rows = !SHUF && !(a.tab.on[0] || a.tab.on[1]) && ((uintptr_t)base & 15) == 0;
-#pragma unroll
-            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-                if (d < a.ndim) {
-                    if (k < 0) {
-                        const bool full = s.step[d] == 1 && s.start[d] == 0 &&
-                                          (int64_t)s.cnt[d] == a.shape[d];
-                        if (!full) {
-                            k = d;
-                            if (s.step[d] != 1) rows = false;
-                            if (((int64_t)s.start[d] * a.cstride[d] * ES) % 16 != 0) rows = false;
-                            L *= s.cnt[d];
-                        } else {
-                            L *= a.shape[d];
-                        }
-                    } else if ((a.cstride[d] * ES) % 16 != 0) {
-                        rows = false;  // an outer dim whose rows start unaligned
-                    }
-                }
-            }
+            const bool rows = rows_aligned<T, SHUF>(a, base, s, &k, &L);
             // any unit-step innermost partial dim, no shuffle or tables: runs
             // of L contiguous elements at any alignment (run_rows_any)
             bool runs = !SHUF && !(a.tab.on[0] || a.tab.on[1]) && k >= 0 && a.chunk_elems < (int64_t(1) << 31);
@@ -813,7 +1172,6 @@ __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
                 if (d == k && s.step[d] != 1) runs = false;
                 if (d < k && s.step[d] == 0) runs = false;   // an index list: the generic walk
             }
-            if (k < 0 || (L * ES) % 16 != 0) rows = false;
             // (aligned rows stay on run_rows: through run_rows_any they measured
             // slower, C3 [4:1020]^3 0.96 -> 1.08 ms and C5 86.9 -> 66.7 %)
             if (rows) {
@@ -1398,142 +1756,6 @@ __device__ __forceinline__ bool chunk_is_full(const Sel &s, const int64_t *shape
     return full;
 }
 
-// 16 bytes at any element-aligned address (AL: 16-B aligned -> one load)
-template <bool AL>
-__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
-    if constexpr (AL) {
-        return ldg16(reinterpret_cast<const uint4 *>(p));
-    } else {
-        uint4 r;
-        __builtin_memcpy(&r, p, 16);
-        return r;
-    }
-}
-
-// One byte-plane piece of a shuffled vector: W bytes at q (AL: W-aligned)
-#ifndef PYAS_PLANE_NT
-#define PYAS_PLANE_NT 1   // plane pieces loaded non-temporal (0: plain loads, a tuning variant)
-#endif
-template <typename W, bool AL, bool NT = true>
-__device__ __forceinline__ W ldp(const uint8_t *q) {
-    if constexpr (AL && NT && PYAS_PLANE_NT) {
-        return __builtin_nontemporal_load(reinterpret_cast<const W *>(q));
-    } else if constexpr (AL) {
-        return *reinterpret_cast<const W *>(q);
-    } else {
-        W r;
-        __builtin_memcpy(&r, q, sizeof(W));
-        return r;
-    }
-}
-
-// 16 bytes = N = 16/ES consecutive elements of the plain layout, addressed
-// by `p` in the plain layout of the chunk at `base` (n elements).  With SHUF
-// the chunk is HDF5-shuffled (byte b of element e at b*n + e), so those
-// elements are N consecutive bytes of each of the ES byte planes: ES loads
-// of N bytes (f32: 4 dwords, 256 contiguous bytes per plane per wave),
-// reassembled into the plain bytes with v_perm; the caller's unpack16 then
-// applies the byte order as for plain chunks.  AL: see ldv_aligned.
-// NT = false: plain loads for the plane pieces (the lean fold's walk over
-// rows whose plane pieces share 128-B lines, measured faster there).
-template <typename T, bool SHUF, bool AL, bool NT = true>
-__device__ __forceinline__ uint4 ldv(const uint8_t *base, const uint8_t *p, int64_t n) {
-    constexpr int ES = sizeof(T);
-    if constexpr (!SHUF || ES == 1) {
-        return ld16<AL>(p);
-    } else {
-        const uint8_t *q = base + ((uint64_t)(p - base) / ES);
-        if constexpr (ES == 4) {          // 4 planes x 4 bytes
-            uint32_t w[4], e[4];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) w[b] = ldp<uint32_t, AL, NT>(q + b * n);
-            transpose4(w[0], w[1], w[2], w[3], e);
-            return make_uint4(e[0], e[1], e[2], e[3]);
-        } else if constexpr (ES == 2) {   // 2 planes x 8 bytes
-            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-            const u32x2 a = ldp<u32x2, AL, NT>(q), b = ldp<u32x2, AL, NT>(q + n);
-            return make_uint4(perm(b.x, a.x, 0x05010400u), perm(b.x, a.x, 0x07030602u),
-                              perm(b.y, a.y, 0x05010400u), perm(b.y, a.y, 0x07030602u));
-        } else {                          // 8 planes x 2 bytes
-            uint32_t h[8];
-#pragma unroll
-            for (int b = 0; b < 8; ++b) h[b] = ldp<uint16_t, AL, NT>(q + b * n);
-            const uint32_t x01 = h[0] | (h[1] << 16), x23 = h[2] | (h[3] << 16);
-            const uint32_t x45 = h[4] | (h[5] << 16), x67 = h[6] | (h[7] << 16);
-            return make_uint4(perm(x23, x01, 0x06040200u), perm(x67, x45, 0x06040200u),
-                              perm(x23, x01, 0x07050301u), perm(x67, x45, 0x07050301u));
-        }
-    }
-}
-
-// Whether ldv<T, SHUF, true> may be used on the chunk at `base` of n elements:
-// plain: base 16-B aligned; shuffled: every plane piece W = 16/ES-aligned
-// (vector offsets are multiples of N elements in every dense layout).
-template <typename T, bool SHUF>
-__device__ __forceinline__ bool ldv_aligned(const uint8_t *base, int64_t n) {
-    constexpr int ES = sizeof(T), N = 16 / ES;
-    if constexpr (!SHUF || ES == 1) return ((uintptr_t)base & 15) == 0;
-    else return (((uintptr_t)base | (uint64_t)n) & (N - 1)) == 0;
-}
-
-// A load unit of the row layouts: VPL = (SHUF ? ES : 1) consecutive 16-B
-// vectors of the plain layout.  Shuffled, that is 16 consecutive elements =
-// one 16-B load from each of the ES byte planes (a wave reads 1 KiB of a
-// plane per instruction when its lanes' units are adjacent), transposed
-// into ES plain vectors with v_perm; the caller's unpack16 applies the byte
-// order as for plain chunks.  AL: see ldu_aligned.
-template <typename T, bool SHUF>
-struct Unit {
-    static constexpr int VPL = (SHUF && sizeof(T) > 1) ? (int)sizeof(T) : 1;
-};
-
-template <typename T, bool SHUF, bool AL>
-__device__ __forceinline__ void ldu(const uint8_t *base, const uint8_t *p, int64_t n,
-                                    uint4 v[Unit<T, SHUF>::VPL]) {
-    constexpr int ES = sizeof(T);
-    if constexpr (Unit<T, SHUF>::VPL == 1) {
-        v[0] = ld16<AL>(p);
-    } else {
-        const uint8_t *q = base + ((uint64_t)(p - base) / ES);
-        uint4 pl[ES];
-#pragma unroll
-        for (int b = 0; b < ES; ++b) pl[b] = ld16<AL>(q + b * n);
-        if constexpr (ES == 4) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                uint32_t e[4];
-                transpose4(word(pl[0], j), word(pl[1], j), word(pl[2], j), word(pl[3], j), e);
-                v[j] = make_uint4(e[0], e[1], e[2], e[3]);
-            }
-        } else if constexpr (ES == 2) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const uint32_t a0 = word(pl[0], 2 * j), b0 = word(pl[1], 2 * j);
-                const uint32_t a1 = word(pl[0], 2 * j + 1), b1 = word(pl[1], 2 * j + 1);
-                v[j] = make_uint4(perm(b0, a0, 0x05010400u), perm(b0, a0, 0x07030602u),
-                                  perm(b1, a1, 0x05010400u), perm(b1, a1, 0x07030602u));
-            }
-        } else {
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                uint32_t lo[4], hi[4];
-                transpose4(word(pl[0], w), word(pl[1], w), word(pl[2], w), word(pl[3], w), lo);
-                transpose4(word(pl[4], w), word(pl[5], w), word(pl[6], w), word(pl[7], w), hi);
-                v[2 * w] = make_uint4(lo[0], hi[0], lo[1], hi[1]);
-                v[2 * w + 1] = make_uint4(lo[2], hi[2], lo[3], hi[3]);
-            }
-        }
-    }
-}
-
-// Whether ldu<T, SHUF, true> may be used on the chunk at `base` of n
-// elements (unit offsets are multiples of 16 elements when shuffled).
-template <typename T, bool SHUF>
-__device__ __forceinline__ bool ldu_aligned(const uint8_t *base, int64_t n) {
-    if constexpr (Unit<T, SHUF>::VPL == 1) return ((uintptr_t)base & 15) == 0;
-    else return (((uintptr_t)base | (uint64_t)n) & 15) == 0;
-}
-
 template <int CTRL, typename V>
 __device__ __forceinline__ V dpp_mov(V v) {
     if constexpr (sizeof(V) <= 4) {
@@ -1636,6 +1858,155 @@ __device__ __forceinline__ void store_group(const TileAcc<T> &a, uint32_t cnt, u
 #define PYAS_WAVES_FLOOR_8 PYAS_WAVES_FLOOR_(8)
 #define PYAS_XATTR(W) PYAS_WAVES_FLOOR(W)
 
+// ---------------------------------------------------------------------------
+// cut chunks in the dense kernels
+// ---------------------------------------------------------------------------
+// A chunk cut by a box selection (a hyperslab's edge: unit steps, at least
+// half the chunk selected) is read by the dense kernels as its whole chunk:
+// the reduced elements outside the box are excluded (a per-row bit from an
+// LDS map in the column layouts, per-element bits in the row layouts) and
+// the outputs outside it are not written; those inside go to their place in
+// the chunk's partial array (C order over the box's kept extents).  The
+// bytes outside the box are still read: at most half the chunk by the
+// eligibility rule, ~1.6 % per cut dim at a [1:1023] edge of 64^3 chunks.
+struct CutBox {
+    int32_t lo[PYAS_MAX_DIMS], hi[PYAS_MAX_DIMS];   // the box, chunk coordinates
+    int64_t ost[PYAS_MAX_DIMS];                    // kept dims: output strides; reduced: 0
+};
+
+// Whether the dense launch (a.cuts) takes this cut chunk; identical in the
+// dense kernels and k_reduce_axes, which leaves it to them.
+__device__ __forceinline__ bool cut_eligible(const AxesArgs &a, const Sel &s) {
+    if (!a.cuts) return false;
+    int64_t sel = 1, all = 1;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+        if (d < a.r.ndim) {
+            if (s.step[d] != 1 && s.cnt[d] != 1) return false;   // a box: unit steps (or one index)
+            if (s.cnt[d] < 1) return false;
+            sel *= s.cnt[d];
+            all *= a.r.shape[d];
+        }
+    }
+    return 2 * sel >= all;
+}
+
+__device__ __forceinline__ void cut_box(const AxesArgs &a, const Sel &s, CutBox &cb) {
+    int64_t st = 1;
+#pragma unroll
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+        cb.lo[d] = 0;
+        cb.hi[d] = 1;
+        cb.ost[d] = 0;
+        if (d < a.r.ndim) {
+            cb.lo[d] = (int32_t)sel_index(s, a.r.pool, d, 0);
+            cb.hi[d] = cb.lo[d] + s.cnt[d];
+            if (!((a.axes >> d) & 1u)) {
+                cb.ost[d] = st;
+                st *= s.cnt[d];
+            }
+        }
+    }
+}
+
+// Kept index f (C order over the kept dims, whole-chunk extents) -> its
+// place in the cut chunk's partial array, or -1 outside the box.  32-bit
+// arithmetic (a.cuts needs chunks under 2^31 elements).
+__device__ __forceinline__ int64_t cut_out(const AxesArgs &a, const CutBox &cb, int64_t fi) {
+    uint32_t f = (uint32_t)fi;
+    int64_t o = 0;
+    bool in = true;
+#pragma unroll
+    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+        if (d < a.r.ndim && !((a.axes >> d) & 1u)) {
+            const uint32_t n = (uint32_t)a.r.shape[d], q = f / n, c = f - q * n;
+            f = q;
+            in = in && (int32_t)c >= cb.lo[d] && (int32_t)c < cb.hi[d];
+            o += ((int64_t)c - cb.lo[d]) * cb.ost[d];
+        }
+    }
+    return in ? o : -1;
+}
+
+// The kept coordinates of consecutive kept indices f0, f0 + 1, ... (a
+// column item's N outputs): one decomposition, then carry-propagating steps.
+struct CutWalk {
+    int32_t c[PYAS_MAX_DIMS];
+    __device__ __forceinline__ void init(const AxesArgs &a, int64_t f0) {
+        uint32_t f = (uint32_t)f0;
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            c[d] = 0;
+            if (d < a.r.ndim && !((a.axes >> d) & 1u)) {
+                const uint32_t n = (uint32_t)a.r.shape[d], q = f / n;
+                c[d] = (int32_t)(f - q * n);
+                f = q;
+            }
+        }
+    }
+    // place of the current index in the cut chunk's array, or -1
+    __device__ __forceinline__ int64_t out(const AxesArgs &a, const CutBox &cb) const {
+        int64_t o = 0;
+        bool in = true;
+#pragma unroll
+        for (int d = 0; d < PYAS_MAX_DIMS; ++d) {
+            if (d < a.r.ndim && !((a.axes >> d) & 1u)) {
+                in = in && c[d] >= cb.lo[d] && c[d] < cb.hi[d];
+                o += (int64_t)(c[d] - cb.lo[d]) * cb.ost[d];
+            }
+        }
+        return in ? o : -1;
+    }
+    __device__ __forceinline__ void step(const AxesArgs &a) {
+        bool carry = true;
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            if (carry && d < a.r.ndim && !((a.axes >> d) & 1u)) {
+                ++c[d];
+                carry = c[d] >= (int32_t)a.r.shape[d];
+                if (carry) c[d] = 0;
+            }
+        }
+    }
+};
+
+// Bit map over the reduced positions r (C order over the reduced dims,
+// whole-chunk extents; the column layouts' row r = ro * RI + ri, the row
+// layouts' element ro * RI + x): bit r set iff r lies in the box.  Built by
+// the whole block; nr <= 32 * kCutMapWords (host-checked).
+__device__ __forceinline__ void cut_map(const AxesArgs &a, const CutBox &cb, int64_t nr, uint32_t *map) {
+    const int64_t nw = (nr + 31) / 32;
+    for (int64_t w = threadIdx.x; w < nw; w += kBlock) {
+        uint32_t bits = 0;
+        for (int b = 0; b < 32; ++b) {
+            uint32_t r = (uint32_t)(w * 32 + b);
+            bool in = (int64_t)r < nr;
+#pragma unroll
+            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+                if (d < a.r.ndim && ((a.axes >> d) & 1u)) {
+                    const uint32_t n = (uint32_t)a.r.shape[d], q = r / n, c = r - q * n;
+                    r = q;
+                    in = in && (int32_t)c >= cb.lo[d] && (int32_t)c < cb.hi[d];
+                }
+            }
+            bits |= in ? 1u << b : 0u;
+        }
+        map[w] = bits;
+    }
+    if (threadIdx.x == 0) map[nw] = 0;   // cut_bits may read one word past the end
+    __syncthreads();
+}
+
+// Bits [r, r + n) of the map (n <= 32), bit 0 = position r.
+__device__ __forceinline__ uint32_t cut_bits(const uint32_t *map, int64_t r, int n) {
+    const int64_t w = r >> 5;
+    const int sh = (int)(r & 31);
+    uint64_t v = map[w];
+    if (sh + n > 32) v |= (uint64_t)map[w + 1] << 32;
+    const uint64_t m = n >= 32 ? 0xffffffffull : ((1ull << n) - 1);
+    return (uint32_t)((v >> sh) & m);
+}
+
 // U rows of N outputs (16-B vectors w[u]) into acc[N]: output k's U rows as
 // groups of 4 (sums widened once per group, one mask test per element,
 // per-lane counts), one NaN ballot for all of them.
@@ -1660,12 +2031,38 @@ __device__ __forceinline__ void col_consume(const uint4 *w, TileAcc<T> *acc, con
     }
 }
 
+// col_consume for a cut chunk: only rows whose bit is set in `rows` (bit u =
+// row u of the step) count; per-lane counts, masked or not.
+template <typename T, bool BSWAP, int MASKED, int U>
+__device__ __forceinline__ void col_consume_p(const uint4 *w, TileAcc<T> *acc, const MaskT<T> &mk, uint32_t rows) {
+    constexpr int N = 16 / sizeof(T);
+    T xs[N][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        T x[N];
+        unpack16<T, BSWAP>(w[u], x);
+#pragma unroll
+        for (int k = 0; k < N; ++k) xs[k][u] = x[k];
+    }
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < N; ++k) bad |= acc[k].template add_pred<U, MASKED, 1>(xs[k], rows, mk);
+    if (__builtin_expect(__ballot(bad) != 0, 0)) {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if ((rows >> u) & 1u) acc[k].template check_nan<1>(&xs[k][u]);
+    }
+}
+
 // One pass of the column layout over one chunk: lane (il, sp) folds split
 // sp of the reduced rows of vector item i (N consecutive kept outputs) into
 // acc[N], PYAS_COL_U 16-B loads in flight.
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, bool CUT = false>
 __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base, int64_t n, int64_t i,
-                                         int sp, const MaskT<T> &mk, TileAcc<T> *acc) {
+                                         int sp, const MaskT<T> &mk, TileAcc<T> *acc,
+                                         const uint32_t *rmap = nullptr) {
     constexpr int ES = sizeof(T), N = 16 / ES;
     const int S = d.split;
     const int64_t KIV = d.KI / N, R = d.RO * d.RI;
@@ -1688,16 +2085,30 @@ __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base
         uint4 w[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) { w[u] = ldv<T, SHUF, AL>(base, p, n); next(); }
-        col_consume<T, BSWAP, MASKED, U>(w, acc, mk);
+        if constexpr (CUT) {
+            uint32_t rb = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) rb |= cut_bits(rmap, sp + (t + u) * S, 1) << u;
+            col_consume_p<T, BSWAP, MASKED, U>(w, acc, mk, rb);
+        } else {
+            col_consume<T, BSWAP, MASKED, U>(w, acc, mk);
+        }
     }
     for (; t < nt; ++t) {
         T x[N];
         unpack16<T, BSWAP>(ldv<T, SHUF, AL>(base, p, n), x);
         next();
+        if constexpr (CUT) {
+            const uint32_t rb = cut_bits(rmap, sp + t * S, 1);
 #pragma unroll
-        for (int k = 0; k < N; ++k) acc[k].template add_n<1, MASKED, false>(x + k, mk);
+            for (int k = 0; k < N; ++k)
+                if (acc[k].template add_pred<1, MASKED, 1>(x + k, rb, mk)) acc[k].template check_nan<1>(x + k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc[k].template add_n<1, MASKED, false>(x + k, mk);
+        }
     }
-    if constexpr (!MASKED) {   // add_n counts only in masked mode
+    if constexpr (!MASKED && !CUT) {   // add_n counts only in masked mode
 #pragma unroll
         for (int k = 0; k < N; ++k) acc[k].count += (uint32_t)nt;
     }
@@ -1709,9 +2120,10 @@ __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base
 #ifndef PYAS_COL_RING
 #define PYAS_COL_RING 1
 #endif
-template <typename T, bool SHUF, bool BSWAP, int MASKED>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool CUT = false>
 __device__ __forceinline__ void col_rows_ring(const AxesDense &d, const uint8_t *base, int64_t n, int64_t i,
-                                              int sp, const MaskT<T> &mk, TileAcc<T> *acc) {
+                                              int sp, const MaskT<T> &mk, TileAcc<T> *acc,
+                                              const uint32_t *rmap = nullptr) {
     constexpr int ES = sizeof(T), N = 16 / ES, U = PYAS_COL_U;
     const int S = d.split;
     const int64_t KIV = d.KI / N, R = d.RO * d.RI;
@@ -1732,6 +2144,17 @@ __device__ __forceinline__ void col_rows_ring(const AxesDense &d, const uint8_t 
             if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
         }
     };
+    // rows of group g: sp + (g * U + u) * S (CUT: their bits from the map)
+    auto rbits = [&](int64_t g) -> uint32_t {
+        uint32_t rb = 0;
+        if (S == 1) {
+            rb = cut_bits(rmap, sp + g * U, U);
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) rb |= cut_bits(rmap, sp + (g * U + u) * S, 1) << u;
+        }
+        return rb;
+    };
     uint4 buf[2][U];
     if (ng > 0) fetch(buf[0]);
     if (ng > 1) fetch(buf[1]);
@@ -1743,7 +2166,8 @@ __device__ __forceinline__ void col_rows_ring(const AxesDense &d, const uint8_t 
 #pragma unroll
                 for (int u = 0; u < U; ++u) cur[u] = buf[s][u];
                 if (g + s + 2 < ng) fetch(buf[s]);
-                col_consume<T, BSWAP, MASKED, U>(cur, acc, mk);
+                if constexpr (CUT) col_consume_p<T, BSWAP, MASKED, U>(cur, acc, mk, rbits(g + s));
+                else col_consume<T, BSWAP, MASKED, U>(cur, acc, mk);
             }
         }
     }
@@ -1753,10 +2177,17 @@ __device__ __forceinline__ void col_rows_ring(const AxesDense &d, const uint8_t 
         p += step_off;
         ri += dr;
         if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
+        if constexpr (CUT) {
+            const uint32_t rb = cut_bits(rmap, sp + t * S, 1);
 #pragma unroll
-        for (int k = 0; k < N; ++k) acc[k].template add_n<1, MASKED, false>(x + k, mk);
+            for (int k = 0; k < N; ++k)
+                if (acc[k].template add_pred<1, MASKED, 1>(x + k, rb, mk)) acc[k].template check_nan<1>(x + k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc[k].template add_n<1, MASKED, false>(x + k, mk);
+        }
     }
-    if constexpr (!MASKED) {
+    if constexpr (!MASKED && !CUT) {
 #pragma unroll
         for (int k = 0; k < N; ++k) acc[k].count += (uint32_t)nt;
     }
@@ -1832,9 +2263,10 @@ __device__ void col_rows_units(const AxesDense &d, const uint8_t *base, int64_t 
     }
 }
 
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, bool CUT = false>
 __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
-                          const MaskT<T> &mk, uint4 *stage) {
+                          const MaskT<T> &mk, uint4 *stage, const CutBox *cb = nullptr,
+                          const uint32_t *rmap = nullptr) {
     constexpr int ES = sizeof(T), N = 16 / ES;
     const AxesDense &d = a.d;
     const int IT = d.it, S = d.split;
@@ -1844,7 +2276,7 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     // aligned chunks: the ring walk (measured faster than the shuffled unit
     // exchange too); PYAS_COL_RING=0 builds the earlier walks
     constexpr bool ring = PYAS_COL_RING && AL;
-    const bool units = !ring && SHUF && AL && col_units_ok<T>(d) && ldu_aligned<T, SHUF>(base, a.r.chunk_elems);
+    const bool units = !CUT && !ring && SHUF && AL && col_units_ok<T>(d) && ldu_aligned<T, SHUF>(base, a.r.chunk_elems);
     for (int64_t i0 = j * IT; i0 < items; i0 += d.bpc * IT) {   // block-uniform
         const int64_t i = i0 + il;
         TileAcc<T> acc[N];
@@ -1852,8 +2284,8 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
         for (int k = 0; k < N; ++k) acc[k].init();
         if constexpr (ring) {
             if (i < items && sp < S && sp < d.RO * d.RI)
-                col_rows_ring<T, SHUF, BSWAP, MASKED>(d, base, a.r.chunk_elems, i, sp, mk, acc);
-        } else if constexpr (SHUF && sizeof(T) >= 4) {
+                col_rows_ring<T, SHUF, BSWAP, MASKED, CUT>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap);
+        } else if constexpr (SHUF && sizeof(T) >= 4 && !CUT) {
             if (units) {
                 if (i < items && sp < S) col_rows_units<T, BSWAP, MASKED>(d, base, a.r.chunk_elems, i, sp, mk, acc, stage);
                 __syncthreads();   // the exchange area is reused below
@@ -1861,9 +2293,34 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
                 col_rows<T, SHUF, BSWAP, MASKED, AL>(d, base, a.r.chunk_elems, i, sp, mk, acc);
             }
         } else if (i < items && sp < S && sp < d.RO * d.RI) {
-            col_rows<T, SHUF, BSWAP, MASKED, AL>(d, base, a.r.chunk_elems, i, sp, mk, acc);
+            col_rows<T, SHUF, BSWAP, MASKED, AL, CUT>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap);
         }
-        if constexpr (N <= 4) {
+        if constexpr (CUT) {
+            PYAS_MARK(3);
+            // outputs inside the box only, each at its place in the cut
+            // chunk's partial array (not a contiguous range: direct stores)
+            if constexpr (N <= 4) {
+                if (S > 1) fold_splits_n<T, N>(acc, S, IT, il, sp, stage);
+            }
+            CutWalk cw;
+            cw.init(a, i * N);   // kept index ko * KI + v * N of the item's first output
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                if constexpr (N > 4) {
+                    if (S > 1) fold_splits(acc[k], S, IT, il, sp);
+                }
+                if (sp == 0 && i < items) {
+                    const int64_t o = cw.out(a, *cb);
+                    if (o >= 0) {
+                        pyas_partial pp;
+                        tile_store_lane(acc[k], &pp);
+                        put_out<T>(a, ob + o, pp);
+                    }
+                }
+                cw.step(a);
+            }
+            PYAS_MARK(4);
+        } else if constexpr (N <= 4) {
             // Stage the pass's IT*N partials (<= 32 KiB) in LDS, then write
             // them as consecutive 16-B stores (a lane's own N partials are
             // 32*N bytes apart from its neighbours').  The split fold uses
@@ -1895,11 +2352,43 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     }
 }
 
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int UO>
+// U units of VPL vectors into acc, the elements of unit u selected by bits
+// ub[u] (bit e = element e of the unit): a cut chunk's row layouts.
+template <typename T, bool BSWAP, int MASKED, int U, int VPL>
+__device__ __forceinline__ void consume_units_p(const uint4 *w, const uint32_t *ub, TileAcc<T> &acc,
+                                                const MaskT<T> &mk) {
+    constexpr int N = 16 / sizeof(T);
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+            T x[N];
+            unpack16<T, BSWAP>(w[u * VPL + v], x);
+            bad |= acc.template add_pred<N, MASKED, 1>(x, ub[u] >> (v * N), mk);
+        }
+    }
+    if (__builtin_expect(__ballot(bad) != 0, 0)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+                T x[N];
+                unpack16<T, BSWAP>(w[u * VPL + v], x);
+#pragma unroll
+                for (int t = 0; t < N; ++t)
+                    if ((ub[u] >> (v * N + t)) & 1u) acc.template check_nan<1>(&x[t]);
+            }
+        }
+    }
+}
+
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int UO, bool CUT = false>
 __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
-                          const MaskT<T> &mk) {
+                          const MaskT<T> &mk, const CutBox *cb = nullptr, const uint32_t *rmap = nullptr) {
     const int64_t n = a.r.chunk_elems;
     constexpr int ES = sizeof(T), N = 16 / ES, VPL = Unit<T, SHUF>::VPL;
+    constexpr int NU = N * VPL;                      // elements per load unit
     const AxesDense &d = a.d;
     const int G = d.group, P = kWave / G;
     const int lane = threadIdx.x & (kWave - 1), gl = lane & (G - 1), pg = lane / G;
@@ -1922,39 +2411,54 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
                 const int64_t o = o0 + u * P + pg;
                 if (o < d.KO) ldu<T, SHUF, AL>(base, base + (o * d.RI + gl * N * VPL) * ES, n, w[u]);
             }
+            uint32_t ub = 0;
+            if constexpr (CUT) ub = cut_bits(rmap, (int64_t)gl * NU, NU);
 #pragma unroll
             for (int u = 0; u < UO; ++u) {
                 const int64_t o = o0 + u * P + pg;
                 if (o < d.KO) {
-                    consume16_u<T, BSWAP, MASKED, false, VPL>(w[u], acc[u], mk);
-                    if constexpr (!MASKED) acc[u].count += N * VPL;
+                    if constexpr (CUT) {
+                        consume_units_p<T, BSWAP, MASKED, 1, VPL>(w[u], &ub, acc[u], mk);
+                    } else {
+                        consume16_u<T, BSWAP, MASKED, false, VPL>(w[u], acc[u], mk);
+                        if constexpr (!MASKED) acc[u].count += N * VPL;
+                    }
                 }
             }
         } else {
             const int64_t o = o0 + pg;
             if (o < d.KO) {
                 const uint8_t *p = base + (o * d.RI + gl * N * VPL) * ES;
-                int64_t vc = 0;
+                int64_t vc = 0, ro = 0;
                 auto next = [&]() {
                     p += vstep;
-                    if (++vc == VG) { vc = 0; p += wrap; }
+                    if (++vc == VG) { vc = 0; ++ro; p += wrap; }
                 };
                 // units in flight: 4 plain vectors, or 2 (f32) / 1 (f64) shuffled units
                 constexpr int U = VPL == 1 ? 4 : (VPL >= 8 ? 1 : 8 / VPL);
                 int64_t t = 0;
                 for (; t + U <= Q; t += U) {
                     uint4 w[U * VPL];
+                    uint32_t ub[U];
 #pragma unroll
-                    for (int u = 0; u < U; ++u) { ldu<T, SHUF, AL>(base, p, n, w + u * VPL); next(); }
-                    consume16_u<T, BSWAP, MASKED, false, U * VPL>(w, acc[0], mk);
+                    for (int u = 0; u < U; ++u) {
+                        if constexpr (CUT) ub[u] = cut_bits(rmap, ro * d.RI + (vc * G + gl) * NU, NU);
+                        ldu<T, SHUF, AL>(base, p, n, w + u * VPL);
+                        next();
+                    }
+                    if constexpr (CUT) consume_units_p<T, BSWAP, MASKED, U, VPL>(w, ub, acc[0], mk);
+                    else consume16_u<T, BSWAP, MASKED, false, U * VPL>(w, acc[0], mk);
                 }
                 for (; t < Q; ++t) {
                     uint4 w[VPL];
+                    uint32_t ub = 0;
+                    if constexpr (CUT) ub = cut_bits(rmap, ro * d.RI + (vc * G + gl) * NU, NU);
                     ldu<T, SHUF, AL>(base, p, n, w);
                     next();
-                    consume16_u<T, BSWAP, MASKED, false, VPL>(w, acc[0], mk);
+                    if constexpr (CUT) consume_units_p<T, BSWAP, MASKED, 1, VPL>(w, &ub, acc[0], mk);
+                    else consume16_u<T, BSWAP, MASKED, false, VPL>(w, acc[0], mk);
                 }
-                if constexpr (!MASKED) acc[0].count += (uint32_t)(Q * N * VPL);
+                if constexpr (!MASKED && !CUT) acc[0].count += (uint32_t)(Q * N * VPL);
             }
         }
 #pragma unroll
@@ -1963,9 +2467,13 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
             group_reduce(acc[u], G, cnt, nan);
             const int64_t o = o0 + u * P + pg;
             if (gl == 0 && o < d.KO) {
-                pyas_partial pp;
-                store_group(acc[u], cnt, nan, &pp);
-                put_out<T>(a, ob + o, pp);
+                int64_t oo = o;
+                if constexpr (CUT) oo = cut_out(a, *cb, o);
+                if (oo >= 0) {
+                    pyas_partial pp;
+                    store_group(acc[u], cnt, nan, &pp);
+                    put_out<T>(a, ob + oo, pp);
+                }
             }
         }
     }
@@ -1981,9 +2489,10 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
 constexpr int kRowLdsStride = 17;   // 16-B vectors per LDS run (V <= 16, + 1 pad)
 
 
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int H>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int H, bool CUT = false>
 __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
-                              const MaskT<T> &mk, uint4 *tile) {
+                              const MaskT<T> &mk, uint4 *tile, const CutBox *cb = nullptr,
+                              const uint32_t *rmap = nullptr) {
     const int64_t n = a.r.chunk_elems;
     constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
     // load units per lane per tile (64 * UL * VPL >= the tile's RPW * 16 vectors)
@@ -2031,11 +2540,32 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
         for (int i = 0; i < VH; ++i) {
             T x[N];
             unpack16<T, BSWAP>(row[i], x);
-            acc.template add_n<N, MASKED, false>(x, mk);
+            if constexpr (CUT) {   // the run's elements inside the box (RO == 1: position = element)
+                if (acc.template add_pred<N, MASKED, 1>(x, cut_bits(rmap, (int64_t)(h * VH + i) * N, N), mk)) {
+                    const uint32_t b = cut_bits(rmap, (int64_t)(h * VH + i) * N, N);
+#pragma unroll
+                    for (int q = 0; q < N; ++q)
+                        if ((b >> q) & 1u) acc.template check_nan<1>(&x[q]);
+                }
+            } else {
+                acc.template add_n<N, MASKED, false>(x, mk);
+            }
         }
-        if constexpr (!MASKED) acc.count += (uint32_t)(VH * N);
+        if constexpr (!MASKED && !CUT) acc.count += (uint32_t)(VH * N);
         uint32_t cnt, nan;
         group_reduce(acc, H, cnt, nan);
+        if constexpr (CUT) {   // rows inside the box only, at their place in the cut chunk's array
+            if (h == 0 && o0 + r < d.KO) {
+                const int64_t oo = cut_out(a, *cb, o0 + r);
+                if (oo >= 0) {
+                    pyas_partial pp;
+                    store_group(acc, cnt, nan, &pp);
+                    put_out<T>(a, ob + oo, pp);
+                }
+            }
+            wave_sync_lds();   // the tile's reads before the next tile's writes
+            continue;
+        }
         // the tile's partials go out as consecutive 16-B non-temporal stores,
         // staged in the (now read) tile area, instead of store_group's
         // per-lane 32-B writes that half fill each store instruction's span
@@ -2052,12 +2582,13 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
     }
 }
 
-// Which kernel owns chunk c: the dense one when the chunk is fully selected.
+// Which kernel owns chunk c: the dense one when the chunk is fully selected,
+// or (a.cuts) a box covering at least half of it.
 __device__ __forceinline__ bool dense_owns(const AxesArgs &a, const Sel &s) {
-    return a.d.mode != 0 && chunk_is_full(s, a.r.shape, a.r.ndim);
+    return a.d.mode != 0 && (chunk_is_full(s, a.r.shape, a.r.ndim) || cut_eligible(a, s));
 }
 
-template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE, bool CUTS>
 __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
     const int64_t c = blockIdx.x / a.d.bpc;
     const int64_t j = blockIdx.x - c * a.d.bpc;
@@ -2069,17 +2600,44 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
     MaskT<T> mk;
     mk.init(r.mask);
     const bool al = MODE == 1 ? ldv_aligned<T, SHUF>(base, r.chunk_elems) : ldu_aligned<T, SHUF>(base, r.chunk_elems);
+    // LDS: dense_col's store stage (32 KiB; also the shuffled unit exchange
+    // area, col_units_lds <= 2080 vectors, and the split-fold scratch), or
+    // the LDS row layout's tile; CUTS: the cut chunks' reduced-position map
+    constexpr int H = MODE == 4 ? 1 : MODE == 5 ? 2 : 4;
+    constexpr int kLds = MODE == 1 ? (sizeof(T) >= 4 ? (kBlock * 8 > col_units_lds<T>() ? kBlock * 8 : col_units_lds<T>()) : 1)
+                        : MODE >= 4 ? (kBlock / kWave) * (kWave / H) * kRowLdsStride : 1;
+    __shared__ uint4 lds[kLds];
+    if constexpr (CUTS) {
+        // a cut chunk (a.cuts launches): read as its whole chunk, the box
+        // applied through the reduced-position map and the output remap
+        if (!chunk_is_full(s, r.shape, r.ndim)) {
+            __shared__ uint32_t cmap[kCutMapWords + 1];
+            CutBox cb;
+            PYAS_MARK(1);
+            cut_box(a, s, cb);
+            cut_map(a, cb, a.d.RO * a.d.RI, cmap);
+            PYAS_MARK(2);
+            if constexpr (MODE == 1) {
+                if (al) dense_col<T, SHUF, BSWAP, MASKED, true, true>(a, c, j, base, mk, lds, &cb, cmap);
+                else dense_col<T, SHUF, BSWAP, MASKED, false, true>(a, c, j, base, mk, lds, &cb, cmap);
+            } else if constexpr (MODE >= 4) {
+                if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H, true>(a, c, j, base, mk, lds, &cb, cmap);
+                else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H, true>(a, c, j, base, mk, lds, &cb, cmap);
+            } else {
+                constexpr int UO = MODE == 2 ? 1 : 4;
+                if (al) dense_row<T, SHUF, BSWAP, MASKED, true, UO, true>(a, c, j, base, mk, &cb, cmap);
+                else dense_row<T, SHUF, BSWAP, MASKED, false, UO, true>(a, c, j, base, mk, &cb, cmap);
+            }
+            PYAS_MARK(5);
+            return;
+        }
+    }
     if constexpr (MODE == 1) {
-        // staging for coalesced partial stores (dense_col, N <= 4): 32 KiB
-        // (also the shuffled unit exchange area: col_units_lds <= 2080 vectors)
-        __shared__ uint4 stage[sizeof(T) >= 4 ? (kBlock * 8 > col_units_lds<T>() ? kBlock * 8 : col_units_lds<T>()) : 1];
-        if (al) dense_col<T, SHUF, BSWAP, MASKED, true>(a, c, j, base, mk, stage);
-        else dense_col<T, SHUF, BSWAP, MASKED, false>(a, c, j, base, mk, stage);
+        if (al) dense_col<T, SHUF, BSWAP, MASKED, true>(a, c, j, base, mk, lds);
+        else dense_col<T, SHUF, BSWAP, MASKED, false>(a, c, j, base, mk, lds);
     } else if constexpr (MODE >= 4) {
-        constexpr int H = MODE == 4 ? 1 : MODE == 5 ? 2 : 4;
-        __shared__ uint4 tile[(kBlock / kWave) * (kWave / H) * kRowLdsStride];
-        if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H>(a, c, j, base, mk, tile);
-        else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H>(a, c, j, base, mk, tile);
+        if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H>(a, c, j, base, mk, lds);
+        else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H>(a, c, j, base, mk, lds);
     } else if constexpr (MODE == 2) {
         if (al) dense_row<T, SHUF, BSWAP, MASKED, true, 1>(a, c, j, base, mk);
         else dense_row<T, SHUF, BSWAP, MASKED, false, 1>(a, c, j, base, mk);
@@ -2090,17 +2648,18 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
 }
 
 // One kernel per layout family, so each carries its own occupancy floor.
-template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+// CUTS: the launch also takes the batch's cut chunks (AxesArgs::cuts).
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE, bool CUTS = false>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_COL_WAVES) void k_axes_dense_col(AxesArgs a) {
-    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE>(a);
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, CUTS>(a);
 }
-template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE, bool CUTS = false>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_ROW_WAVES) void k_axes_dense_row(AxesArgs a) {
-    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE>(a);
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, CUTS>(a);
 }
-template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE, bool CUTS = false>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LDS_WAVES) void k_axes_dense_lds(AxesArgs a) {
-    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE>(a);
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, CUTS>(a);
 }
 
 // Whole-chunk box query, column layout, chunk layers folded in the kernel
@@ -4151,6 +4710,15 @@ hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int
 template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
 static void launch_dense_k(const AxesArgs &a, dim3 g, hipStream_t st) {
     const dim3 blk(kBlock);
+    if (a.cuts) {
+        // with cut chunks: the unmasked and full-mask variants only (the
+        // trimmed mask modes evaluate the same rules)
+        constexpr int M = MASKED ? kMaskAll : 0;
+        if constexpr (MODE == 1) hipLaunchKernelGGL((k_axes_dense_col<T, SHUF, BSWAP, M, MODE, true>), g, blk, 0, st, a);
+        else if constexpr (MODE >= 4) hipLaunchKernelGGL((k_axes_dense_lds<T, SHUF, BSWAP, M, MODE, true>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_dense_row<T, SHUF, BSWAP, M, MODE, true>), g, blk, 0, st, a);
+        return;
+    }
     if constexpr (MODE == 1) hipLaunchKernelGGL((k_axes_dense_col<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
     else if constexpr (MODE >= 4) hipLaunchKernelGGL((k_axes_dense_lds<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
     else hipLaunchKernelGGL((k_axes_dense_row<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);

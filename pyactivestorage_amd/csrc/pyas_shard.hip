@@ -11,11 +11,18 @@
 // (one process per GPU); here a non-Python host that holds every device in
 // one process gets it through the C ABI.
 #include <dlfcn.h>
+#include <link.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "pyas.h"
@@ -24,45 +31,83 @@
 namespace {
 
 // RCCL is opened on first use, not linked: a process that never shards does
-// not load it, and a process that already holds an RCCL (torch's, loaded by
-// `import torch`) shares that copy instead of loading a second one.
+// not load it, and a process that already holds an RCCL (torch's
+// torch/lib/librccl.so, loaded by `import torch` as a dependency of a
+// RTLD_LOCAL extension, so its symbols are not in the global scope) shares
+// that copy instead of loading a second one.
 struct Rccl {
     decltype(&ncclCommInitAll) comm_init_all = nullptr;
     decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;
+    decltype(&ncclCommGetAsyncError) async_error = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclAllGather) all_gather = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
 };
 
+// The path of an RCCL already mapped into the process (any file name
+// containing "librccl"), or "" if none.
+std::string loaded_rccl_path() {
+    std::string found;
+    dl_iterate_phdr(
+        [](struct dl_phdr_info *info, size_t, void *data) -> int {
+            const char *n = info->dlpi_name;
+            if (n && std::strstr(n, "librccl")) {
+                *static_cast<std::string *>(data) = n;
+                return 1;
+            }
+            return 0;
+        },
+        &found);
+    return found;
+}
+
+bool bind(void *h, Rccl &r) {
+    r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
+    r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.comm_abort = (decltype(r.comm_abort))dlsym(h, "ncclCommAbort");
+    r.async_error = (decltype(r.async_error))dlsym(h, "ncclCommGetAsyncError");
+    r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+    r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+    r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    return r.comm_init_all && r.comm_destroy && r.comm_abort && r.async_error && r.group_start &&
+           r.group_end && r.all_gather && r.error_string;
+}
+
 int rccl(const Rccl *&out) {
     static std::once_flag once;
     static Rccl r;
     static bool ok = false;
     std::call_once(once, [] {
-        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);   // already loaded?
+        // 1. symbols already in the global scope; 2. an RCCL mapped by
+        // someone else (torch's copy); 3. the system RCCL
+        if (dlsym(RTLD_DEFAULT, "ncclCommInitAll") && bind(RTLD_DEFAULT, r)) { ok = true; return; }
+        const std::string mapped = loaded_rccl_path();
+        void *h = mapped.empty() ? nullptr : dlopen(mapped.c_str(), RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
         if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
         if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-        if (!h) return;
-        r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
-        r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
-        r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
-        r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
-        r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
-        r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
-        ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.all_gather && r.error_string;
+        ok = h && bind(h, r);
     });
     if (!ok) return pyas::set_error(PYAS_ENOTSUP, "RCCL (librccl.so.1) could not be loaded");
     out = &r;
     return PYAS_OK;
 }
 
+// One communicator set per device list.  `mu` serialises its users: RCCL
+// does not allow two group-start..group-end sequences on the same
+// communicators at once, and pyas_shard_release must not destroy them while
+// a call is still using them.
 struct CommSet {
+    std::mutex mu;
     std::vector<ncclComm_t> comms;   // comms[k] drives devices[k]
+    bool dead = false;               // aborted or released: do not use
 };
 
-std::mutex g_mu;
-std::map<std::vector<int>, CommSet> g_comms;   // keyed by the device list, in order
+std::mutex g_mu;   // guards g_comms (the map), never held across RCCL calls
+std::map<std::vector<int>, std::shared_ptr<CommSet>> g_comms;   // keyed by the device list, in order
 
 int nccl_fail(const Rccl *x, ncclResult_t r, const char *what) {
     return pyas::set_error(PYAS_EDEVICE, "%s: %s", what, x->error_string(r));
@@ -70,19 +115,77 @@ int nccl_fail(const Rccl *x, ncclResult_t r, const char *what) {
 
 // Communicators over `devs` (ncclCommInitAll: one rank per listed device,
 // rank k = devs[k]); created once per device list and kept until
-// pyas_shard_release().
-int comms_for(const Rccl *x, const std::vector<int> &devs, std::vector<ncclComm_t> &out) {
+// pyas_shard_release() (or until a timed-out exchange aborts them).
+int comms_for(const Rccl *x, const std::vector<int> &devs, std::shared_ptr<CommSet> &out) {
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_comms.find(devs);
     if (it == g_comms.end()) {
-        CommSet cs;
-        cs.comms.resize(devs.size());
-        ncclResult_t r = x->comm_init_all(cs.comms.data(), (int)devs.size(), devs.data());
+        auto cs = std::make_shared<CommSet>();
+        cs->comms.resize(devs.size());
+        ncclResult_t r = x->comm_init_all(cs->comms.data(), (int)devs.size(), devs.data());
         if (r != ncclSuccess) return nccl_fail(x, r, "ncclCommInitAll");
         it = g_comms.emplace(devs, std::move(cs)).first;
     }
-    out = it->second.comms;
+    out = it->second;
     return PYAS_OK;
+}
+
+// Drop a communicator set from the cache (it was aborted).
+void forget(const std::vector<int> &devs, const std::shared_ptr<CommSet> &cs) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_comms.find(devs);
+    if (it != g_comms.end() && it->second == cs) g_comms.erase(it);
+}
+
+// PYAS_SHARD_TIMEOUT_MS: when set (>= 0), pyas_reduce_sharded waits for the
+// exchange up to that many milliseconds instead of returning at once.
+long shard_timeout_ms() {
+    const char *e = std::getenv("PYAS_SHARD_TIMEOUT_MS");
+    if (!e || !*e) return -1;
+    char *end = nullptr;
+    const long v = std::strtol(e, &end, 10);
+    return (end && *end == 0 && v >= 0) ? v : -1;
+}
+
+// Wait for every stream to drain, watching the communicators for
+// asynchronous errors, until `ms` have passed.  On expiry or error: abort
+// the set (a stalled peer would otherwise hang every later user) and report
+// which devices had not finished.  Caller holds cs.mu.
+int bounded_wait(const Rccl *x, CommSet &cs, const std::vector<int> &devs, void *const *streams, long ms) {
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
+    const size_t n = devs.size();
+    std::vector<char> done(n, 0);
+    for (;;) {
+        size_t ndone = 0;
+        for (size_t k = 0; k < n; ++k) {
+            if (!done[k]) {
+                ncclResult_t ae = ncclSuccess;
+                if (x->async_error(cs.comms[k], &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                    for (ncclComm_t c : cs.comms) x->comm_abort(c);
+                    cs.dead = true;
+                    return pyas::set_error(PYAS_EDEVICE, "RCCL all-gather on device %d failed: %s", devs[k],
+                                           x->error_string(ae));
+                }
+                const hipError_t q = hipStreamQuery((hipStream_t)streams[k]);
+                if (q == hipSuccess) done[k] = 1;
+                else if (q != hipErrorNotReady)
+                    return pyas::set_error(PYAS_EDEVICE, "device %d stream: %s", devs[k], hipGetErrorString(q));
+            }
+            ndone += done[k] ? 1 : 0;
+        }
+        if (ndone == n) return PYAS_OK;
+        if (std::chrono::steady_clock::now() >= t_end) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    std::string late;
+    for (size_t k = 0; k < n; ++k)
+        if (!done[k]) late += (late.empty() ? "" : ",") + std::to_string(devs[k]);
+    for (ncclComm_t c : cs.comms) x->comm_abort(c);
+    cs.dead = true;
+    return pyas::set_error(PYAS_EDEVICE,
+                           "sharded reduce: device(s) %s did not finish within %ld ms; the RCCL "
+                           "communicators were aborted (the next call creates new ones)",
+                           late.c_str(), ms);
 }
 
 }  // namespace
@@ -109,29 +212,44 @@ int pyas_reduce_sharded(pyas_ctx *const *ctx, const pyas_batch *const *per_dev, 
     // 1. each device: its batch -> its total, written where the in-place
     //    all-gather expects rank k's piece (out[k][1 + k])
     for (int k = 0; k < ndev; ++k) {
-        int rc = pyas_reduce_chunks(ctx[k], per_dev[k], mask ? mask[k] : nullptr, nullptr, out[k] + 1 + k,
+        const int rc0 = pyas_reduce_chunks(ctx[k], per_dev[k], mask ? mask[k] : nullptr, nullptr, out[k] + 1 + k,
                                     combine_flags, streams[k]);
-        if (rc) return rc;
+        if (rc0) return rc0;
     }
-    // 2. ONE all-gather of the 32-byte totals over xGMI, in place
+    // 2. ONE all-gather of the 32-byte totals over xGMI, in place; the
+    //    communicator set is held from group start to group end (and through
+    //    the optional bounded wait), so concurrent callers on the same device
+    //    list take turns
     const Rccl *x = nullptr;
     int rc = rccl(x);
     if (rc) return rc;
-    std::vector<ncclComm_t> comms;
-    rc = comms_for(x, devs, comms);
+    std::shared_ptr<CommSet> cs;
+    rc = comms_for(x, devs, cs);
     if (rc) return rc;
-    ncclResult_t r = x->group_start();
-    if (r != ncclSuccess) return nccl_fail(x, r, "ncclGroupStart");
-    for (int k = 0; k < ndev; ++k) {
-        r = x->all_gather(out[k] + 1 + k, out[k] + 1, sizeof(pyas_partial), ncclUint8, comms[k],
-                          (hipStream_t)streams[k]);
-        if (r != ncclSuccess) {
-            x->group_end();
-            return nccl_fail(x, r, "ncclAllGather");
+    {
+        std::lock_guard<std::mutex> lk(cs->mu);
+        if (cs->dead) return pyas::set_error(PYAS_EDEVICE, "the RCCL communicators were released during the call");
+        ncclResult_t r = x->group_start();
+        if (r != ncclSuccess) return nccl_fail(x, r, "ncclGroupStart");
+        for (int k = 0; k < ndev; ++k) {
+            r = x->all_gather(out[k] + 1 + k, out[k] + 1, sizeof(pyas_partial), ncclUint8, cs->comms[k],
+                              (hipStream_t)streams[k]);
+            if (r != ncclSuccess) {
+                x->group_end();
+                return nccl_fail(x, r, "ncclAllGather");
+            }
+        }
+        r = x->group_end();
+        if (r != ncclSuccess) return nccl_fail(x, r, "ncclGroupEnd");
+        const long ms = shard_timeout_ms();
+        if (ms >= 0) {
+            rc = bounded_wait(x, *cs, devs, streams, ms);
+            if (rc) {
+                if (cs->dead) forget(devs, cs);
+                return rc;
+            }
         }
     }
-    r = x->group_end();
-    if (r != ncclSuccess) return nccl_fail(x, r, "ncclGroupEnd");
     // 3. every device folds the totals in device order (the per-chunk sums
     //    were already rounded to the variable dtype under combine_flags)
     for (int k = 0; k < ndev; ++k) {
@@ -142,17 +260,24 @@ int pyas_reduce_sharded(pyas_ctx *const *ctx, const pyas_batch *const *per_dev, 
 }
 
 int pyas_shard_release(void) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (g_comms.empty()) return PYAS_OK;
+    std::map<std::vector<int>, std::shared_ptr<CommSet>> sets;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        sets.swap(g_comms);
+    }
+    if (sets.empty()) return PYAS_OK;
     const Rccl *x = nullptr;
     int rc = rccl(x);
     if (rc) return rc;
-    for (auto &kv : g_comms)
-        for (ncclComm_t c : kv.second.comms) {
+    for (auto &kv : sets) {
+        std::lock_guard<std::mutex> lk(kv.second->mu);   // waits for a call still using the set
+        if (kv.second->dead) continue;
+        kv.second->dead = true;
+        for (ncclComm_t c : kv.second->comms) {
             ncclResult_t r = x->comm_destroy(c);
             if (r != ncclSuccess && rc == PYAS_OK) rc = nccl_fail(x, r, "ncclCommDestroy");
         }
-    g_comms.clear();
+    }
     return rc;
 }
 

@@ -52,3 +52,52 @@ def assert_counts(want_n, got_n, what=""):
     assert type(got_n) is type(want_n), f"{what}: count type {type(got_n)} != {type(want_n)}"
     assert got_n.dtype == want_n.dtype and got_n.shape == want_n.shape, what
     assert np.array_equal(got_n, want_n), f"{what}: counts {got_n} != {want_n}"
+
+
+def oracle_partials(arr, sel, axis, missing):
+    """Per-output (count, sum, min, max) of one chunk straight from the
+    oracle (``oracle.storage_ref.reduce_chunk_bytes``: ``chunk[sel]``, then
+    mask_missing, storage.py:95-100), C order over the kept dims.  Sums in
+    the class accumulator (f64 / i64 / u64); min/max in the native dtype,
+    NaN where an unmasked NaN is present.  For checking a kernel's raw
+    per-output partials against the reference semantics directly."""
+    from oracle import storage_ref as ref
+    dt = arr.dtype
+    nd = dt.newbyteorder("=")
+    if missing is None:
+        missing = (None, None, None, None)
+    vals, _ = ref.reduce_chunk_bytes(arr.tobytes(), None, None, missing, dt.str, arr.shape, "C", sel, axis, None)
+    m = np.ma.getmaskarray(vals)
+    vm = np.ma.MaskedArray(np.ma.getdata(vals).astype(nd), mask=m)
+    acc = np.float64 if dt.kind == "f" else (np.int64 if dt.kind == "i" else np.uint64)
+    out = {"count": (~m).sum(axis=axis, keepdims=True).reshape(-1)}
+    out["sum"] = np.ma.filled(vm.astype(acc), 0).sum(axis=axis, keepdims=True).reshape(-1)
+    with np.errstate(invalid="ignore"):
+        out["min"] = np.ma.getdata(np.ma.min(vm, axis=axis, keepdims=True)).reshape(-1)
+        out["max"] = np.ma.getdata(np.ma.max(vm, axis=axis, keepdims=True)).reshape(-1)
+    return out
+
+
+def assert_partials_match_oracle(parts, want, dt, what, rtol=1e-6):
+    """Kernel partials (engine.partial_dtype rows) vs oracle_partials: count
+    exact, min/max equal where count > 0 (NaN where NumPy gives NaN; the
+    sign of a zero extreme is fixed later by the zero-sign passes, so values
+    compare equal here), sums within rtol (floats) or exact."""
+    nd = dt.newbyteorder("=")
+    np.testing.assert_array_equal(parts["count"], want["count"], err_msg=f"{what}: count")
+    ok = want["count"] > 0
+    for k in ("min", "max"):
+        g = parts[k][ok].astype(nd)
+        w = want[k][ok]
+        if dt.kind == "f":
+            np.testing.assert_array_equal(np.isnan(g), np.isnan(w), err_msg=f"{what}: {k} NaN")
+            fin = ~np.isnan(w)
+            np.testing.assert_array_equal(g[fin], w[fin], err_msg=f"{what}: {k}")
+        else:
+            np.testing.assert_array_equal(g, w, err_msg=f"{what}: {k}")
+    if dt.kind == "f":
+        g, w = parts["sum"][ok].astype(np.float64), want["sum"][ok]
+        fin = np.isfinite(w)
+        np.testing.assert_allclose(g[fin], w[fin], rtol=rtol, atol=1e-3, err_msg=f"{what}: sum")
+    else:
+        np.testing.assert_array_equal(parts["sum"][ok], want["sum"][ok], err_msg=f"{what}: sum")

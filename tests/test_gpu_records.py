@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 
 from pyactivestorage_amd import _lib, engine, selection
-from tests._compare import shuffle_bytes
+from tests._compare import assert_partials_match_oracle, oracle_partials, shuffle_bytes
 
 pytestmark = pytest.mark.gpu
 
@@ -144,6 +144,14 @@ def test_records_equal_converted_partials(gpu, layout, dtype, shuf, sel, monkeyp
     for rec in (_lib.REC_SUM, _lib.REC_MIN, _lib.REC_MAX):
         got = _run(ctx, st, plan, bits, out_offs, n_total, dt, rec)
         _same_records(got, _expected(full, dt, rec), dt, (dtype, shape, axes, env, shuf, sel, rec))
+    # the partials behind the records, straight against the oracle
+    # (VERDICT r4 #7): the first chunk (whole) and the second (cut if hyperslab)
+    for k in (0, 1):
+        sk = tuple(slice(0, m) for m in shape) if sels is None else \
+            tuple(slice(d.start, d.start + d.count) for d in sels[k].dims)
+        assert_partials_match_oracle(full[out_offs[k]:out_offs[k] + n_outs[k]],
+                                     oracle_partials(chunks[k], sk, axes, miss), dt,
+                                     f"{dtype} {shape} axes={axes} {env} shuf={shuf} {sel} chunk {k}")
 
 
 def test_record_argument_errors(gpu):

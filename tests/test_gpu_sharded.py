@@ -116,3 +116,35 @@ def test_several_devices_equal_one(gpu):
         g = r[0]
         assert g["count"] == want["count"] and g["min"] == want["min"] and g["max"] == want["max"]
         assert abs(g["sum"] - want["sum"]) <= 1e-6 * abs(want["sum"])
+
+
+def test_bounded_wait(gpu, monkeypatch):
+    """PYAS_SHARD_TIMEOUT_MS: with a deadline the call waits for the exchange;
+    a zero deadline on a stream still busy with a long reduce aborts the
+    communicators and returns PYAS_EDEVICE naming the device, and the next
+    call builds new communicators and succeeds."""
+    st = gpu.thread_stream()
+    data, offsets = _data(gpu, st)
+    plan = ReductionPlan(gpu, np.float32, CHUNKS, data.ptr, offsets, missing=MISSING, stream=st)
+    plan.launch(st, chunk_partials=False)
+    want = plan.read_total(st)
+    monkeypatch.setenv("PYAS_SHARD_TIMEOUT_MS", "60000")
+    got = _sharded([gpu], [plan], [st])[0]
+    assert got[0].tobytes() == want.tobytes()
+    # ~8 GiB of reads (the 32 chunks 256 times over) keep the stream busy
+    big = ReductionPlan(gpu, np.float32, CHUNKS, data.ptr, np.tile(offsets, 256), missing=MISSING, stream=st)
+    monkeypatch.setenv("PYAS_SHARD_TIMEOUT_MS", "0")
+    n = 1
+    outs = [DeviceBuffer(gpu, (n + 1) * _lib.PARTIAL_NBYTES)]
+    lib = gpu.lib
+    rc = lib.pyas_reduce_sharded(
+        _arr(ctypes.c_void_p, [gpu.handle]), _arr(ctypes.c_void_p, [ctypes.addressof(big.batch)]),
+        _arr(ctypes.c_void_p, [ctypes.addressof(big.mask_up.struct)]), n, 1,
+        _arr(ctypes.c_void_p, [o.ptr for o in outs]), _arr(ctypes.c_void_p, [st]))
+    gpu.synchronize(st)
+    assert rc == _lib.EDEVICE, rc
+    msg = lib.pyas_last_error()
+    assert b"did not finish" in msg and b"device(s) %d" % gpu.device in msg, msg
+    monkeypatch.delenv("PYAS_SHARD_TIMEOUT_MS")
+    got = _sharded([gpu], [plan], [st])[0]
+    assert got[0].tobytes() == want.tobytes()

@@ -1,0 +1,9 @@
+# round 5: rocprofv3 kernel splits of single C3 query shapes
+O=gpurun_out/r05/qprof
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+for q in "c3_slab 0" "c3_slab 4" "c3_slab 5" "c3_stride 2" "c3_stride 1"; do
+  set -- $q
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/$O/${1}_$2 -o run -- python3 $R/tools/query_c3.py $1 $2 --reps 10 > $R/$O/${1}_$2.json 2> $R/$O/${1}_$2.err || exit 1
+done

@@ -1,0 +1,62 @@
+"""One Active query shape over the C3 variable attached resident (as
+bench.py's c3_slab / c3_stride extras), repeated: for rocprofv3 kernel
+splits of a single query shape.
+
+    python tools/query_c3.py NAME LABEL_INDEX [--reps 10]
+    e.g. python tools/query_c3.py c3_slab 4     (the 5th query of c3_slab)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("name")
+    ap.add_argument("which", type=int)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    import torch
+    from pyactivestorage_amd.active import Active, attach_resident, release_resident
+    from pyactivestorage_amd.synthetic import chunk_major_device
+    from pyactivestorage_amd.variable import ChunkedVariable
+    cfg = bench.CONFIGS["c3"]
+    dt = np.dtype(cfg["dtype"])
+    shape, chunks = cfg["shape"], cfg["chunks"]
+    dev = torch.device("cuda", 0)
+    data, offsets, _ = chunk_major_device(torch, shape, chunks, dt, dev, fill=bench.FILL, fill_frac=0.01, seed=0)
+    torch.cuda.synchronize()
+    grid = [s // c for s, c in zip(shape, chunks)]
+    cb = int(np.prod(chunks)) * dt.itemsize
+    index = {co: (int(offsets[k]), cb) for k, co in enumerate(np.ndindex(*grid))}
+    attrs = {"_FillValue": np.array([bench.FILL], dtype=dt), "valid_min": np.array([bench.VMIN], dtype=dt),
+             "valid_max": np.array([bench.VMAX], dtype=dt)}
+    var = ChunkedVariable(name="q", shape=shape, chunks=chunks, dtype=dt, chunk_index=index, attrs=attrs,
+                          filename=None, filter_pipeline=None)
+    attach_resident(var, data.data_ptr(), device=0, owner=data)
+    label, mk, axis, method = bench.ACTIVE_EXTRAS[a.name][a.which]
+    ix = mk()
+    act = Active(var, resident=True)
+    times = []
+    for _ in range(a.reps + 2):
+        getattr(act, method)(axis=axis)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        act[ix]
+        times.append(time.perf_counter() - t0)
+    times = times[2:]
+    print(json.dumps({"query": label, "axis": axis, "method": method,
+                      "ms_median": round(float(np.median(times)) * 1e3, 4),
+                      "ms_min": round(min(times) * 1e3, 4)}), flush=True)
+    release_resident(var)
+
+
+if __name__ == "__main__":
+    main()
