@@ -659,6 +659,12 @@ ACTIVE_EXTRAS = {
         ("[1:1023]^3", lambda: (slice(1, 1023),) * 3, (0,), "min"),
         ("[1:1023]^3", lambda: (slice(1, 1023),) * 3, (2,), "min"),
     ],
+    # the whole variable (zero-sign cost studies: tools/query_c3.py --zeros)
+    "c3_whole": [
+        ("[:]^3", lambda: (slice(None),) * 3, None, "min"),
+        ("[:]^3", lambda: (slice(None),) * 3, (0,), "min"),
+        ("[:]^3", lambda: (slice(None),) * 3, (2,), "min"),
+    ],
     "c3_stride": [
         ("[:, 0:1024:3, :]", lambda: (slice(None), slice(0, 1024, 3), slice(None)), None, "mean"),
         ("[:, :, 0:1024:4]", lambda: (slice(None), slice(None), slice(0, 1024, 4)), None, "mean"),

@@ -298,6 +298,15 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch,
 #define PYAS_REC_BYTES(itemsize) ((itemsize) <= 4 ? 8 : 16)
 #define PYAS_COMBINE_REC(rec) ((uint32_t)(rec) << 4)
 #define PYAS_TIE_REC 4u    /* which: parts are PYAS_REC_MIN (which 1) / _MAX (which 2) records */
+/* OR'ed into pyas_reduce_axes_ex's rec (PYAS_REC_MIN / PYAS_REC_MAX of a
+ * float variable): the per-chunk walk writes NumPy's sign of a zero min/max
+ * itself (storage.py:99-100; valid when the innermost chunk dim is kept: the
+ * calls are elementwise and the last zero wins), so pyas_tie_chunks need
+ * not run.  The caller promises every chunk is whole or a unit-step box
+ * covering at least half the chunk with more than one index in the
+ * innermost dim; PYAS_ENOTSUP when the launch cannot key the sign (another
+ * layout, no tie rule, cut chunks it would not take). */
+#define PYAS_REC_ZERO_SIGN 0x100
 /* pyas_reduce_axes writing `rec` records (PYAS_REC_*; PYAS_REC_FULL is
  * pyas_reduce_axes itself): out[out_offsets[c] + o] in record units.  A
  * chunk's outputs must count < 2^31 elements each. */
@@ -438,7 +447,12 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
  *    position in the `out` array's call (MIN or MAX, not both).
  * Float dtypes; PYAS_ENOTSUP (nothing launched) when the geometry takes
  * another fold kernel, a reduction the kernel cannot key, or no rule is set:
- * fold without the flag and run the zero-sign passes then. */
+ * fold without the flag and run the zero-sign passes then.
+ * pyas_combine_grid takes the same flags over records that already carry
+ * level 1's signs (pyas_reduce_axes_ex with PYAS_REC_ZERO_SIGN): where the
+ * `out` array's calls are elementwise (its innermost non-1 dim kept) each
+ * output takes the sign of its last layer whose min (max) is a zero, so
+ * pyas_tie_grid is not needed; PYAS_ENOTSUP (nothing launched) otherwise. */
 #define PYAS_FOLD_ZERO_SIGN_MIN 0x100u
 #define PYAS_FOLD_ZERO_SIGN_MAX 0x200u
 

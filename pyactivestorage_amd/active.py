@@ -64,14 +64,20 @@ _MISS = object()
 
 
 def _index_key(index):
-    """Hashable form of an index made only of slices and Ellipsis (the box
-    queries a plan can be replayed for); None otherwise."""
+    """Hashable form of an index made of slices, Ellipsis and 1-D integer
+    index lists (the box queries a plan can be replayed for); None
+    otherwise."""
     if not isinstance(index, tuple):
         index = (index,)
     out = []
     for x in index:
         if x is Ellipsis:
             out.append(("e",))
+        elif isinstance(x, (list, np.ndarray)):
+            a = np.asarray(x)
+            if a.ndim != 1 or a.dtype.kind not in "iu":
+                return None
+            out.append(("l",) + tuple(int(v) for v in a))
         elif isinstance(x, slice):
             part = ["s"]
             for v in (x.start, x.stop, x.step):
@@ -128,9 +134,10 @@ class _CachedQuery:
             g["tie"]["fused"] = act._fold(ctx, st, self.plan, g["g"], g["fin"].ptr, g["zs_ok"])
         else:   # records of this replay's method (one size per dtype: the buffer fits every method)
             g["rec"] = engine.method_rec(act._method)
-            engine.reduce_axes(ctx, self.plan.batch, self.plan.mask_up.struct, g["axes_mask"], g["obuf"].ptr,
-                               g["parts"].ptr, st, rec=g["rec"])
-            engine.combine_grid(ctx, act.ds.dtype, g["parts"].ptr, g["g"], g["fin"].ptr, True, st, rec=g["rec"])
+            g["zs1"] = act._reduce_axes_zs(ctx, st, self.plan, g["axes_mask"], g["obuf"].ptr, g["parts"].ptr,
+                                           g["rec"], g.get("zs_ok1", False))
+            g["zs2"] = act._combine_zs(ctx, st, g["parts"].ptr, g["g"], g["fin"].ptr, g["rec"],
+                                       g["zs1"] and g["tie"]["lr"] == 1)
         act._tie_grid(ctx, st, self.plan, g)
         return act._format_device(ctx, st, g["fin"], g["n_final"], shape, bufs=self.fmt)
 
@@ -754,6 +761,21 @@ class Active:
                 keys.append(host)
         return plan.read_total(st)
 
+    def _reduce_axes_zs(self, ctx, st, plan, axes_mask, obuf_ptr, parts_ptr, prec, zs_ok1) -> bool:
+        """pyas_reduce_axes_ex into records; with PYAS_REC_ZERO_SIGN when
+        the query is a min/max whose level-1 zero sign the walk can key
+        (``zs_ok1``).  Returns whether it did (then pyas_tie_chunks is not
+        needed)."""
+        if zs_ok1 and self._tie_which() and prec in (_lib.REC_MIN, _lib.REC_MAX):
+            try:
+                engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf_ptr, parts_ptr, st,
+                                   rec=prec | _lib.REC_ZERO_SIGN)
+                return True
+            except NotImplementedError:
+                pass   # another layout: the scan pass keys the sign
+        engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf_ptr, parts_ptr, st, rec=prec)
+        return False
+
     def _tie_grid(self, ctx, st, plan, rec, keys_ptr=None):
         """NumPy's sign of the zero min/max outputs of a partial-axis box
         query (``rec``: _grid_partials' record): per chunk output
@@ -775,6 +797,11 @@ class Active:
             engine.tie_grid(ctx, dt, rec["g"], None, t["flags"].ptr, t["lr"], which, rec["fin"].ptr, keys_ptr, st)
         else:   # per-chunk partials: compact records of the method (pyas_reduce_axes_ex)
             pw = which | (_lib.TIE_REC if rec.get("rec") else 0)
+            if rec.get("zs2") and keys_ptr is None:   # walk and combine keyed both levels
+                return
+            if rec.get("zs1"):   # the walk keyed level 1 itself: only the `out` level
+                engine.tie_grid(ctx, dt, rec["g"], rec["parts"].ptr, None, t["lr"], pw, rec["fin"].ptr, keys_ptr, st)
+                return
             try:
                 engine.tie_chunks(ctx, plan.batch, plan.mask_up.struct, geom, rec["axes_mask"], pw,
                                   rec["obuf"].ptr, rec["parts"].ptr, st)
@@ -905,14 +932,23 @@ class Active:
             if neutral:   # zero records: count 0, neutral in the combine
                 zeros = np.zeros(neutral * rb, dtype=np.uint8)
                 ctx.h2d(parts.ptr + n_parts * rb, zeros, st)
-            engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf.ptr, parts.ptr, st, rec=prec)
-            engine.combine_grid(ctx, dt, parts.ptr, g, fin.ptr, True, st, rec=prec)
+            # level 1 of NumPy's zero sign keyed by the per-chunk walk itself
+            # where it can (PYAS_REC_ZERO_SIGN), else pyas_tie_chunks below
+            zs_ok1 = zs_ok and plan.dense_boxes()
         ext = [tables["n_coords"][d] if d in axes else final_shape[d] for d in range(ds.ndim)]
+        lr = zerosign.grid_lr(ext, set(axes))
+        zs2 = False
+        if not folded:
+            zs1 = self._reduce_axes_zs(ctx, st, plan, axes_mask, obuf.ptr, parts.ptr, prec, zs_ok1)
+            # level 2 in the combine where the `out` calls are elementwise
+            # (group queries key it across ranks: pyas_tie_grid below)
+            zs2 = self._combine_zs(ctx, st, parts.ptr, g, fin.ptr, prec, zs1 and lr == 1 and keys is None)
         r = rec if rec is not None else {}
+        if folded:
+            zs_ok1 = zs1 = False
         r.update(folded=folded, g=g, fin=fin, obuf=obuf, abuf=abuf, tbuf=tbuf, parts=parts, rec=prec,
-                 axes_mask=axes_mask, n_final=n_final, zs_ok=zs_ok,
-                 tie={"lr": zerosign.grid_lr(ext, set(axes)), "n_parts": n_parts_all, "flags": None,
-                      "fused": fused})
+                 axes_mask=axes_mask, n_final=n_final, zs_ok=zs_ok, zs_ok1=zs_ok1, zs1=zs1, zs2=zs2,
+                 tie={"lr": lr, "n_parts": n_parts_all, "flags": None, "fused": fused})
         if keys is not None and self._tie_which():
             kbuf = DeviceBuffer(ctx, max(n_final, 1) * 16)
             engine.tie_keys_reset(ctx, kbuf.ptr, n_final, st)
@@ -929,6 +965,21 @@ class Active:
         ctx.d2h(final, fin.ptr, st)
         ctx.synchronize(st)
         return final
+
+    def _combine_zs(self, ctx, st, parts_ptr, g, fin_ptr, prec, keyed) -> bool:
+        """pyas_combine_grid of the per-chunk records; ``keyed`` (level 1
+        keyed by the walk, the `out` calls elementwise): level 2 of NumPy's
+        zero sign keyed in the same launch.  Returns whether it was."""
+        dt = self.ds.dtype
+        which = self._tie_which() if keyed else 0
+        if which:
+            try:
+                engine.combine_grid(ctx, dt, parts_ptr, g, fin_ptr, True, st, rec=prec, zero_sign=which)
+                return True
+            except NotImplementedError:
+                pass
+        engine.combine_grid(ctx, dt, parts_ptr, g, fin_ptr, True, st, rec=prec)
+        return False
 
     def _fold_sign_ok(self, axes) -> bool:
         """Whether the fold may fuse NumPy's zero sign of this partial-axis

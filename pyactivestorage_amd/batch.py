@@ -54,6 +54,7 @@ class ReductionPlan:
         self.offsets_buf = self._upload(offsets, st)
         sel_ptr = pool_ptr = None
         table = None
+        self.sel_table_host = None   # the uploaded selection table (host copy), None: every chunk whole
         sel_shape, kept = self.chunk_shape, tuple(range(len(self.chunk_shape)))
         self._sel0 = None        # a chunk's selection, for tie_geom
         if selections is not None:
@@ -67,6 +68,7 @@ class ReductionPlan:
                 # kernels' lean/dense paths)
                 sel_ptr = self._upload(table, st).ptr
                 pool_ptr = self._upload(pool, st).ptr
+                self.sel_table_host = table
             shapes = {s.shape for s in selections}
             if (self.cm.tables[0] is not None or self.cm.tables[1] is not None) and len(shapes) > 1:
                 raise NotImplementedError("vector fill/missing values need equal selection shapes")
@@ -84,6 +86,7 @@ class ReductionPlan:
             sel_ptr = self._upload(table, st).ptr
             pool_ptr = self._upload(index_pool if index_pool is not None
                                     else np.zeros(1, dtype=np.int32), st).ptr
+            self.sel_table_host = table
             if self.n_chunks:
                 self._sel0 = _row_sel(table[0], self.chunk_shape, index_pool)
         self.layout = engine.Layout(self.dtype, self.chunk_shape,
@@ -93,6 +96,22 @@ class ReductionPlan:
         self.mask_up = engine.MaskUpload(ctx, self.cm, sel_shape, kept, st)
         self.chunk_partials = DeviceBuffer(ctx, max(self.n_chunks, 1) * _lib.PARTIAL_NBYTES)
         self.total = DeviceBuffer(ctx, _lib.PARTIAL_NBYTES)
+
+    def dense_boxes(self) -> bool:
+        """Whether every chunk is whole or a unit-step box covering at least
+        half of it with more than one index in its innermost dim: the chunks
+        the dense per-chunk kernels walk themselves (pyas_kernels.hpp
+        cut_eligible), the promise PYAS_REC_ZERO_SIGN needs."""
+        t = self.sel_table_host
+        nd = len(self.chunk_shape)
+        if self.chunk_shape[-1] < 2:
+            return False
+        if t is None:
+            return True
+        step, cnt = t[:, :nd, 1], t[:, :nd, 2].astype(np.int64)
+        ok = ((step == 1) | (cnt == 1)).all(axis=1) & (cnt >= 1).all(axis=1) & (cnt[:, nd - 1] > 1)
+        ok &= 2 * cnt.prod(axis=1) >= int(np.prod(self.chunk_shape))
+        return bool(ok.all())
 
     def tie_geom(self, order="C") -> _lib.TieGeom:
         """How NumPy walks these chunks' ``chunk[sel]`` after mask_missing

@@ -177,10 +177,11 @@ int prepare(const pyas_ctx *ctx, const pyas_batch *b, const pyas_mask *m, pyas::
     a.pool = b->index_pool;
     a.ndim = b->ndim;
     a.chunk_elems = elems;
-    {   // PYAS_SPANS (per call: tests and benches switch it): 0 off, 2 also the
-        // aligned runs run_rows streams, unset / 1 the default
+    {   // PYAS_SPANS (per call: tests and benches switch it): 0 off, 1 not on
+        // the aligned runs run_rows streams, unset / 2 every cut chunk a span
+        // plan fits (C3 [4:1020]^3 0.726 -> 0.708 ms; C5 level)
         const char *e = getenv("PYAS_SPANS");
-        a.spans = e && *e ? atoi(e) : 1;
+        a.spans = e && *e ? atoi(e) : 2;
     }
     int64_t stride = 1;
     for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
@@ -948,6 +949,8 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
                         uint32_t axes_mask, int32_t rec, const int64_t *out_offsets, void *out,
                         void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    const bool want_zs = (rec & PYAS_REC_ZERO_SIGN) != 0;
+    rec &= ~PYAS_REC_ZERO_SIGN;
     if (rec < PYAS_REC_FULL || rec > PYAS_REC_MAX) return fail(PYAS_EINVAL, "unknown record form %d", rec);
     pyas::AxesArgs x;
     std::memset(&x, 0, sizeof(x));
@@ -1019,6 +1022,38 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
                  x.d.RO * x.d.RI <= 32 * (int64_t)pyas::kCutMapWords &&
                  x.r.chunk_elems < (int64_t(1) << 31);   // 32-bit index arithmetic
     }
+    // PYAS_REC_ZERO_SIGN: the column walk keys NumPy's sign of a zero
+    // min/max itself (the level-1 calls are elementwise: the innermost dim
+    // kept, so the last zero in row order wins), instead of pyas_tie_chunks
+    // scanning the chunks again.  Every chunk must then be walked by the
+    // dense kernel: whole, or a cut box it takes (the caller's promise).
+    if (want_zs) {
+        if (rec != PYAS_REC_MIN && rec != PYAS_REC_MAX)
+            return fail(PYAS_EINVAL, "PYAS_REC_ZERO_SIGN needs PYAS_REC_MIN or PYAS_REC_MAX");
+        if (batch->dtype != PYAS_F32 && batch->dtype != PYAS_F64)
+            return fail(PYAS_ENOTSUP, "zero sign: float dtypes only");
+        if (batch->sel && !x.cuts) return fail(PYAS_ENOTSUP, "zero sign in the per-chunk walk: cut chunks not taken");
+        const pyas::TieRule *t = tie_of(ctx, batch->dtype);
+        if (!t) return fail(PYAS_ENOTSUP, "zero sign: no tie rule set for this dtype");
+        if (x.d.mode == 1) {
+            if ((axes_mask >> (batch->ndim - 1)) & 1u)
+                return fail(PYAS_ENOTSUP, "zero sign in the column walk: innermost dim reduced");
+        } else if (x.d.mode >= 4) {
+            // LDS row layout: each output row is one contiguous NumPy call (of
+            // the box's run along the innermost dim for a cut chunk, so the
+            // reduced group must be that dim alone), keyed with the rule
+            if (batch->sel && x.d.RI != batch->chunk_shape[batch->ndim - 1])
+                return fail(PYAS_ENOTSUP, "zero sign in the row walk: a cut chunk's reduced group spans dims");
+            if (x.d.RI > 64 || x.d.RI - 1 >= t->piece)
+                return fail(PYAS_ENOTSUP, "zero sign in the row walk: rows over 64 elements or NumPy's buffer");
+            if (t->lanes < 1 || t->lanes > 64 || (t->lanes & (t->lanes - 1)))
+                return fail(PYAS_ENOTSUP, "zero sign in the row walk: a lane count that is not a power of two");
+            x.t = *t;
+        } else {
+            return fail(PYAS_ENOTSUP, "zero sign in the per-chunk walk: column or LDS row layouts only");
+        }
+        x.zs = rec == PYAS_REC_MIN ? 1 : 2;
+    }
     // Streamed column layout (k_axes_col_stream): every chunk whole, one
     // lane per item column (split 1), rows in whole 4-row groups; each
     // workgroup walks cpb chunks as one ring of loads.  Measured on C3
@@ -1035,7 +1070,7 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
     // PYAS_COL_STREAM: 0 off, N > 0 forces N chunks per workgroup wherever
     // the kernel can run (tests), unset auto.
     const int64_t col_items = x.d.mode == 1 ? x.d.KO * (x.d.KI / (16 / es)) : 0;
-    if (x.d.mode == 1 && !batch->sel && es >= 4 && x.d.split == 1 && x.d.it == pyas::kBlock &&
+    if (x.d.mode == 1 && !batch->sel && !x.zs && es >= 4 && x.d.split == 1 && x.d.it == pyas::kBlock &&
         (x.d.RO * x.d.RI) % 4 == 0) {
         const char *e = getenv("PYAS_COL_STREAM");   // per call: tests and benches switch it
         const int64_t forced = e ? atoll(e) : -1;
@@ -1067,7 +1102,7 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
     // Split 1 only (one lane set walks all rows): the same 4-row groups in the
     // same order as dense_col / k_axes_col_stream / k_axes_fold_lean, so the
     // partials stay bit-identical to theirs.
-    if (x.d.mode == 1 && shuf && !batch->sel && es >= 2 && x.d.RO == 1 && (x.d.KI == 64 || x.d.KI == 128) &&
+    if (x.d.mode == 1 && shuf && !batch->sel && !x.zs && es >= 2 && x.d.RO == 1 && (x.d.KI == 64 || x.d.KI == 128) &&
         x.d.split == 1 && !x.r.tab.on[0] && !x.r.tab.on[1]) {
         const char *e = getenv("PYAS_SHUF_SLAB");   // per call: tests and benches switch it
         int64_t rb = pyas::kSlabBytes / (x.d.KI * es);
@@ -1092,7 +1127,12 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
         PYAS_HIP(pyas::launch_axes_dense(batch->dtype, x, masked, g, (hipStream_t)stream));
     }
     if (!x.d.mode || batch->sel) {
-        const int64_t grid = batch->n_chunks * bpc;
+        // with cut chunks in the dense launch, the generic kernel keeps only
+        // boxes under half a chunk and non-box selections: one workgroup per
+        // chunk (most of its workgroups only find their chunk taken; at 8 per
+        // chunk that empty launch cost C3 [1:1023]^3 (2,) 74 us)
+        if (x.cuts) x.bpc = 1;
+        const int64_t grid = batch->n_chunks * x.bpc;
         if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
         PYAS_HIP(pyas::launch_reduce_axes(batch->dtype, x, grid, (hipStream_t)stream));
     }
@@ -1352,8 +1392,29 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, cons
         return fail(PYAS_EINVAL, "grid rank %d outside 1..%d", g->ndim, PYAS_MAX_DIMS);
     if (g->axes_mask >> g->ndim) return fail(PYAS_EINVAL, "axes mask 0x%x beyond rank %d", g->axes_mask, g->ndim);
     // PYAS_COMBINE_REC: `in` holds compact records (pyas_reduce_axes_ex)
-    if (combine_flags & ~(PYAS_COMBINE_ROUND_TO_VAR | PYAS_COMBINE_REC(3)))
+    if (combine_flags & ~(PYAS_COMBINE_ROUND_TO_VAR | PYAS_COMBINE_REC(3) | PYAS_FOLD_ZERO_SIGN_MIN |
+                          PYAS_FOLD_ZERO_SIGN_MAX))
         return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
+    // PYAS_FOLD_ZERO_SIGN_*: `in` carries level 1's signs (PYAS_REC_ZERO_SIGN);
+    // the combine keys level 2 itself when the `out` array's calls are
+    // elementwise (its trailing non-1 dims kept): the last zero layer wins
+    if (combine_flags & (PYAS_FOLD_ZERO_SIGN_MIN | PYAS_FOLD_ZERO_SIGN_MAX)) {
+        if ((combine_flags & (PYAS_FOLD_ZERO_SIGN_MIN | PYAS_FOLD_ZERO_SIGN_MAX)) ==
+            (PYAS_FOLD_ZERO_SIGN_MIN | PYAS_FOLD_ZERO_SIGN_MAX))
+            return fail(PYAS_EINVAL, "zero sign: min or max, not both");
+        if (dtype != PYAS_F32 && dtype != PYAS_F64) return fail(PYAS_ENOTSUP, "zero sign: float dtypes only");
+        if (!tie_of(ctx, dtype)) return fail(PYAS_ENOTSUP, "zero sign: no tie rule set for this dtype");
+        int64_t lr2 = 1;
+        for (int d = g->ndim - 1; d >= 0; --d) {
+            const bool red = (g->axes_mask >> d) & 1u;
+            const int64_t ext = red ? g->n_coords[d] : g->out_extent[d];
+            if (ext == 1) continue;
+            if (!red) break;
+            lr2 *= ext;
+        }
+        if (lr2 != 1) return fail(PYAS_ENOTSUP, "zero sign in the combine: the out calls are not elementwise");
+        combine_flags |= pyas::kCombineThreadOnly;   // the per-thread form keys it
+    }
     int64_t n_out = 1, n_layers = 1;
     for (int d = 0; d < g->ndim; ++d) {
         if (g->n_coords[d] < 1) return fail(PYAS_EINVAL, "n_coords[%d] = %lld", d, (long long)g->n_coords[d]);

@@ -1,5 +1,5 @@
 // pyas_inst.hip — instantiates the kernel launchers for ONE dtype, chosen by
-// -DPYAS_INST_<name>, part -DPYAS_PART=1|2|3 (the Makefile builds this file
+// -DPYAS_INST_<name>, part -DPYAS_PART=1..5 (the Makefile builds this file
 // once per dtype and part).
 #include "pyas_kernels.hpp"
 
@@ -34,7 +34,11 @@ PYAS_INSTANTIATE_PART1(PYAS_T)
 PYAS_INSTANTIATE_PART2(PYAS_T)
 #elif PYAS_PART == 3
 PYAS_INSTANTIATE_PART3(PYAS_T)
+#elif PYAS_PART == 4
+PYAS_INSTANTIATE_PART4(PYAS_T)
+#elif PYAS_PART == 5
+PYAS_INSTANTIATE_PART5(PYAS_T)
 #else
-#error "define PYAS_PART=1|2|3"
+#error "define PYAS_PART=1|2|3|4|5"
 #endif
 }  // namespace pyas

@@ -64,6 +64,11 @@ struct AxesDense {
     int64_t rb;                       // k_axes_shuf_slab: rows per LDS tile (0: off)
 };
 
+// NumPy's sign of a zero min/max (pyas_tie_*); float types only
+struct TieRule {
+    int32_t lanes, piece, acc;        // lanes 0: no rule set
+    uint8_t rank[64], acc_rank[64];
+};
 struct AxesArgs {
     ReduceArgs r;
     AxesDense d;
@@ -78,6 +83,8 @@ struct AxesArgs {
     bool vec;                         // geometry admits 16-B vector walks (kernel re-checks per chunk)
     int32_t rec;                      // per-chunk outputs: 0 pyas_partial, else a PYAS_REC_* record
     bool cuts;                        // dense launch also takes cut chunks (box, >= half the chunk)
+    int32_t zs;                       // the walk keys NumPy's sign of a zero min (1) / max (2)
+    TieRule t;                        // zs in the LDS row layout: the host's rule (rows are calls)
 };
 
 // pyas_reduce_axes_grid: the chunk layers of a whole-chunk box query folded
@@ -135,15 +142,15 @@ hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int
 template <typename T>
 hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
 template <typename T>
+hipError_t launch_axes_dense_rows_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);
+template <typename T>
 hipError_t launch_axes_fold_t(const AxesArgs &a, const FoldGrid &g, bool masked, int64_t grid,
                               hipStream_t st);
 template <typename T>
+hipError_t launch_axes_fold_rows_t(const AxesArgs &a, const FoldGrid &g, bool masked, int64_t grid,
+                                   hipStream_t st);
+template <typename T>
 hipError_t launch_select_t(const SelectArgs &a, int64_t grid, hipStream_t st);
-// NumPy's sign of a zero min/max (pyas_tie_*); float types only
-struct TieRule {
-    int32_t lanes, piece, acc;        // lanes 0: no rule set
-    uint8_t rank[64], acc_rank[64];
-};
 struct TieCall {
     int32_t acc;                      // 1: strided reduce loop (accumulator keys)
     uint32_t block;                   // acc: kept dims of NumPy's copied first buffer fill

@@ -689,7 +689,10 @@ __device__ __forceinline__ bool span_plan(const ReduceArgs &a, const uint8_t *ba
     if (sk < 0) { st_k += (cn_k - 1) * sk; sk = -sk; }   // same elements, ascending
     // three span forms (written as selects: a branch-per-form version of this
     // lost the `ext` of the last form at -O1 and above, ROCm 7.2 hipcc)
-    const bool run = sk == 1;                             // a run of whole inner rows
+    // a run of whole inner rows -- unless it would exceed one block pass
+    // (> 4 KiB): then dim k is enumerated too and a span is one inner block
+    // (C3 [:, 1:64, :]: 63 spans of 256 B, not one of 15.75 KiB)
+    const bool run = sk == 1 && (cn_k * cs_k + NU - 1) / NU + 1 <= kBlock;
     const bool strided = !run && sk > 1 && k == a.ndim - 1;   // strided innermost dim
     // otherwise: a list, or strided with inner rows -> dim k enumerated too
     sp.kk = (run || strided) ? k : k + 1;
@@ -707,6 +710,8 @@ __device__ __forceinline__ bool span_plan(const ReduceArgs &a, const uint8_t *ba
             nsp *= s.cnt[d];
             if (s.cnt[d] > 0) m0 += sel_index(s, a.pool, d, 0) * a.cstride[d];
             if (s.cnt[d] > 1) {
+                // SpanWalk: an index list only as the last span dim
+                if (s.step[d] == 0 && d < sp.kk - 1) return false;
                 const int64_t delta = (s.step[d] != 0 ? (int64_t)s.step[d] : 1) * a.cstride[d];
                 if (SH ? (delta & 15) != 0 : ((delta * ES) & 15) != 0) return false;
             }
@@ -721,10 +726,72 @@ __device__ __forceinline__ bool span_plan(const ReduceArgs &a, const uint8_t *ba
     return true;
 }
 
-// Spans [q0, q1) of the chunk at `base` (plan sp).  Lane tid reads group
-// j = tid % G of spans tid / G + P*i; U groups per lane in flight.  Counts:
-// masked tiles count through ballots, unmasked ones are counted by the caller
-// ((q1 - q0) * per_span).
+// The spans of one lane group, walked in order, for span dims that are all
+// slices (any step): the digits of the current span and its first group's
+// element offset.  The next span adds the last span dim's memory step; only
+// a carry out of that dim (every cnt[kk-1] spans) walks the outer digits.
+// (A block-strided walk advanced every digit with a carry chain per item:
+// ~40 VALU ops per 16-B group, C3 [1:1023]^3's cut chunks at 39 % of 8 TB/s.)
+struct SpanWalk {
+    int32_t ix[PYAS_MAX_DIMS];   // digits of the dims < last
+    int32_t xl;                  // digit of the last span dim
+    int32_t mem;                 // element offset of this lane's group in the current span
+    __device__ __forceinline__ void init(const ReduceArgs &a, const Sel &s, int kk, int64_t q, int32_t gofs) {
+        uint32_t r = (uint32_t)q;
+        int32_t m = gofs;
+        xl = 0;
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            ix[d] = 0;
+            if (d < kk) {
+                const uint32_t c = (uint32_t)s.cnt[d], qq = r / c;
+                const int32_t dig = (int32_t)(r - qq * c);
+                r = qq;
+                m += (int32_t)sel_index(s, a.pool, d, dig) * (int32_t)a.cstride[d];
+                if (d == kk - 1) xl = dig;
+                else ix[d] = dig;
+            }
+        }
+        mem = m;
+    }
+    // one more span along the last span dim; an index list there costs a
+    // pool read per span
+    __device__ __forceinline__ void next(const ReduceArgs &a, const Sel &s, int kk) {
+        int32_t cl = 1, st = 0, sk = 0, cs = 0;
+#pragma unroll
+        for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+            if (d == kk - 1) { cl = s.cnt[d]; st = s.start[d]; sk = s.step[d]; cs = (int32_t)a.cstride[d]; }
+        const int32_t x0 = xl;
+        if (__builtin_expect(++xl < cl, 1)) {
+            mem += sk != 0 ? sk * cs : (a.pool[st + xl] - a.pool[st + x0]) * cs;
+            return;
+        }
+        // carry into the outer span dims (rare; slices or single indices,
+        // span_plan's rule: affine in the digits)
+        xl = 0;
+        mem -= sk != 0 ? x0 * sk * cs : (a.pool[st + x0] - a.pool[st]) * cs;
+        bool carry = true;
+#pragma unroll
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            if (carry && d < kk - 1) {
+                const int32_t dd = s.step[d] * (int32_t)a.cstride[d];
+                mem += dd;
+                if (++ix[d] >= s.cnt[d]) {
+                    ix[d] = 0;
+                    mem -= s.cnt[d] * dd;
+                } else {
+                    carry = false;
+                }
+            }
+        }
+    }
+};
+
+// Spans [q0, q1) of the chunk at `base` (plan sp).  Lane group p (P of
+// them, G lanes each) walks the spans [q0 + p*M, q0 + (p+1)*M) in order, lane
+// j of a group reading group j of each span; U groups per lane in flight.
+// Counts: masked tiles count through ballots, unmasked ones are counted by
+// the caller ((q1 - q0) * per_span).
 template <typename T, bool SHUF, bool BSWAP, int MASKED>
 __device__ void run_spans(const ReduceArgs &a, const uint8_t *base, const Sel &s, const SpanPlan &sp,
                           int64_t q0, int64_t q1, TileAcc<T> &acc, const MaskT<T> &mk) {
@@ -743,37 +810,37 @@ __device__ void run_spans(const ReduceArgs &a, const uint8_t *base, const Sel &s
             if (x >= 0 && x < sp.ext && x % sp.istep == 0) bits |= 1u << t;
         }
     }
-    const uint32_t dm = (1u << sp.kk) - 1u;
-    RadixCounter rc;
-    rc.init(s, a.ndim, dm, (uint64_t)(q0 + p), (uint64_t)sp.P);
+    const int64_t M = (q1 - q0 + sp.P - 1) / sp.P;   // spans per lane group
+    const int64_t qa = q0 + (int64_t)p * M;
+    const int64_t qb = qa + M < q1 ? qa + M : q1;
+    SpanWalk w;
     // span-independent part of a group's address (elements; may be -off < 0)
-    const int32_t gofs = j * NU - sp.off + sp.m_in;
-    const int64_t nit = (q1 - q0 + sp.P - 1) / sp.P;
+    w.init(a, s, sp.kk, qa < q1 ? qa : q0, j * NU - sp.off + sp.m_in);
+    const int kk = sp.kk;
     // groups in flight per lane: 4, or 8 plain vectors' worth when shuffled
     // (f64: one group = 8 vectors; 4 of them took k_reduce_u to ~300 VGPRs)
-    constexpr int U = VPL == 1 ? 4 : (8 / VPL > 0 ? 8 / VPL : 1);
-    int64_t q = q0 + p;
-    for (int64_t it = 0; it < nit; it += U) {
+#ifndef PYAS_SPANS_U
+#define PYAS_SPANS_U 2   // plain groups in flight per lane (4 took k_reduce_u f32 to 248 VGPRs + scratch)
+#endif
+    constexpr int U = VPL == 1 ? PYAS_SPANS_U : (8 / VPL > 0 ? 8 / VPL : 1);
+    int64_t q = qa;
+    for (int64_t it = 0; it < M; it += U) {   // uniform trip count
         uint4 r[U][VPL];
         bool on[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            on[u] = bits != 0 && q < q1;
+            on[u] = bits != 0 && q < qb;
 #pragma unroll
             for (int v = 0; v < VPL; ++v) r[u][v] = make_uint4(0u, 0u, 0u, 0u);
             if (on[u]) {
-                int32_t mem = gofs;
-#pragma unroll
-                for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-                    if (d < sp.kk) mem += (int32_t)sel_index(s, a.pool, d, rc.idx[d]) * (int32_t)a.cstride[d];
                 if constexpr (SH) {
-                    ldu<T, true, true>(base, base + (int64_t)mem * ES, a.chunk_elems, r[u]);
+                    ldu<T, true, true>(base, base + (int64_t)w.mem * ES, a.chunk_elems, r[u]);
                 } else {
-                    r[u][0] = ldg16(reinterpret_cast<const uint4 *>(base + (int64_t)mem * ES));
+                    r[u][0] = ldg16(reinterpret_cast<const uint4 *>(base + (int64_t)w.mem * ES));
                 }
+                if (q + 1 < qb) w.next(a, s, kk);
             }
-            rc.advance();
-            q += sp.P;
+            ++q;
         }
         bool bad = false;
 #pragma unroll
@@ -1277,6 +1344,10 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
 #pragma unroll
     for (int d = 0; d < PYAS_MAX_DIMS; ++d) digit[d] = 0;
     int64_t n = nk;
+    // PYAS_FOLD_ZERO_SIGN_* (flags bits 8-9): the sign of the last layer whose
+    // min (max) is a zero (elementwise `out` calls; the records carry level 1)
+    const uint32_t zs = (flags >> 8) & 3u;
+    bool zneg = false;
     constexpr int U = 8;
     for (int64_t l0 = 0; l0 < n_layers; l0 += U) {
         int64_t off[U];
@@ -1307,6 +1378,21 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (l0 + u < n_layers) merge(acc, p[u], round);
+        if constexpr (TT<T>::kind == 0) {
+            if (zs) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (l0 + u < n_layers && p[u].count > 0) {
+                        const double v = zs == 1 ? p[u].min.f : p[u].max.f;
+                        if (v == 0.0) zneg = __builtin_signbit(v) != 0;
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (TT<T>::kind == 0) {
+        if (zs == 1 && acc.mn == (T)0) acc.mn = zneg ? (T)-0.0 : (T)0.0;
+        if (zs == 2 && acc.mx == (T)0) acc.mx = zneg ? (T)-0.0 : (T)0.0;
     }
     store_wpartial(out + f, acc);
 }
@@ -1975,23 +2061,26 @@ struct CutWalk {
 // layouts' element ro * RI + x): bit r set iff r lies in the box.  Built by
 // the whole block; nr <= 32 * kCutMapWords (host-checked).
 __device__ __forceinline__ void cut_map(const AxesArgs &a, const CutBox &cb, int64_t nr, uint32_t *map) {
+    // one position per lane, 64 per wave step, words from a ballot (a
+    // word per thread, 32 serial decompositions each, made the LDS row
+    // layout's small workgroups wait ~2k cycles on threads 0-1: C3
+    // [1:1023]^3 (2,) 1.30 ms)
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
     const int64_t nw = (nr + 31) / 32;
-    for (int64_t w = threadIdx.x; w < nw; w += kBlock) {
-        uint32_t bits = 0;
-        for (int b = 0; b < 32; ++b) {
-            uint32_t r = (uint32_t)(w * 32 + b);
-            bool in = (int64_t)r < nr;
+    for (int64_t r0 = (int64_t)wv * kWave; r0 < nr; r0 += kBlock) {   // wave-uniform
+        uint32_t r = (uint32_t)(r0 + lane);
+        bool in = (int64_t)r < nr;
 #pragma unroll
-            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-                if (d < a.r.ndim && ((a.axes >> d) & 1u)) {
-                    const uint32_t n = (uint32_t)a.r.shape[d], q = r / n, c = r - q * n;
-                    r = q;
-                    in = in && (int32_t)c >= cb.lo[d] && (int32_t)c < cb.hi[d];
-                }
+        for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+            if (d < a.r.ndim && ((a.axes >> d) & 1u)) {
+                const uint32_t n = (uint32_t)a.r.shape[d], q = r / n, c = r - q * n;
+                r = q;
+                in = in && (int32_t)c >= cb.lo[d] && (int32_t)c < cb.hi[d];
             }
-            bits |= in ? 1u << b : 0u;
         }
-        map[w] = bits;
+        const uint64_t b = __ballot(in);
+        if (lane == 0) map[r0 / 32] = (uint32_t)b;
+        if (lane == 0 && r0 / 32 + 1 < nw) map[r0 / 32 + 1] = (uint32_t)(b >> 32);
     }
     if (threadIdx.x == 0) map[nw] = 0;   // cut_bits may read one word past the end
     __syncthreads();
@@ -2056,13 +2145,49 @@ __device__ __forceinline__ void col_consume_p(const uint4 *w, TileAcc<T> *acc, c
     }
 }
 
+// NumPy's sign of a zero min/max per column output (elementwise level-1
+// calls: the chunk's innermost non-1 dim kept, so every later zero wins).
+// ZT 1 (splits, S > 1: rows interleave across lanes): zt[k] = ((r + 1) << 1)
+// | sign of the last zero of output k this lane read (row r in visiting
+// order), max-combined across splits.  ZT 2 (S == 1: one lane walks every
+// row in order): zt[k] = the high word of the last zero read (1: none), a
+// compare and a select per element; zt_final turns it into ZT 1's form.
+// rows: the step's rows in the box (bit u = row r0 + u * S).  Zeros are
+// masked all or none (value rules), so a masked zero never decides.
+template <typename T, bool BSWAP, int U, int ZT>
+__device__ __forceinline__ void col_track_zeros(const uint4 *w, uint32_t *zt, uint32_t rows, int64_t r0, int S) {
+    constexpr int N = 16 / sizeof(T);
+    using Ub = typename TT<T>::U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        T x[N];
+        unpack16<T, BSWAP>(w[u], x);
+        const bool in = (rows >> u) & 1u;
+        if constexpr (ZT == 2) {
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                const uint32_t hi = (uint32_t)(bits_to<Ub>(x[k]) >> (8 * sizeof(T) - 32));
+                zt[k] = (in && x[k] == (T)0) ? hi : zt[k];
+            }
+        } else {
+            const uint32_t key = (uint32_t)(r0 + (int64_t)u * S + 1) << 1;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                const uint32_t sg = (uint32_t)(bits_to<Ub>(x[k]) >> (8 * sizeof(T) - 1));
+                if (in && x[k] == (T)0) zt[k] = key | sg;
+            }
+        }
+    }
+}
+__device__ __forceinline__ uint32_t zt_final(uint32_t z) { return z == 1u ? 0u : (2u | (z >> 31)); }
+
 // One pass of the column layout over one chunk: lane (il, sp) folds split
 // sp of the reduced rows of vector item i (N consecutive kept outputs) into
 // acc[N], PYAS_COL_U 16-B loads in flight.
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, bool CUT = false>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, bool CUT = false, int ZT = 0>
 __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base, int64_t n, int64_t i,
                                          int sp, const MaskT<T> &mk, TileAcc<T> *acc,
-                                         const uint32_t *rmap = nullptr) {
+                                         const uint32_t *rmap = nullptr, uint32_t *zt = nullptr) {
     constexpr int ES = sizeof(T), N = 16 / ES;
     const int S = d.split;
     const int64_t KIV = d.KI / N, R = d.RO * d.RI;
@@ -2085,21 +2210,25 @@ __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base
         uint4 w[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) { w[u] = ldv<T, SHUF, AL>(base, p, n); next(); }
+        uint32_t rb = (1u << U) - 1u;
         if constexpr (CUT) {
-            uint32_t rb = 0;
+            rb = 0;
 #pragma unroll
             for (int u = 0; u < U; ++u) rb |= cut_bits(rmap, sp + (t + u) * S, 1) << u;
             col_consume_p<T, BSWAP, MASKED, U>(w, acc, mk, rb);
         } else {
             col_consume<T, BSWAP, MASKED, U>(w, acc, mk);
         }
+        if constexpr (ZT) col_track_zeros<T, BSWAP, U, ZT>(w, zt, rb, sp + t * S, S);
     }
     for (; t < nt; ++t) {
+        const uint4 wv = ldv<T, SHUF, AL>(base, p, n);
         T x[N];
-        unpack16<T, BSWAP>(ldv<T, SHUF, AL>(base, p, n), x);
+        unpack16<T, BSWAP>(wv, x);
         next();
+        uint32_t rb = 1u;
         if constexpr (CUT) {
-            const uint32_t rb = cut_bits(rmap, sp + t * S, 1);
+            rb = cut_bits(rmap, sp + t * S, 1);
 #pragma unroll
             for (int k = 0; k < N; ++k)
                 if (acc[k].template add_pred<1, MASKED, 1>(x + k, rb, mk)) acc[k].template check_nan<1>(x + k);
@@ -2107,6 +2236,7 @@ __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base
 #pragma unroll
             for (int k = 0; k < N; ++k) acc[k].template add_n<1, MASKED, false>(x + k, mk);
         }
+        if constexpr (ZT) col_track_zeros<T, BSWAP, 1, ZT>(&wv, zt, rb, sp + t * S, S);
     }
     if constexpr (!MASKED && !CUT) {   // add_n counts only in masked mode
 #pragma unroll
@@ -2120,10 +2250,10 @@ __device__ __forceinline__ void col_rows(const AxesDense &d, const uint8_t *base
 #ifndef PYAS_COL_RING
 #define PYAS_COL_RING 1
 #endif
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool CUT = false>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool CUT = false, int ZT = 0>
 __device__ __forceinline__ void col_rows_ring(const AxesDense &d, const uint8_t *base, int64_t n, int64_t i,
                                               int sp, const MaskT<T> &mk, TileAcc<T> *acc,
-                                              const uint32_t *rmap = nullptr) {
+                                              const uint32_t *rmap = nullptr, uint32_t *zt = nullptr) {
     constexpr int ES = sizeof(T), N = 16 / ES, U = PYAS_COL_U;
     const int S = d.split;
     const int64_t KIV = d.KI / N, R = d.RO * d.RI;
@@ -2166,19 +2296,27 @@ __device__ __forceinline__ void col_rows_ring(const AxesDense &d, const uint8_t 
 #pragma unroll
                 for (int u = 0; u < U; ++u) cur[u] = buf[s][u];
                 if (g + s + 2 < ng) fetch(buf[s]);
-                if constexpr (CUT) col_consume_p<T, BSWAP, MASKED, U>(cur, acc, mk, rbits(g + s));
-                else col_consume<T, BSWAP, MASKED, U>(cur, acc, mk);
+                uint32_t rb = (1u << U) - 1u;
+                if constexpr (CUT) {
+                    rb = rbits(g + s);
+                    col_consume_p<T, BSWAP, MASKED, U>(cur, acc, mk, rb);
+                } else {
+                    col_consume<T, BSWAP, MASKED, U>(cur, acc, mk);
+                }
+                if constexpr (ZT) col_track_zeros<T, BSWAP, U, ZT>(cur, zt, rb, sp + (g + s) * U * S, S);
             }
         }
     }
     for (int64_t t = ng * U; t < nt; ++t) {   // p is at row ng * U
+        const uint4 wv = ldv<T, SHUF, true>(base, p, n);
         T x[N];
-        unpack16<T, BSWAP>(ldv<T, SHUF, true>(base, p, n), x);
+        unpack16<T, BSWAP>(wv, x);
         p += step_off;
         ri += dr;
         if (ri >= d.RI) { ri -= d.RI; p += wrap_off; }
+        uint32_t rb = 1u;
         if constexpr (CUT) {
-            const uint32_t rb = cut_bits(rmap, sp + t * S, 1);
+            rb = cut_bits(rmap, sp + t * S, 1);
 #pragma unroll
             for (int k = 0; k < N; ++k)
                 if (acc[k].template add_pred<1, MASKED, 1>(x + k, rb, mk)) acc[k].template check_nan<1>(x + k);
@@ -2186,6 +2324,7 @@ __device__ __forceinline__ void col_rows_ring(const AxesDense &d, const uint8_t 
 #pragma unroll
             for (int k = 0; k < N; ++k) acc[k].template add_n<1, MASKED, false>(x + k, mk);
         }
+        if constexpr (ZT) col_track_zeros<T, BSWAP, 1, ZT>(&wv, zt, rb, sp + t * S, S);
     }
     if constexpr (!MASKED && !CUT) {
 #pragma unroll
@@ -2263,7 +2402,17 @@ __device__ void col_rows_units(const AxesDense &d, const uint8_t *base, int64_t 
     }
 }
 
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, bool CUT = false>
+// NumPy's sign on a zero min/max partial (ZT, a.zs = 1 min / 2 max): the
+// sign of the last zero the output's column walk saw (col_track_zeros).
+template <typename T>
+__device__ __forceinline__ void zs_apply(const AxesArgs &a, pyas_partial &pp, uint32_t z) {
+    if (!z) return;
+    const double sg = (z & 1u) ? -0.0 : 0.0;
+    if (a.zs == 1 && pp.min.f == 0.0) pp.min.f = sg;
+    if (a.zs == 2 && pp.max.f == 0.0) pp.max.f = sg;
+}
+
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, bool CUT = false, bool ZT = false>
 __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                           const MaskT<T> &mk, uint4 *stage, const CutBox *cb = nullptr,
                           const uint32_t *rmap = nullptr) {
@@ -2276,16 +2425,32 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
     // aligned chunks: the ring walk (measured faster than the shuffled unit
     // exchange too); PYAS_COL_RING=0 builds the earlier walks
     constexpr bool ring = PYAS_COL_RING && AL;
-    const bool units = !CUT && !ring && SHUF && AL && col_units_ok<T>(d) && ldu_aligned<T, SHUF>(base, a.r.chunk_elems);
+    const bool units = !CUT && !ZT && !ring && SHUF && AL && col_units_ok<T>(d) &&
+                       ldu_aligned<T, SHUF>(base, a.r.chunk_elems);
+    // ZT: the splits' zero trackers meet here (max of the keys)
+    __shared__ uint32_t zfold[ZT ? N * kBlock : 1];
     for (int64_t i0 = j * IT; i0 < items; i0 += d.bpc * IT) {   // block-uniform
         const int64_t i = i0 + il;
         TileAcc<T> acc[N];
+        uint32_t zt[N];
 #pragma unroll
-        for (int k = 0; k < N; ++k) acc[k].init();
+        for (int k = 0; k < N; ++k) { acc[k].init(); zt[k] = 0; }
+        if constexpr (ZT) {   // one lane per column (S == 1): the compare-and-select tracker
+            if (S == 1) {
+#pragma unroll
+                for (int k = 0; k < N; ++k) zt[k] = 1u;
+            }
+        }
         if constexpr (ring) {
-            if (i < items && sp < S && sp < d.RO * d.RI)
-                col_rows_ring<T, SHUF, BSWAP, MASKED, CUT>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap);
-        } else if constexpr (SHUF && sizeof(T) >= 4 && !CUT) {
+            if (i < items && sp < S && sp < d.RO * d.RI) {
+                if constexpr (ZT) {
+                    if (S == 1) col_rows_ring<T, SHUF, BSWAP, MASKED, CUT, 2>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap, zt);
+                    else col_rows_ring<T, SHUF, BSWAP, MASKED, CUT, 1>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap, zt);
+                } else {
+                    col_rows_ring<T, SHUF, BSWAP, MASKED, CUT>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap, zt);
+                }
+            }
+        } else if constexpr (SHUF && sizeof(T) >= 4 && !CUT && !ZT) {
             if (units) {
                 if (i < items && sp < S) col_rows_units<T, BSWAP, MASKED>(d, base, a.r.chunk_elems, i, sp, mk, acc, stage);
                 __syncthreads();   // the exchange area is reused below
@@ -2293,7 +2458,32 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
                 col_rows<T, SHUF, BSWAP, MASKED, AL>(d, base, a.r.chunk_elems, i, sp, mk, acc);
             }
         } else if (i < items && sp < S && sp < d.RO * d.RI) {
-            col_rows<T, SHUF, BSWAP, MASKED, AL, CUT>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap);
+            if constexpr (ZT) {
+                if (S == 1) col_rows<T, SHUF, BSWAP, MASKED, AL, CUT, 2>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap, zt);
+                else col_rows<T, SHUF, BSWAP, MASKED, AL, CUT, 1>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap, zt);
+            } else {
+                col_rows<T, SHUF, BSWAP, MASKED, AL, CUT>(d, base, a.r.chunk_elems, i, sp, mk, acc, rmap, zt);
+            }
+        }
+        if constexpr (ZT) {
+            if (S == 1) {
+#pragma unroll
+                for (int k = 0; k < N; ++k) zt[k] = zt_final(zt[k]);
+            } else {   // the latest zero over the splits (rows interleave: the largest key)
+#pragma unroll
+                for (int k = 0; k < N; ++k) zfold[k * kBlock + threadIdx.x] = zt[k];
+                __syncthreads();
+                if (sp == 0) {
+                    for (int q = 1; q < S; ++q) {
+#pragma unroll
+                        for (int k = 0; k < N; ++k) {
+                            const uint32_t o = zfold[k * kBlock + q * IT + il];
+                            zt[k] = o > zt[k] ? o : zt[k];
+                        }
+                    }
+                }
+                __syncthreads();
+            }
         }
         if constexpr (CUT) {
             PYAS_MARK(3);
@@ -2314,6 +2504,7 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
                     if (o >= 0) {
                         pyas_partial pp;
                         tile_store_lane(acc[k], &pp);
+                        if constexpr (ZT) zs_apply<T>(a, pp, zt[k]);
                         put_out<T>(a, ob + o, pp);
                     }
                 }
@@ -2332,6 +2523,7 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
                 if (sp == 0) {
                     pyas_partial pp;
                     tile_store_lane(acc[k], &pp);
+                    if constexpr (ZT) zs_apply<T>(a, pp, zt[k]);
                     stage_put<T>(a, stage, il * N + k, pp);
                 }
             }
@@ -2345,6 +2537,7 @@ __device__ void dense_col(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
                 if (sp == 0 && i < items) {
                     pyas_partial pp;
                     tile_store_lane(acc[k], &pp);
+                    if constexpr (ZT) zs_apply<T>(a, pp, zt[k]);
                     put_out<T>(a, ob + i * N + k, pp);
                 }
             }
@@ -2489,10 +2682,64 @@ __device__ void dense_row(const AxesArgs &a, int64_t c, int64_t j, const uint8_t
 constexpr int kRowLdsStride = 17;   // 16-B vectors per LDS run (V <= 16, + 1 pad)
 
 
-template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int H, bool CUT = false>
+// ZT (a.zs: 1 min, 2 max; floats): each output row is ONE contiguous NumPy
+// call over the box's run along the innermost dim (storage.py:99-100; the
+// reduced group is that dim alone when the chunk is cut).  A row whose
+// min/max is a zero keys NumPy's winning zero from the tile still in LDS, as
+// k_axes_fold_row does (the K1/W keys of tie_keys on bit masks of the call's
+// positions, row_zs_masks): the last remainder zero if any, else the later of
+// the last seed/top-lane zero and, unless the seed is a zero, the last zero of
+// the lowest lane-rank class holding one.  Its sign goes into the record.
+// Zero-free tiles cost one ballot.
+__device__ __forceinline__ int msb64(uint64_t v) { return 63 - __builtin_clzll(v); }   // v != 0
+constexpr int kRowZsWords = 4 + 64;   // rem, top, vec, box run, then the rank classes
+
+// The masks ZT reads (LDS, zm[kRowZsWords]) for a call of L positions e
+// (e = 0 the seed, then m = L - 1 elements: the first nv in t.lanes lanes, the
+// rest remainder): built by wave 0 with ballots, once per workgroup.
+__device__ __forceinline__ void row_zs_masks(const TieRule &t, int L, uint64_t *zm) {
+    if (threadIdx.x >= kWave) return;
+    const int e = threadIdx.x, lanes = t.lanes;
+    const int m = L - 1, nv = m - m % lanes;
+    const bool vec = e >= 1 && e <= nv;
+    const int rk = vec ? (int)t.rank[(e - 1) % lanes] : -1;
+    const uint64_t rem = __ballot(e > nv && e < L), top = __ballot(vec && rk == 0), vm = __ballot(vec);
+    const uint64_t run = __ballot(e < L);
+    for (int k = 0; k < lanes && k < 64; ++k) {
+        const uint64_t cm = __ballot(rk == k);
+        if (e == 0) zm[4 + k] = cm;
+    }
+    if (e == 0) {
+        zm[0] = rem;
+        zm[1] = top;
+        zm[2] = vm;
+        zm[3] = run;
+    }
+}
+
+// The winning zero of a row call (box positions Z, bit e = position e).
+__device__ __forceinline__ int row_zs_pick(uint64_t Z, const uint64_t *zm, int lanes) {
+    const uint64_t zr = Z & zm[0];
+    if (zr) return msb64(zr);
+    const uint64_t sig = Z & (zm[1] | 1u);
+    const int e1 = sig ? msb64(sig) : -1;
+    int ew = -1;
+    if (!(Z & 1u) && (Z & zm[2])) {
+        for (int k = 0; k < lanes; ++k) {
+            const uint64_t cz = Z & zm[4 + k];
+            if (cz) {
+                ew = msb64(cz);
+                break;
+            }
+        }
+    }
+    return ew > e1 ? ew : e1;
+}
+
+template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int H, bool CUT = false, bool ZT = false>
 __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                               const MaskT<T> &mk, uint4 *tile, const CutBox *cb = nullptr,
-                              const uint32_t *rmap = nullptr) {
+                              const uint32_t *rmap = nullptr, const uint64_t *zm = nullptr, int zs0 = 0) {
     const int64_t n = a.r.chunk_elems;
     constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
     // load units per lane per tile (64 * UL * VPL >= the tile's RPW * 16 vectors)
@@ -2506,12 +2753,11 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
     const int64_t nwaves = d.bpc * (kBlock / kWave);
     const int64_t ob = sload(a.out_offsets + c);
     // tile unit q = u * kWave + lane: vectors q*VPL .. +VPL-1, in run q*VPL / V
-    int lrow[UL], lcol[UL];
+    int lidx[UL];   // the unit's place in the wave's LDS tile (run q / V, vector q % V)
 #pragma unroll
     for (int u = 0; u < UL; ++u) {
-        const int q = (u * kWave + lane) * VPL;
-        lrow[u] = q / V;
-        lcol[u] = q - lrow[u] * V;
+        const int q = (u * kWave + lane) * VPL, lr = q / V;
+        lidx[u] = lr * kRowLdsStride + (q - lr * V);
     }
     uint4 w[UL][VPL];
     auto load = [&](int64_t o0) {
@@ -2522,6 +2768,15 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
             if ((u * kWave + lane) * VPL < nvec)
                 ldu<T, SHUF, AL>(base, src + (int64_t)(u * kWave + lane) * VPL * 16, n, w[u]);
     };
+    // CUT: this lane's VH * N run positions inside the box (the same for
+    // every row: RO == 1), read from the map once
+    uint64_t lbits = 0;
+    if constexpr (CUT) {
+        const int64_t p0 = (int64_t)h * VH * N;
+        const int nb = VH * N;
+        lbits = cut_bits(rmap, p0, nb < 32 ? nb : 32);
+        if (nb > 32) lbits |= (uint64_t)cut_bits(rmap, p0 + 32, nb - 32 < 32 ? nb - 32 : 32) << 32;
+    }
     int64_t o0 = wave * RPW;
     if (o0 < d.KO) load(o0);
     for (; o0 < d.KO; o0 += nwaves * RPW) {   // wave-uniform
@@ -2530,7 +2785,7 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
         for (int u = 0; u < UL; ++u)
             if ((u * kWave + lane) * VPL < nvec) {
 #pragma unroll
-                for (int i = 0; i < VPL; ++i) t[lrow[u] * kRowLdsStride + lcol[u] + i] = w[u][i];
+                for (int i = 0; i < VPL; ++i) t[lidx[u] + i] = w[u][i];
             }
         wave_sync_lds();
         if (o0 + nwaves * RPW < d.KO) load(o0 + nwaves * RPW);
@@ -2541,8 +2796,8 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
             T x[N];
             unpack16<T, BSWAP>(row[i], x);
             if constexpr (CUT) {   // the run's elements inside the box (RO == 1: position = element)
-                if (acc.template add_pred<N, MASKED, 1>(x, cut_bits(rmap, (int64_t)(h * VH + i) * N, N), mk)) {
-                    const uint32_t b = cut_bits(rmap, (int64_t)(h * VH + i) * N, N);
+                const uint32_t b = (uint32_t)(lbits >> (i * N)) & (uint32_t)((1ull << N) - 1);
+                if (acc.template add_pred<N, MASKED, 1>(x, b, mk)) {
 #pragma unroll
                     for (int q = 0; q < N; ++q)
                         if ((b >> q) & 1u) acc.template check_nan<1>(&x[q]);
@@ -2554,12 +2809,60 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
         if constexpr (!MASKED && !CUT) acc.count += (uint32_t)(VH * N);
         uint32_t cnt, nan;
         group_reduce(acc, H, cnt, nan);
+        int zsg = -1;   // ZT: the row's NumPy zero sign bit (-1: not a zero row)
+        if constexpr (ZT) {
+            const T v = a.zs == 1 ? acc.mn : acc.mx;
+            const bool zrow = o0 + r < d.KO && cnt > 0 && !nan && v == (T)0;   // the row's H lanes agree
+            if (__ballot(zrow)) {
+                uint64_t Z = 0;
+                if (zrow) {
+                    // the lane's zero bits shifted in (its first element ends
+                    // up highest), then reversed to element order at its offset
+                    using ZW = typename std::conditional<H == 1, uint64_t, uint32_t>::type;
+                    ZW zl = 0;
+                    for (int i = 0; i < VH; ++i) {
+                        T xe[N];
+                        unpack16<T, BSWAP>(row[i], xe);
+#pragma unroll
+                        for (int k = 0; k < N; ++k) zl = (ZW)((zl << 1) | (xe[k] == (T)0 ? 1u : 0u));
+                    }
+                    const int J = VH * N;
+                    if constexpr (H == 1) Z = __builtin_bitreverse64(zl) >> (64 - J);
+                    else Z = (uint64_t)(__builtin_bitreverse32(zl) >> (32 - J)) << (h * J);
+                }
+#pragma unroll
+                for (int mm = H / 2; mm >= 1; mm >>= 1) Z |= shfl_xor(Z, mm);
+                if (zrow && h == 0) {
+                    // the box's run along the innermost dim: positions from its start zs0
+                    const int e = row_zs_pick((Z >> zs0) & zm[3], zm, a.t.lanes);
+                    if (e >= 0) {
+                        const int x = zs0 + e;
+                        T xe[N];
+                        unpack16<T, BSWAP>(t[r * kRowLdsStride + x / N], xe);
+                        T we = xe[0];
+#pragma unroll
+                        for (int k = 1; k < N; ++k) we = (x % N) == k ? xe[k] : we;
+                        zsg = __builtin_signbit(we) ? 1 : 0;
+                    }
+                }
+            }
+        }
+        auto row_out = [&](pyas_partial &pp) {
+            store_group(acc, cnt, nan, &pp);
+            if constexpr (ZT) {
+                if (zsg >= 0) {
+                    const T zz = zsg ? -(T)0 : (T)0;
+                    if (a.zs == 1) TT<T>::put(pp.min, zz);
+                    else TT<T>::put(pp.max, zz);
+                }
+            }
+        };
         if constexpr (CUT) {   // rows inside the box only, at their place in the cut chunk's array
             if (h == 0 && o0 + r < d.KO) {
                 const int64_t oo = cut_out(a, *cb, o0 + r);
                 if (oo >= 0) {
                     pyas_partial pp;
-                    store_group(acc, cnt, nan, &pp);
+                    row_out(pp);
                     put_out<T>(a, ob + oo, pp);
                 }
             }
@@ -2573,7 +2876,7 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
         wave_sync_lds();
         if (h == 0) {
             pyas_partial pp;
-            store_group(acc, cnt, nan, &pp);
+            row_out(pp);
             stage_put<T>(a, t, r, pp);
         }
         wave_sync_lds();
@@ -2588,8 +2891,12 @@ __device__ __forceinline__ bool dense_owns(const AxesArgs &a, const Sel &s) {
     return a.d.mode != 0 && (chunk_is_full(s, a.r.shape, a.r.ndim) || cut_eligible(a, s));
 }
 
-template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE, bool CUTS>
+// ZS (a.zs set; float types, MODE 1 or >= 4; kernels of their own, so the
+// keying's registers never cost the other launches occupancy): the walk keys
+// NumPy's sign of a zero min/max of every chunk it takes, whole or cut.
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE, bool CUTS, bool ZS = false>
 __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
+    static_assert(!ZS || (CUTS && TT<T>::kind == 0 && (MODE == 1 || MODE >= 4)), "zero-sign keying: float column/LDS rows");
     const int64_t c = blockIdx.x / a.d.bpc;
     const int64_t j = blockIdx.x - c * a.d.bpc;
     const ReduceArgs &r = a.r;
@@ -2607,6 +2914,9 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
     constexpr int kLds = MODE == 1 ? (sizeof(T) >= 4 ? (kBlock * 8 > col_units_lds<T>() ? kBlock * 8 : col_units_lds<T>()) : 1)
                         : MODE >= 4 ? (kBlock / kWave) * (kWave / H) * kRowLdsStride : 1;
     __shared__ uint4 lds[kLds];
+    // ZS row layouts: the masks of the row call's positions (row_zs_masks)
+    constexpr bool kRowZs = ZS && MODE >= 4;
+    __shared__ uint64_t zm[kRowZs ? kRowZsWords : 1];
     if constexpr (CUTS) {
         // a cut chunk (a.cuts launches): read as its whole chunk, the box
         // applied through the reduced-position map and the output remap
@@ -2616,13 +2926,26 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
             PYAS_MARK(1);
             cut_box(a, s, cb);
             cut_map(a, cb, a.d.RO * a.d.RI, cmap);
+            int zs0 = 0;   // kRowZs: the box's run along the innermost dim (static indices:
+            int zL = 1;    // a runtime index would put the box in scratch memory)
+            if constexpr (kRowZs) {
+#pragma unroll
+                for (int dd = 0; dd < PYAS_MAX_DIMS; ++dd) {
+                    if (dd == r.ndim - 1) {
+                        zs0 = cb.lo[dd];
+                        zL = cb.hi[dd] - cb.lo[dd];
+                    }
+                }
+                row_zs_masks(a.t, zL, zm);
+                __syncthreads();
+            }
             PYAS_MARK(2);
             if constexpr (MODE == 1) {
-                if (al) dense_col<T, SHUF, BSWAP, MASKED, true, true>(a, c, j, base, mk, lds, &cb, cmap);
-                else dense_col<T, SHUF, BSWAP, MASKED, false, true>(a, c, j, base, mk, lds, &cb, cmap);
+                if (al) dense_col<T, SHUF, BSWAP, MASKED, true, true, ZS>(a, c, j, base, mk, lds, &cb, cmap);
+                else dense_col<T, SHUF, BSWAP, MASKED, false, true, ZS>(a, c, j, base, mk, lds, &cb, cmap);
             } else if constexpr (MODE >= 4) {
-                if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H, true>(a, c, j, base, mk, lds, &cb, cmap);
-                else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H, true>(a, c, j, base, mk, lds, &cb, cmap);
+                if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H, true, ZS>(a, c, j, base, mk, lds, &cb, cmap, zm, zs0);
+                else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H, true, ZS>(a, c, j, base, mk, lds, &cb, cmap, zm, zs0);
             } else {
                 constexpr int UO = MODE == 2 ? 1 : 4;
                 if (al) dense_row<T, SHUF, BSWAP, MASKED, true, UO, true>(a, c, j, base, mk, &cb, cmap);
@@ -2633,11 +2956,15 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
         }
     }
     if constexpr (MODE == 1) {
-        if (al) dense_col<T, SHUF, BSWAP, MASKED, true>(a, c, j, base, mk, lds);
-        else dense_col<T, SHUF, BSWAP, MASKED, false>(a, c, j, base, mk, lds);
+        if (al) dense_col<T, SHUF, BSWAP, MASKED, true, false, ZS>(a, c, j, base, mk, lds);
+        else dense_col<T, SHUF, BSWAP, MASKED, false, false, ZS>(a, c, j, base, mk, lds);
     } else if constexpr (MODE >= 4) {
-        if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H>(a, c, j, base, mk, lds);
-        else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H>(a, c, j, base, mk, lds);
+        if constexpr (kRowZs) {
+            row_zs_masks(a.t, (int)a.d.RI, zm);
+            __syncthreads();
+        }
+        if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H, false, ZS>(a, c, j, base, mk, lds, nullptr, nullptr, zm);
+        else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H, false, ZS>(a, c, j, base, mk, lds, nullptr, nullptr, zm);
     } else if constexpr (MODE == 2) {
         if (al) dense_row<T, SHUF, BSWAP, MASKED, true, 1>(a, c, j, base, mk);
         else dense_row<T, SHUF, BSWAP, MASKED, false, 1>(a, c, j, base, mk);
@@ -2648,18 +2975,45 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
 }
 
 // One kernel per layout family, so each carries its own occupancy floor.
-// CUTS: the launch also takes the batch's cut chunks (AxesArgs::cuts).
-template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE, bool CUTS = false>
+// The *_cut kernels also take the batch's cut chunks (AxesArgs::cuts).
+#ifndef PYAS_LDS_CUT_WAVES
+#define PYAS_LDS_CUT_WAVES 4   // the cut path must not cost whole chunks a wave: 137 VGPRs (3 per SIMD)
+#endif
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_COL_WAVES) void k_axes_dense_col(AxesArgs a) {
-    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, CUTS>(a);
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, false>(a);
 }
-template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE, bool CUTS = false>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_ROW_WAVES) void k_axes_dense_row(AxesArgs a) {
-    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, CUTS>(a);
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, false>(a);
 }
-template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE, bool CUTS = false>
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LDS_WAVES) void k_axes_dense_lds(AxesArgs a) {
-    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, CUTS>(a);
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, false>(a);
+}
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_COL_WAVES) void k_axes_dense_col_cut(AxesArgs a) {
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, true>(a);
+}
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_ROW_WAVES) void k_axes_dense_row_cut(AxesArgs a) {
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, true>(a);
+}
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LDS_CUT_WAVES) void k_axes_dense_lds_cut(AxesArgs a) {
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, true>(a);
+}
+// Zero-sign keying (a.zs): column and LDS row layouts, whole and cut chunks
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_COL_WAVES) void k_axes_dense_col_zs(AxesArgs a) {
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, true, true>(a);
+}
+#ifndef PYAS_LDS_ZS_WAVES
+#define PYAS_LDS_ZS_WAVES 3   // at 4 the row keying spilled 256 B per lane (C3 [1:1023]^3 (2,) min 1.75 ms)
+#endif
+template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
+__global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LDS_ZS_WAVES) void k_axes_dense_lds_zs(AxesArgs a) {
+    axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, true, true>(a);
 }
 
 // Whole-chunk box query, column layout, chunk layers folded in the kernel
@@ -3452,7 +3806,6 @@ __device__ __forceinline__ void tie_keys(int64_t e, uint64_t sg, const TieCall &
 __device__ __forceinline__ int tie_finalize(uint64_t k1, uint64_t w, uint64_t ka, const TieCall &c,
                                             const TieRule &t);
 
-__device__ __forceinline__ int msb64(uint64_t v) { return 63 - __builtin_clzll(v); }   // v != 0
 
 // A position's place in a contiguous call, stepped one position at a time
 // (l = q * lr + k * piece + kpos): tie_keys(l, sign 0) without a division,
@@ -4625,7 +4978,10 @@ static void launch_reduce_ts(const ReduceArgs &a, bool shuf, bool bsw, bool mask
     if constexpr (sizeof(T) == 1) {
         if (masked) PYAS_L(false, false, kMaskAll);
         else PYAS_L(false, false, 0);
-    } else if constexpr (!SEL && sizeof(T) >= 4) {
+    } else if constexpr (sizeof(T) >= 4) {
+        // the trimmed mask modes for the selection kernel too (a cut
+        // chunk's predicate stream with all six compares was VALU-bound:
+        // C3 [1:1023]^3 k_reduce_u 1.11 ms)
 #define PYAS_LM(S, B)                                                 \
         do {                                                          \
             if (!mm) PYAS_L(S, B, 0);                                 \
@@ -4710,13 +5066,17 @@ hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int
 template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
 static void launch_dense_k(const AxesArgs &a, dim3 g, hipStream_t st) {
     const dim3 blk(kBlock);
-    if (a.cuts) {
-        // with cut chunks: the unmasked and full-mask variants only (the
-        // trimmed mask modes evaluate the same rules)
-        constexpr int M = MASKED ? kMaskAll : 0;
-        if constexpr (MODE == 1) hipLaunchKernelGGL((k_axes_dense_col<T, SHUF, BSWAP, M, MODE, true>), g, blk, 0, st, a);
-        else if constexpr (MODE >= 4) hipLaunchKernelGGL((k_axes_dense_lds<T, SHUF, BSWAP, M, MODE, true>), g, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_axes_dense_row<T, SHUF, BSWAP, M, MODE, true>), g, blk, 0, st, a);
+    if constexpr (TT<T>::kind == 0 && (MODE == 1 || MODE >= 4)) {
+        if (a.zs) {   // the host admits zero-sign keying for these layouts only
+            if constexpr (MODE == 1) hipLaunchKernelGGL((k_axes_dense_col_zs<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
+            else hipLaunchKernelGGL((k_axes_dense_lds_zs<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
+            return;
+        }
+    }
+    if (a.cuts) {   // the batch's cut chunks too (every mask mode: kMaskAll cost C3 (2,) ~2x)
+        if constexpr (MODE == 1) hipLaunchKernelGGL((k_axes_dense_col_cut<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
+        else if constexpr (MODE >= 4) hipLaunchKernelGGL((k_axes_dense_lds_cut<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((k_axes_dense_row_cut<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
         return;
     }
     if constexpr (MODE == 1) hipLaunchKernelGGL((k_axes_dense_col<T, SHUF, BSWAP, MASKED, MODE>), g, blk, 0, st, a);
@@ -4803,7 +5163,16 @@ hipError_t launch_axes_dense_t(const AxesArgs &a, bool masked, int64_t grid, hip
         }
     }
     if (a.d.mode == 1) launch_dense_m<T, 1>(a, masked, g, st);
-    else if (a.d.mode == 2) launch_dense_m<T, 2>(a, masked, g, st);
+    else return launch_axes_dense_rows_t<T>(a, masked, grid, st);   // separate object (build time)
+    return hipGetLastError();
+}
+
+// The row layouts (modes 2-6) of launch_axes_dense_t, instantiated in their
+// own object per dtype so the build runs them in parallel.
+template <typename T>
+hipError_t launch_axes_dense_rows_t(const AxesArgs &a, bool masked, int64_t grid, hipStream_t st) {
+    const dim3 g((unsigned)grid);
+    if (a.d.mode == 2) launch_dense_m<T, 2>(a, masked, g, st);
     else if (a.d.mode == 4) launch_dense_m<T, 4>(a, masked, g, st);
     else if (a.d.mode == 5) launch_dense_m<T, 5>(a, masked, g, st);
     else if (a.d.mode == 6) launch_dense_m<T, 6>(a, masked, g, st);
@@ -4895,12 +5264,25 @@ hipError_t launch_axes_fold_t(const AxesArgs &a, const FoldGrid &g, bool masked,
     if constexpr (sizeof(T) < 4) {
         return hipErrorInvalidValue;     // dense_geometry: >= 4-byte elements only
     } else if (a.d.mode >= 4) {
-        if (a.d.mode == 4) launch_fold_row<T, 1>(a, g, masked, gr, st);
-        else if (a.d.mode == 5) launch_fold_row<T, 2>(a, g, masked, gr, st);
-        else launch_fold_row<T, 4>(a, g, masked, gr, st);
+        return launch_axes_fold_rows_t<T>(a, g, masked, grid, st);   // separate object (build time)
     } else {
         if (a.shuf) launch_fold_col<T, true>(a, g, masked, gr, st);
         else launch_fold_col<T, false>(a, g, masked, gr, st);
+    }
+    return hipGetLastError();
+}
+
+// The LDS row fold (modes 4-6) of launch_axes_fold_t, in its own object.
+template <typename T>
+hipError_t launch_axes_fold_rows_t(const AxesArgs &a, const FoldGrid &g, bool masked, int64_t grid,
+                                   hipStream_t st) {
+    const dim3 gr((unsigned)grid);
+    if constexpr (sizeof(T) < 4) {
+        return hipErrorInvalidValue;
+    } else {
+        if (a.d.mode == 4) launch_fold_row<T, 1>(a, g, masked, gr, st);
+        else if (a.d.mode == 5) launch_fold_row<T, 2>(a, g, masked, gr, st);
+        else launch_fold_row<T, 4>(a, g, masked, gr, st);
     }
     return hipGetLastError();
 }
@@ -5024,9 +5406,18 @@ hipError_t launch_format_t(const pyas_partial *in, int64_t n, int32_t method, vo
     template hipError_t launch_tie_finalize_t<T>(const uint64_t *, int64_t, int32_t, const TieCall &, \
                                                  const TieRule &, uint32_t, pyas_partial *, hipStream_t);
 #define PYAS_INSTANTIATE_PART2(T)                                                              \
+    extern template hipError_t launch_axes_dense_rows_t<T>(const AxesArgs &, bool, int64_t,     \
+                                                           hipStream_t); /* part 4 */         \
     template hipError_t launch_axes_dense_t<T>(const AxesArgs &, bool, int64_t, hipStream_t);
 #define PYAS_INSTANTIATE_PART3(T)                                                              \
+    extern template hipError_t launch_axes_fold_rows_t<T>(const AxesArgs &, const FoldGrid &,   \
+                                                          bool, int64_t, hipStream_t); /* part 5 */ \
     template hipError_t launch_axes_fold_t<T>(const AxesArgs &, const FoldGrid &, bool, int64_t, \
                                               hipStream_t);
+#define PYAS_INSTANTIATE_PART4(T)                                                              \
+    template hipError_t launch_axes_dense_rows_t<T>(const AxesArgs &, bool, int64_t, hipStream_t);
+#define PYAS_INSTANTIATE_PART5(T)                                                              \
+    template hipError_t launch_axes_fold_rows_t<T>(const AxesArgs &, const FoldGrid &, bool, int64_t, \
+                                                   hipStream_t);
 
 }  // namespace pyas

@@ -202,8 +202,12 @@ def combine_segments(ctx: Context, dt, in_ptr, index_ptr, seg_ptr, n_seg, out_pt
 
 
 def combine_grid(ctx: Context, dt, in_ptr, grid: _lib.Grid, out_ptr, round_to_var: bool, stream,
-                 rec: int = 0) -> None:
-    flags = (_lib.COMBINE_ROUND_TO_VAR if round_to_var else 0) | _lib.combine_rec(rec)
+                 rec: int = 0, zero_sign: int = 0) -> None:
+    """pyas_combine_grid.  ``zero_sign`` (1 min, 2 max): the records carry
+    level 1's NumPy sign (PYAS_REC_ZERO_SIGN) and the combine keys level 2
+    (PYAS_FOLD_ZERO_SIGN_*); NotImplementedError where the `out` array's
+    calls are not elementwise."""
+    flags = (_lib.COMBINE_ROUND_TO_VAR if round_to_var else 0) | _lib.combine_rec(rec) | (int(zero_sign) << 8)
     _lib.check(ctx.lib.pyas_combine_grid(ctx.handle, dtype_code(dt), in_ptr, ctypes.byref(grid), flags,
                                          out_ptr, stream), "pyas_combine_grid")
 

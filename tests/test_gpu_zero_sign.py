@@ -397,3 +397,48 @@ def test_full_reduction_pick(gpu, dt, dens, kind):
             act.method = kind
             _same_bytes(want, act[q], (q, resident))
         active_mod.release_resident(var)
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("kind", ["min", "max"])
+@pytest.mark.parametrize("dens", [0.5, 0.02])
+def test_walk_keyed_level1_sign(gpu, dt, kind, dens):
+    """The two-step path over a hyperslab whose edge chunks are cut boxes:
+    the column walk keys level 1 of NumPy's zero sign itself
+    (PYAS_REC_ZERO_SIGN, the last zero in row order wins) instead of
+    pyas_tie_chunks; dense and sparse zeros, min and max, against the
+    reference's combine over storage.py's results (sign bit included).  The
+    fused path must actually run for the column-layout axis sets, and with
+    the `out` calls elementwise pyas_combine_grid keys level 2 (the last zero
+    layer wins, PYAS_FOLD_ZERO_SIGN_*) so no tie pass runs.  The replay goes
+    through _CachedQuery's same two launches."""
+    if tie_rule(dt) is None:
+        pytest.skip("no NumPy tie rule derived on this host")
+    rng = np.random.default_rng(41 + int(dens * 100) + len(kind))
+    shape, chunks = (32, 48, 64), (16, 16, 32)
+    a = _chunk(rng, shape, np.dtype(dt), "min0" if kind == "min" else "max0", dens=dens, n_fill=10)
+    attrs = {"_FillValue": np.array([-999.0], dtype=dt)}
+    missing = (np.dtype(dt).type(-999.0), None, None, None)
+    var, data = _variable(a, chunks, attrs)
+    data_of = lambda cc: data[var.chunk_index[cc][0]: var.chunk_index[cc][0] + var.chunk_index[cc][1]]
+    q = (slice(1, 31), slice(1, 47), slice(1, 63))
+    old = active_mod._AXES_FOLD
+    active_mod._AXES_FOLD = False
+    try:
+        for axis in [(0,), (1,), (0, 1), (2,), (1, 2)]:
+            want = _reference_active(a, chunks, q, axis, kind, missing, data_of)
+            act = Active(var, axis=axis, resident=True)
+            act.method = kind
+            got = act[q]
+            _same_bytes(want, got, (q, axis))
+            act.method = kind
+            _same_bytes(want, act[q], (q, axis, "replay"))
+            plans = list(var._pyas_resident.get("plans", {}).values())
+            if 2 not in axis:   # innermost dim kept: the walk keyed level 1, the combine level 2
+                assert any(p.grid is not None and p.grid.get("zs1") for p in plans), axis
+                assert any(p.grid is not None and p.grid.get("zs2") for p in plans), axis
+            elif axis == (2,):   # LDS rows: each row one call, keyed by the walk
+                assert any(p.grid is not None and p.grid.get("zs1") for p in plans), axis
+            active_mod.release_resident(var)
+    finally:
+        active_mod._AXES_FOLD = old

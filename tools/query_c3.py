@@ -22,6 +22,9 @@ def main():
     ap.add_argument("name")
     ap.add_argument("which", type=int)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--zeros", type=float, default=0.0,
+                    help="fraction of elements set to +-0.0 (random signs; a zero-heavy field)")
+    ap.add_argument("--method", default=None, help="override the query's method (e.g. min)")
     a = ap.parse_args()
     import torch
     from pyactivestorage_amd.active import Active, attach_resident, release_resident
@@ -32,16 +35,31 @@ def main():
     shape, chunks = cfg["shape"], cfg["chunks"]
     dev = torch.device("cuda", 0)
     data, offsets, _ = chunk_major_device(torch, shape, chunks, dt, dev, fill=bench.FILL, fill_frac=0.01, seed=0)
+    if a.zeros > 0:   # values in [1, 1000) with a fraction of +-0.0, on the device
+        v = data.view(torch.float32)
+        g = torch.Generator(device="cuda")
+        g.manual_seed(1)
+        step = 1 << 26
+        for i in range(0, v.numel(), step):
+            part = v[i:i + step]
+            u = torch.rand(part.numel(), generator=g, device="cuda")
+            sg = torch.rand(part.numel(), generator=g, device="cuda") < 0.5
+            vals = 1.0 + torch.rand(part.numel(), generator=g, device="cuda") * 999.0
+            z = torch.where(sg, torch.tensor(-0.0, device="cuda"), torch.tensor(0.0, device="cuda"))
+            part.copy_(torch.where(u < a.zeros, z, vals))
     torch.cuda.synchronize()
     grid = [s // c for s, c in zip(shape, chunks)]
     cb = int(np.prod(chunks)) * dt.itemsize
     index = {co: (int(offsets[k]), cb) for k, co in enumerate(np.ndindex(*grid))}
     attrs = {"_FillValue": np.array([bench.FILL], dtype=dt), "valid_min": np.array([bench.VMIN], dtype=dt),
              "valid_max": np.array([bench.VMAX], dtype=dt)}
+    if a.zeros > 0:   # the zero-heavy field: _FillValue only (bench_zeros.py's variable)
+        attrs = {"_FillValue": np.array([bench.FILL], dtype=dt)}
     var = ChunkedVariable(name="q", shape=shape, chunks=chunks, dtype=dt, chunk_index=index, attrs=attrs,
                           filename=None, filter_pipeline=None)
     attach_resident(var, data.data_ptr(), device=0, owner=data)
     label, mk, axis, method = bench.ACTIVE_EXTRAS[a.name][a.which]
+    method = a.method or method
     ix = mk()
     act = Active(var, resident=True)
     times = []
@@ -52,7 +70,7 @@ def main():
         act[ix]
         times.append(time.perf_counter() - t0)
     times = times[2:]
-    print(json.dumps({"query": label, "axis": axis, "method": method,
+    print(json.dumps({"query": label, "axis": axis, "method": method, "zeros": a.zeros,
                       "ms_median": round(float(np.median(times)) * 1e3, 4),
                       "ms_min": round(min(times) * 1e3, 4)}), flush=True)
     release_resident(var)
