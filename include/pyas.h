@@ -300,9 +300,12 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch,
 #define PYAS_TIE_REC 4u    /* which: parts are PYAS_REC_MIN (which 1) / _MAX (which 2) records */
 /* OR'ed into pyas_reduce_axes_ex's rec (PYAS_REC_MIN / PYAS_REC_MAX of a
  * float variable): the per-chunk walk writes NumPy's sign of a zero min/max
- * itself (storage.py:99-100; valid when the innermost chunk dim is kept: the
- * calls are elementwise and the last zero wins), so pyas_tie_chunks need
- * not run.  The caller promises every chunk is whole or a unit-step box
+ * itself (storage.py:99-100), so pyas_tie_chunks need not run.  Column
+ * layout (innermost chunk dim kept): the calls are elementwise and the last
+ * zero wins.  LDS row layout (innermost dim reduced, rows <= 64 elements, the
+ * reduced group that dim alone when chunks are cut): each row is one
+ * contiguous call, keyed with the context's tie rule
+ * (pyas_ctx_set_tie_rule).  The caller promises every chunk is whole or a unit-step box
  * covering at least half the chunk with more than one index in the
  * innermost dim; PYAS_ENOTSUP when the launch cannot key the sign (another
  * layout, no tie rule, cut chunks it would not take). */

@@ -1311,28 +1311,36 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
     const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (f >= n_out) return;
     const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
-    int64_t a[PYAS_MAX_DIMS], gstride[PYAS_MAX_DIMS];
-    int64_t j = 0, jstride = 1, rest = f, st = 1;
+    int64_t gstride[PYAS_MAX_DIMS];
+    int64_t j = 0, jstride = 1, st = 1, nk = 0;   // nk: the chunk position of the kept coordinates
+    // (outputs under 2^32 -- every practical grid -- decode f in 32-bit
+    // divisions: 64-bit ones are a long software sequence per kept dim)
+    const bool narrow = (uint64_t)n_out <= 0xFFFFFFFFull;
+    int64_t rest = f;
+    uint32_t rest32 = (uint32_t)f;
 #pragma unroll
     for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-        a[d] = 0;
         gstride[d] = st;
         if (d < g.ndim) {
-            st *= g.n_coords[d];
             if (!((g.axes_mask >> d) & 1u)) {
-                const int64_t e = g.out_extent[d];
-                const int64_t p = rest % e;
-                rest /= e;
-                a[d] = g.pos_coord[d][p];
+                int64_t p;
+                if (narrow) {
+                    const uint32_t e = (uint32_t)g.out_extent[d], q = rest32 / e;
+                    p = rest32 - q * e;
+                    rest32 = q;
+                } else {
+                    const int64_t e = g.out_extent[d];
+                    p = rest % e;
+                    rest /= e;
+                }
+                const int64_t ad = g.pos_coord[d][p];
+                nk += ad * st;
                 j += (int64_t)g.pos_local[d][p] * jstride;
-                jstride *= g.coord_count[d][a[d]];
+                jstride *= g.coord_count[d][ad];
             }
+            st *= g.n_coords[d];
         }
     }
-    int64_t nk = 0;   // chunk position from the kept coordinates
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-        if (d < g.ndim && !((g.axes_mask >> d) & 1u)) nk += a[d] * gstride[d];
     // Layers in C order over the reduced dims: a radix counter walks the
     // chunk positions (no division per layer), and U layers' offset and
     // partial loads are issued before they are merged (in the same order, so
@@ -2814,6 +2822,9 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
             const T v = a.zs == 1 ? acc.mn : acc.mx;
             const bool zrow = o0 + r < d.KO && cnt > 0 && !nan && v == (T)0;   // the row's H lanes agree
             if (__ballot(zrow)) {
+                // re-read the tile: keeping the fold's LDS reads live for this
+                // rare pass would cost the main loop registers (occupancy)
+                wave_sync_lds();
                 uint64_t Z = 0;
                 if (zrow) {
                     // the lane's zero bits shifted in (its first element ends
