@@ -732,11 +732,15 @@ __device__ __forceinline__ bool span_plan(const ReduceArgs &a, const uint8_t *ba
 // a carry out of that dim (every cnt[kk-1] spans) walks the outer digits.
 // (A block-strided walk advanced every digit with a carry chain per item:
 // ~40 VALU ops per 16-B group, C3 [1:1023]^3's cut chunks at 39 % of 8 TB/s.)
+constexpr int kSpanPool = 512;   // index-list entries run_spans copies to LDS
 struct SpanWalk {
     int32_t ix[PYAS_MAX_DIMS];   // digits of the dims < last
     int32_t xl;                  // digit of the last span dim
     int32_t mem;                 // element offset of this lane's group in the current span
-    __device__ __forceinline__ void init(const ReduceArgs &a, const Sel &s, int kk, int64_t q, int32_t gofs) {
+    // lp: the last span dim's index list (its first entry at lp[0]; an LDS
+    // copy, run_spans), unused when that dim is a slice
+    __device__ __forceinline__ void init(const ReduceArgs &a, const Sel &s, int kk, int64_t q, int32_t gofs,
+                                         const int32_t *lp) {
         uint32_t r = (uint32_t)q;
         int32_t m = gofs;
         xl = 0;
@@ -747,29 +751,30 @@ struct SpanWalk {
                 const uint32_t c = (uint32_t)s.cnt[d], qq = r / c;
                 const int32_t dig = (int32_t)(r - qq * c);
                 r = qq;
-                m += (int32_t)sel_index(s, a.pool, d, dig) * (int32_t)a.cstride[d];
+                const int32_t idx = (d == kk - 1 && s.step[d] == 0) ? lp[dig] : (int32_t)sel_index(s, a.pool, d, dig);
+                m += idx * (int32_t)a.cstride[d];
                 if (d == kk - 1) xl = dig;
                 else ix[d] = dig;
             }
         }
         mem = m;
     }
-    // one more span along the last span dim; an index list there costs a
-    // pool read per span
-    __device__ __forceinline__ void next(const ReduceArgs &a, const Sel &s, int kk) {
-        int32_t cl = 1, st = 0, sk = 0, cs = 0;
+    // one more span along the last span dim; an index list there costs an
+    // LDS read per span
+    __device__ __forceinline__ void next(const ReduceArgs &a, const Sel &s, int kk, const int32_t *lp) {
+        int32_t cl = 1, sk = 0, cs = 0;
 #pragma unroll
         for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-            if (d == kk - 1) { cl = s.cnt[d]; st = s.start[d]; sk = s.step[d]; cs = (int32_t)a.cstride[d]; }
+            if (d == kk - 1) { cl = s.cnt[d]; sk = s.step[d]; cs = (int32_t)a.cstride[d]; }
         const int32_t x0 = xl;
         if (__builtin_expect(++xl < cl, 1)) {
-            mem += sk != 0 ? sk * cs : (a.pool[st + xl] - a.pool[st + x0]) * cs;
+            mem += sk != 0 ? sk * cs : (lp[xl] - lp[x0]) * cs;
             return;
         }
         // carry into the outer span dims (rare; slices or single indices,
         // span_plan's rule: affine in the digits)
         xl = 0;
-        mem -= sk != 0 ? x0 * sk * cs : (a.pool[st + x0] - a.pool[st]) * cs;
+        mem -= sk != 0 ? x0 * sk * cs : (lp[x0] - lp[0]) * cs;
         bool carry = true;
 #pragma unroll
         for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
@@ -813,10 +818,30 @@ __device__ void run_spans(const ReduceArgs &a, const uint8_t *base, const Sel &s
     const int64_t M = (q1 - q0 + sp.P - 1) / sp.P;   // spans per lane group
     const int64_t qa = q0 + (int64_t)p * M;
     const int64_t qb = qa + M < q1 ? qa + M : q1;
+    const int kk = sp.kk;
+    // an index list as the last span dim: its entries copied to LDS once,
+    // so a span's address never waits on a global pool read (C3 [:, list64,
+    // :] walked 256 spans per chunk, two dependent global reads each: 20 %)
+    __shared__ int32_t spool[kSpanPool];
+    const int32_t *lp = spool;
+    {
+        int32_t lst = 0, lsk = 1, lcnt = 0;
+#pragma unroll
+        for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+            if (d == kk - 1) { lst = s.start[d]; lsk = s.step[d]; lcnt = s.cnt[d]; }
+        if (lsk == 0) {   // block-uniform
+            if (lcnt <= kSpanPool) {
+                __syncthreads();   // a previous tile's walk may still read it
+                for (int i = tid; i < lcnt; i += kBlock) spool[i] = a.pool[lst + i];
+                __syncthreads();
+            } else {
+                lp = a.pool + lst;
+            }
+        }
+    }
     SpanWalk w;
     // span-independent part of a group's address (elements; may be -off < 0)
-    w.init(a, s, sp.kk, qa < q1 ? qa : q0, j * NU - sp.off + sp.m_in);
-    const int kk = sp.kk;
+    w.init(a, s, kk, qa < q1 ? qa : q0, j * NU - sp.off + sp.m_in, lp);
     // groups in flight per lane: 4, or 8 plain vectors' worth when shuffled
     // (f64: one group = 8 vectors; 4 of them took k_reduce_u to ~300 VGPRs)
 #ifndef PYAS_SPANS_U
@@ -838,7 +863,7 @@ __device__ void run_spans(const ReduceArgs &a, const uint8_t *base, const Sel &s
                 } else {
                     r[u][0] = ldg16(reinterpret_cast<const uint4 *>(base + (int64_t)w.mem * ES));
                 }
-                if (q + 1 < qb) w.next(a, s, kk);
+                if (q + 1 < qb) w.next(a, s, kk, lp);
             }
             ++q;
         }
@@ -1208,8 +1233,12 @@ __device__ __forceinline__ void reduce_body(const ReduceArgs &a) {
     if (a.spans && total > 0 && !sel_contiguous(a, s, &m0s)) {
         SpanPlan sp;
         if (span_plan<T, SHUF>(a, base, s, sp) && (a.spans == 2 || !rows_aligned<T, SHUF>(a, base, s, &ks, &Ls))) {
+            // (tiles sized by the bytes the spans read instead -- fewer, longer
+            // lane-group walks -- measured slower: C3 [:, list64, :] 21 -> 12 %,
+            // [:, 0:1024:3, :] 61 -> 41 % of 8 TB/s; the walk is latency-bound)
             const int64_t per = (sp.nspans + a.tpc - 1) / a.tpc;
-            const int64_t q0 = t * per, q1 = q0 + per < sp.nspans ? q0 + per : sp.nspans;
+            const int64_t q0 = t * per < sp.nspans ? t * per : sp.nspans;
+            const int64_t q1 = q0 + per < sp.nspans ? q0 + per : sp.nspans;
             if (q0 < q1) run_spans<T, SHUF, BSWAP, MASKED>(a, base, s, sp, q0, q1, acc, mk);
             tile_finish(acc, (!MASKED && q0 < q1) ? (uint64_t)((q1 - q0) * sp.per_span) : 0u, tout);
             return;
@@ -1302,12 +1331,41 @@ __global__ __launch_bounds__(kBlock) void k_combine_segments(const pyas_partial 
     store_wpartial(out + sidx, acc);
 }
 
+constexpr int kCombineLayerTab = 2048;   // k_combine_grid: layers whose offsets fit its LDS table
 // box-query combine (pyas_combine_grid): one thread per final output element,
 // chunk layers folded in C order of the reduced dims' coordinates
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in, pyas_grid g,
                                                          int64_t n_out, int64_t n_layers,
                                                          uint32_t flags, pyas_partial *out) {
+    // the layers' chunk-position offsets from the column's first chunk (the
+    // same for every output): one table per workgroup in LDS, so a layer
+    // costs one LDS read instead of a radix step over 8 dims in 64-bit
+    // (C3 [1:1023]^3 (0,): 1M outputs x 16 layers)
+    __shared__ int32_t s_lofs[kCombineLayerTab];
+    int64_t n_grid = 1;
+#pragma unroll
+    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
+        if (d < g.ndim) n_grid *= g.n_coords[d];
+    const bool tab = n_layers <= kCombineLayerTab && n_grid < (int64_t(1) << 31);
+    if (tab) {
+        for (int64_t l = threadIdx.x; l < n_layers; l += kBlock) {
+            int64_t rr = l, o = 0, stt = 1;
+#pragma unroll
+            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+                if (d < g.ndim) {
+                    if ((g.axes_mask >> d) & 1u) {
+                        const int64_t q = rr / g.n_coords[d];
+                        o += (rr - q * g.n_coords[d]) * stt;
+                        rr = q;
+                    }
+                    stt *= g.n_coords[d];
+                }
+            }
+            s_lofs[l] = (int32_t)o;
+        }
+        __syncthreads();
+    }
     const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (f >= n_out) return;
     const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
@@ -1362,7 +1420,9 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             off[u] = 0;
-            if (l0 + u < n_layers) {
+            if (tab) {
+                if (l0 + u < n_layers) off[u] = g.chunk_out_offsets[nk + s_lofs[l0 + u]];
+            } else if (l0 + u < n_layers) {
                 off[u] = g.chunk_out_offsets[n];
                 bool carry = true;
 #pragma unroll
@@ -2800,9 +2860,19 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
         TileAcc<T> acc;
         acc.init();
         const uint4 *row = t + r * kRowLdsStride + h * VH;
+        // ZT: the lane's zero bits, shifted in as the fold reads them (its
+        // first element ends up highest): two VALU ops per element, but no
+        // second pass over the tile holding registers next to the loads in
+        // flight (that pass cost the kernel a wave per SIMD: 1.28 ms vs 0.92)
+        using ZW = typename std::conditional<H == 1, uint64_t, uint32_t>::type;
+        ZW zl = 0;
         for (int i = 0; i < VH; ++i) {
             T x[N];
             unpack16<T, BSWAP>(row[i], x);
+            if constexpr (ZT) {
+#pragma unroll
+                for (int k = 0; k < N; ++k) zl = (ZW)((zl << 1) | (x[k] == (T)0 ? 1u : 0u));
+            }
             if constexpr (CUT) {   // the run's elements inside the box (RO == 1: position = element)
                 const uint32_t b = (uint32_t)(lbits >> (i * N)) & (uint32_t)((1ull << N) - 1);
                 if (acc.template add_pred<N, MASKED, 1>(x, b, mk)) {
@@ -2822,21 +2892,8 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
             const T v = a.zs == 1 ? acc.mn : acc.mx;
             const bool zrow = o0 + r < d.KO && cnt > 0 && !nan && v == (T)0;   // the row's H lanes agree
             if (__ballot(zrow)) {
-                // re-read the tile: keeping the fold's LDS reads live for this
-                // rare pass would cost the main loop registers (occupancy)
-                wave_sync_lds();
                 uint64_t Z = 0;
-                if (zrow) {
-                    // the lane's zero bits shifted in (its first element ends
-                    // up highest), then reversed to element order at its offset
-                    using ZW = typename std::conditional<H == 1, uint64_t, uint32_t>::type;
-                    ZW zl = 0;
-                    for (int i = 0; i < VH; ++i) {
-                        T xe[N];
-                        unpack16<T, BSWAP>(row[i], xe);
-#pragma unroll
-                        for (int k = 0; k < N; ++k) zl = (ZW)((zl << 1) | (xe[k] == (T)0 ? 1u : 0u));
-                    }
+                if (zrow) {   // the lane's zero bits reversed to element order at its offset
                     const int J = VH * N;
                     if constexpr (H == 1) Z = __builtin_bitreverse64(zl) >> (64 - J);
                     else Z = (uint64_t)(__builtin_bitreverse32(zl) >> (32 - J)) << (h * J);
@@ -3020,7 +3077,7 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_COL_WAVES) void k_axes_dens
     axes_dense_body<T, SHUF, BSWAP, MASKED, MODE, true, true>(a);
 }
 #ifndef PYAS_LDS_ZS_WAVES
-#define PYAS_LDS_ZS_WAVES 3   // at 4 the row keying spilled 256 B per lane (C3 [1:1023]^3 (2,) min 1.75 ms)
+#define PYAS_LDS_ZS_WAVES 4   // the row kernel is latency-bound: 3 waves cost C3 [1:1023]^3 (2,) min 0.92 -> 1.28 ms
 #endif
 template <typename T, bool SHUF, bool BSWAP, int MASKED, int MODE>
 __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_LDS_ZS_WAVES) void k_axes_dense_lds_zs(AxesArgs a) {

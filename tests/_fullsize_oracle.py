@@ -37,13 +37,22 @@ def main(name):
     from pyactivestorage_amd.device import get_context
     from pyactivestorage_amd.synthetic import chunk_major_device
 
+    # "c4u" / "c5u": the same configs without valid_max, so every chunk
+    # holds data and the sums run over full-magnitude values: chunks spread
+    # evenly over the whole grid (the masked configs' data sits in the first
+    # chunk column along dim 2 only)
+    unmasked = name.endswith("u")
+    name = name[:-1] if unmasked else name
     cfg = bench.CONFIGS[name]
     dt = np.dtype(cfg["dtype"])
     shape, chunks = cfg["shape"], cfg["chunks"]
     grid = [s // c for s, c in zip(shape, chunks)]
+    n_grid = int(np.prod(grid))
+    if unmasked:
+        ids = sorted({int(x) for x in np.linspace(0, n_grid - 1, 64 if name == "c4" else 256)})
     # valid_max (5e8) masks every chunk beyond the first chunk columns along
     # dim 2 (values i + j*n + k*n^2): sample the chunks that hold data
-    if name == "c4":   # 64 chunks with chunk coordinate 0 along dim 2
+    elif name == "c4":   # 64 chunks with chunk coordinate 0 along dim 2
         ids = [c for c in range(0, 1024) if c % grid[2] == 0]
     else:              # 256 chunks with coordinate 0 along dim 2, in the first four layers
         ids = [c for c in range(0, 8192) if c % grid[2] == 0]
@@ -51,7 +60,7 @@ def main(name):
     dev = torch.device("cuda", 0)
     ctx = get_context(0)
     st = torch.cuda.current_stream().cuda_stream
-    missing = (dt.type(bench.FILL), None, dt.type(bench.VMIN), dt.type(bench.VMAX))
+    missing = (dt.type(bench.FILL), None, dt.type(bench.VMIN), None if unmasked else dt.type(bench.VMAX))
     filters = [ref.Shuffle(dt.itemsize)] if cfg["shuffle"] else None
     n_checked = n_partial = 0
     for ids in ranges:
@@ -121,6 +130,7 @@ def main(name):
         del data, plan
         torch.cuda.empty_cache()
     assert n_checked >= (64 if name == "c4" else 256), n_checked
+    name += "u" if unmasked else ""
     print(f"fullsize-oracle {name} OK: {n_checked} chunks with data vs storage.reduce_chunk "
           f"({n_partial} partially selected), combine over {sum(len(r) for r in ranges)} chunks")
 

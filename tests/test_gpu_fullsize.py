@@ -39,11 +39,13 @@ def test_full_size_config(gpu, name):
     print(r.stdout.strip())
 
 
-@pytest.mark.parametrize("name", ["c4", "c5"])
+@pytest.mark.parametrize("name", ["c4", "c5", "c4u", "c5u"])
 def test_full_size_samples_against_oracle(gpu, name):
     """Real-size chunks of C4 (64 x 128^3 f32, shuffled, masked) and C5 (256 x
     32^3 f64, boundary-heavy hyperslab) against the oracle's storage.py and
-    _from_storage combine (tests/_fullsize_oracle.py, fresh process)."""
+    _from_storage combine (tests/_fullsize_oracle.py, fresh process); "u":
+    the same configs without valid_max, chunks spread over the whole grid,
+    so the sums at scale run over every element."""
     r = subprocess.run([sys.executable, "-u", "-m", "tests._fullsize_oracle", name], cwd=ROOT,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, f"{name}: rc={r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-4000:]}"
