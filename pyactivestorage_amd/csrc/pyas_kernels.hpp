@@ -2860,19 +2860,18 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
         TileAcc<T> acc;
         acc.init();
         const uint4 *row = t + r * kRowLdsStride + h * VH;
-        // ZT: the lane's zero bits, shifted in as the fold reads them (its
-        // first element ends up highest): two VALU ops per element, but no
-        // second pass over the tile holding registers next to the loads in
-        // flight (that pass cost the kernel a wave per SIMD: 1.28 ms vs 0.92)
+        // ZT: the lane's zero bits (its first element highest), gathered as
+        // the fold reads the tile -- a second pass over the tile held
+        // registers next to the loads in flight (a wave per SIMD: 1.28 ms vs
+        // 0.92) -- and only for vectors after which the lane's running
+        // min/max is exactly zero: before that every element was of one sign
+        // (no zero), and once it is past zero the row is not a zero row.
+        // Zero-free rows pay a compare and a branch per vector.
         using ZW = typename std::conditional<H == 1, uint64_t, uint32_t>::type;
         ZW zl = 0;
         for (int i = 0; i < VH; ++i) {
             T x[N];
             unpack16<T, BSWAP>(row[i], x);
-            if constexpr (ZT) {
-#pragma unroll
-                for (int k = 0; k < N; ++k) zl = (ZW)((zl << 1) | (x[k] == (T)0 ? 1u : 0u));
-            }
             if constexpr (CUT) {   // the run's elements inside the box (RO == 1: position = element)
                 const uint32_t b = (uint32_t)(lbits >> (i * N)) & (uint32_t)((1ull << N) - 1);
                 if (acc.template add_pred<N, MASKED, 1>(x, b, mk)) {
@@ -2882,6 +2881,15 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
                 }
             } else {
                 acc.template add_n<N, MASKED, false>(x, mk);
+            }
+            if constexpr (ZT) {
+                const T ext = a.zs == 1 ? acc.mn : acc.mx;
+                if (ext == (T)0) {
+                    uint32_t b = 0;
+#pragma unroll
+                    for (int k = 0; k < N; ++k) b |= (x[k] == (T)0 ? 1u : 0u) << (N - 1 - k);
+                    zl |= (ZW)b << (VH * N - N * (i + 1));
+                }
             }
         }
         if constexpr (!MASKED && !CUT) acc.count += (uint32_t)(VH * N);
@@ -3991,8 +3999,6 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
     mk.init(r.mask);
     const bool round = (g.flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
     const int V = (int)(d.RI / N), VH = V / H;
-    // ZS: the row's first vector holding a remainder position (V: none)
-    const int vrem = ZS && g.zrow_rem ? (int)(__builtin_ctzll(g.zrow_rem) / N) : V;
     const int lane = threadIdx.x & (kWave - 1), rw = lane / H, h = lane - rw * H;
     uint4 *t = tile + (threadIdx.x / kWave) * RPW * kRowLdsStride;
     const int64_t wave = j * (kBlock / kWave) + threadIdx.x / kWave;
@@ -4038,10 +4044,27 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
             TileAcc<T> acc;
             acc.init();
             const uint4 *row = t + rw * kRowLdsStride + h * VH;
+            // ZS: the lane's zero bits (its first element highest), gathered
+            // only for vectors after which its running min/max is exactly
+            // zero (before, no zero was read; past zero, not a zero row):
+            // zero-free rows pay a compare and a branch per vector.  (The
+            // whole mask built unconditionally cost every min/max query 21 %;
+            // re-reading the tile for zero rows cost 2 %-zero data +29 %.)
+            using ZW = typename std::conditional<H == 1, uint64_t, uint32_t>::type;
+            ZW zl = 0;
             for (int i = 0; i < VH; ++i) {
                 T x[N];
                 unpack16<T, BSWAP>(row[i], x);
                 acc.template add_n<N, MASKED, false>(x, mk);
+                if constexpr (ZS) {
+                    const T ext = (g.zs & 1u) ? acc.mn : acc.mx;
+                    if (ext == (T)0) {
+                        uint32_t b = 0;
+#pragma unroll
+                        for (int k = 0; k < N; ++k) b |= (x[k] == (T)0 ? 1u : 0u) << (N - 1 - k);
+                        zl |= (ZW)b << (VH * N - N * (i + 1));
+                    }
+                }
             }
             if constexpr (!MASKED) acc.count += (uint32_t)(VH * N);
             uint32_t cnt, nan;
@@ -4056,52 +4079,25 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
                 if (__ballot(zrow)) {
                     const uint4 *trow = t + rw * kRowLdsStride;
                     int e = -1;
+                    // the row's zero mask Z (lane h: its VH vectors, reversed
+                    // to element order at its offset), then: the last
+                    // remainder zero, if any, wins (K1; W is never later);
+                    // else the later of the last seed/top-lane zero (K1) and,
+                    // unless the seed is a zero, the last zero of the lowest
+                    // lane-rank class holding one (W)
+                    uint64_t Z = 0;
                     if (zrow) {
-                        // the last remainder zero, if any, wins (K1; W is never
-                        // later): lane h reads remainder vectors vlo + h, + H, ...
-                        int er = -1;
-                        for (int vi = vrem + h; vi < V; vi += H) {
-                            T xe[N];
-                            unpack16<T, BSWAP>(trow[vi], xe);
-                            uint32_t m4 = 0;
-#pragma unroll
-                            for (int k = 0; k < N; ++k) m4 |= (xe[k] == (T)0 ? 1u : 0u) << k;
-                            m4 &= (uint32_t)(g.zrow_rem >> (vi * N)) & ((1u << N) - 1u);
-                            if (m4) er = vi * N + (31 - __builtin_clz(m4));
-                        }
-#pragma unroll
-                        for (int mm = H / 2; mm >= 1; mm >>= 1) {
-                            const int o = __shfl_xor(er, mm);
-                            er = o > er ? o : er;
-                        }
-                        e = er;
+                        const int J = VH * N;
+                        if constexpr (H == 1) Z = __builtin_bitreverse64(zl) >> (64 - J);
+                        else Z = (uint64_t)(__builtin_bitreverse32(zl) >> (32 - J)) << (h * J);
                     }
-                    // no remainder zero: the row's zero mask Z (lane h: its VH
-                    // vectors), then the later of the last seed/top-lane zero
-                    // (K1) and, unless the seed is a zero, the last zero of the
-                    // lowest lane-rank class holding one (W)
-                    const bool slow = zrow && e < 0;
-                    if (__ballot(slow)) {
-                        uint64_t Z = 0;
-                        if (slow) {
-                            // the lane's zero bits shifted in (its first element
-                            // ends up highest), then reversed to element order at
-                            // the lane's offset: one shift-or per element
-                            using ZT = typename std::conditional<H == 1, uint64_t, uint32_t>::type;
-                            ZT zl = 0;
-                            for (int i = 0; i < VH; ++i) {
-                                T xe[N];
-                                unpack16<T, BSWAP>(row[i], xe);
 #pragma unroll
-                                for (int k = 0; k < N; ++k) zl = (ZT)((zl << 1) | (xe[k] == (T)0 ? 1u : 0u));
-                            }
-                            const int J = VH * N;
-                            if constexpr (H == 1) Z = __builtin_bitreverse64(zl) >> (64 - J);
-                            else Z = (uint64_t)(__builtin_bitreverse32(zl) >> (32 - J)) << (h * J);
-                        }
-#pragma unroll
-                        for (int mm = H / 2; mm >= 1; mm >>= 1) Z |= shfl_xor(Z, mm);
-                        if (slow && h == 0 && Z) {
+                    for (int mm = H / 2; mm >= 1; mm >>= 1) Z |= shfl_xor(Z, mm);
+                    if (zrow && h == 0 && Z) {
+                        const uint64_t zr = Z & g.zrow_rem;
+                        if (zr) {
+                            e = msb64(zr);
+                        } else {
                             const uint64_t sig = Z & (g.zrow_top | 1u);
                             const int e1 = sig ? msb64(sig) : -1;
                             int ew = -1;
@@ -4112,11 +4108,11 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
                                     // the lane classes holding a zero (bit j: lane j),
                                     // through the rank tables: the lowest rank's class
                                     uint32_t C = 0;
-                                    for (int b = 0; 1 + b * L < 64; ++b)
-                                        C |= (uint32_t)(Zv >> (1 + b * L)) & ((1u << L) - 1u);
+                                    for (int bb = 0; 1 + bb * L < 64; ++bb)
+                                        C |= (uint32_t)(Zv >> (1 + bb * L)) & ((1u << L) - 1u);
                                     const uint32_t P = (uint32_t)s_pt[C & 0xFFu] | (uint32_t)s_pt[256 + (C >> 8)];
-                                    const int j = s_ord[__builtin_ctz(P)];
-                                    ew = msb64(Zv & (g.zrow_rep << (1 + j)));
+                                    const int jj = s_ord[__builtin_ctz(P)];
+                                    ew = msb64(Zv & (g.zrow_rep << (1 + jj)));
                                 } else {
                                     for (int rk = 0; rk < L; ++rk) {
                                         const uint64_t cz = Z & g.zrow_cm[rk];
