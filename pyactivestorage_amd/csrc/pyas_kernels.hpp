@@ -947,25 +947,14 @@ __device__ __forceinline__ uint4 rec_of(const pyas_partial &p, int rec) {
     return r;
 }
 
-// Entry i of a partial array of form `rec` as a pyas_partial (the fields a
-// record does not carry are 0: neutral for the method that reads it).
+// A <= 4-byte type's record (value word, count word) as a pyas_partial.
 template <typename T>
-__device__ __forceinline__ pyas_partial part_at(const void *base, int64_t i, int rec) {
-    if (rec == 0) return reinterpret_cast<const pyas_partial *>(base)[i];
+__device__ __forceinline__ pyas_partial part_raw(uint2 r, int rec) {
+    static_assert(sizeof(T) <= 4, "8-byte records are 16 B");
     pyas_partial p;
-    p.sum.u = 0;
-    p.min.u = 0;
-    p.max.u = 0;
     T v;
-    if constexpr (sizeof(T) <= 4) {
-        const uint2 r = reinterpret_cast<const uint2 *>(base)[i];
-        __builtin_memcpy(&v, &r.x, sizeof(T));
-        p.count = (int64_t)(int32_t)r.y;
-    } else {
-        const uint4 r = reinterpret_cast<const uint4 *>(base)[i];
-        __builtin_memcpy(&v, &r.x, 8);
-        p.count = (int64_t)(int32_t)r.z;
-    }
+    __builtin_memcpy(&v, &r.x, sizeof(T));
+    p.count = (int64_t)(int32_t)r.y;
     pyas_scalar sv, mv;
     if constexpr (TT<T>::kind == 0) sv.f = (double)v;
     else if constexpr (TT<T>::kind == 1) sv.i = (int64_t)v;
@@ -975,6 +964,31 @@ __device__ __forceinline__ pyas_partial part_at(const void *base, int64_t i, int
     p.min.u = rec == PYAS_REC_MIN ? mv.u : 0u;
     p.max.u = rec == PYAS_REC_MAX ? mv.u : 0u;
     return p;
+}
+
+// Entry i of a partial array of form `rec` as a pyas_partial (the fields a
+// record does not carry are 0: neutral for the method that reads it).
+template <typename T>
+__device__ __forceinline__ pyas_partial part_at(const void *base, int64_t i, int rec) {
+    if (rec == 0) return reinterpret_cast<const pyas_partial *>(base)[i];
+    if constexpr (sizeof(T) <= 4) {
+        return part_raw<T>(reinterpret_cast<const uint2 *>(base)[i], rec);
+    } else {
+        pyas_partial p;
+        T v;
+        const uint4 r = reinterpret_cast<const uint4 *>(base)[i];
+        __builtin_memcpy(&v, &r.x, 8);
+        p.count = (int64_t)(int32_t)r.z;
+        pyas_scalar sv, mv;
+        if constexpr (TT<T>::kind == 0) sv.f = (double)v;
+        else if constexpr (TT<T>::kind == 1) sv.i = (int64_t)v;
+        else sv.u = (uint64_t)v;
+        TT<T>::put(mv, v);
+        p.sum.u = rec == PYAS_REC_SUM ? sv.u : 0u;
+        p.min.u = rec == PYAS_REC_MIN ? mv.u : 0u;
+        p.max.u = rec == PYAS_REC_MAX ? mv.u : 0u;
+        return p;
+    }
 }
 
 // Output o of the per-chunk partial-axis kernels in the caller's form
@@ -1331,41 +1345,12 @@ __global__ __launch_bounds__(kBlock) void k_combine_segments(const pyas_partial 
     store_wpartial(out + sidx, acc);
 }
 
-constexpr int kCombineLayerTab = 2048;   // k_combine_grid: layers whose offsets fit its LDS table
 // box-query combine (pyas_combine_grid): one thread per final output element,
 // chunk layers folded in C order of the reduced dims' coordinates
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in, pyas_grid g,
                                                          int64_t n_out, int64_t n_layers,
                                                          uint32_t flags, pyas_partial *out) {
-    // the layers' chunk-position offsets from the column's first chunk (the
-    // same for every output): one table per workgroup in LDS, so a layer
-    // costs one LDS read instead of a radix step over 8 dims in 64-bit
-    // (C3 [1:1023]^3 (0,): 1M outputs x 16 layers)
-    __shared__ int32_t s_lofs[kCombineLayerTab];
-    int64_t n_grid = 1;
-#pragma unroll
-    for (int d = 0; d < PYAS_MAX_DIMS; ++d)
-        if (d < g.ndim) n_grid *= g.n_coords[d];
-    const bool tab = n_layers <= kCombineLayerTab && n_grid < (int64_t(1) << 31);
-    if (tab) {
-        for (int64_t l = threadIdx.x; l < n_layers; l += kBlock) {
-            int64_t rr = l, o = 0, stt = 1;
-#pragma unroll
-            for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-                if (d < g.ndim) {
-                    if ((g.axes_mask >> d) & 1u) {
-                        const int64_t q = rr / g.n_coords[d];
-                        o += (rr - q * g.n_coords[d]) * stt;
-                        rr = q;
-                    }
-                    stt *= g.n_coords[d];
-                }
-            }
-            s_lofs[l] = (int32_t)o;
-        }
-        __syncthreads();
-    }
     const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (f >= n_out) return;
     const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
@@ -1414,49 +1399,66 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
     // min (max) is a zero (elementwise `out` calls; the records carry level 1)
     const uint32_t zs = (flags >> 8) & 3u;
     bool zneg = false;
-    constexpr int U = 8;
-    for (int64_t l0 = 0; l0 < n_layers; l0 += U) {
-        int64_t off[U];
+    const int rec = (int)((flags >> 4) & 3u);
+    // U layers' offsets, then their U partials, in flight before the merges;
+    // compact records of <= 4-byte types (RAW) load as 8-B words, so 16
+    // layers fit the registers 8 full partials took
+    auto layers = [&](auto u_c, auto raw_c) {
+        constexpr int U = decltype(u_c)::value;
+        constexpr bool RAW = decltype(raw_c)::value;
+        for (int64_t l0 = 0; l0 < n_layers; l0 += U) {
+            int64_t off[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            off[u] = 0;
-            if (tab) {
-                if (l0 + u < n_layers) off[u] = g.chunk_out_offsets[nk + s_lofs[l0 + u]];
-            } else if (l0 + u < n_layers) {
-                off[u] = g.chunk_out_offsets[n];
-                bool carry = true;
+            for (int u = 0; u < U; ++u) {
+                off[u] = 0;
+                if (l0 + u < n_layers) {
+                    off[u] = g.chunk_out_offsets[n];
+                    bool carry = true;
 #pragma unroll
-                for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
-                    if (carry && d < g.ndim && ((g.axes_mask >> d) & 1u)) {
-                        n += gstride[d];
-                        if (++digit[d] == g.n_coords[d]) {
-                            digit[d] = 0;
-                            n -= g.n_coords[d] * gstride[d];
-                        } else {
-                            carry = false;
+                    for (int d = PYAS_MAX_DIMS - 1; d >= 0; --d) {
+                        if (carry && d < g.ndim && ((g.axes_mask >> d) & 1u)) {
+                            n += gstride[d];
+                            if (++digit[d] == g.n_coords[d]) {
+                                digit[d] = 0;
+                                n -= g.n_coords[d] * gstride[d];
+                            } else {
+                                carry = false;
+                            }
+                        }
+                    }
+                }
+            }
+            using LT = typename std::conditional<RAW, uint2, pyas_partial>::type;
+            LT ld[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (l0 + u < n_layers) {
+                    if constexpr (RAW) ld[u] = reinterpret_cast<const uint2 *>(in)[off[u] + j];
+                    else ld[u] = part_at<T>(in, off[u] + j, rec);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (l0 + u < n_layers) {
+                    pyas_partial pu;
+                    if constexpr (RAW) pu = part_raw<T>(ld[u], rec);
+                    else pu = ld[u];
+                    merge(acc, pu, round);
+                    if constexpr (TT<T>::kind == 0) {
+                        if (zs && pu.count > 0) {
+                            const double v = zs == 1 ? pu.min.f : pu.max.f;
+                            if (v == 0.0) zneg = __builtin_signbit(v) != 0;
                         }
                     }
                 }
             }
         }
-        pyas_partial p[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (l0 + u < n_layers) p[u] = part_at<T>(in, off[u] + j, (int)((flags >> 4) & 3u));
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (l0 + u < n_layers) merge(acc, p[u], round);
-        if constexpr (TT<T>::kind == 0) {
-            if (zs) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (l0 + u < n_layers && p[u].count > 0) {
-                        const double v = zs == 1 ? p[u].min.f : p[u].max.f;
-                        if (v == 0.0) zneg = __builtin_signbit(v) != 0;
-                    }
-                }
-            }
-        }
+    };
+    if constexpr (sizeof(T) <= 4) {
+        if (rec) layers(std::integral_constant<int, 16>(), std::true_type());
+        else layers(std::integral_constant<int, 8>(), std::false_type());
+    } else {
+        layers(std::integral_constant<int, 8>(), std::false_type());
     }
     if constexpr (TT<T>::kind == 0) {
         if (zs == 1 && acc.mn == (T)0) acc.mn = zneg ? (T)-0.0 : (T)0.0;
