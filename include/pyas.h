@@ -310,6 +310,13 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch,
  * innermost dim; PYAS_ENOTSUP when the launch cannot key the sign (another
  * layout, no tie rule, cut chunks it would not take). */
 #define PYAS_REC_ZERO_SIGN 0x100
+/* OR'ed into pyas_reduce_axes_ex's rec: the caller promises what
+ * PYAS_REC_ZERO_SIGN's caller promises (every chunk whole or a unit-step box
+ * covering at least half the chunk with more than one index in the innermost
+ * dim), so the generic per-element walk is not launched for the chunks the
+ * dense launch leaves (there are none).  A broken promise leaves those
+ * chunks' outputs unwritten. */
+#define PYAS_REC_DENSE_ONLY 0x200
 /* pyas_reduce_axes writing `rec` records (PYAS_REC_*; PYAS_REC_FULL is
  * pyas_reduce_axes itself): out[out_offsets[c] + o] in record units.  A
  * chunk's outputs must count < 2^31 elements each. */

@@ -773,7 +773,9 @@ class Active:
                 return True
             except NotImplementedError:
                 pass   # another layout: the scan pass keys the sign
-        engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf_ptr, parts_ptr, st, rec=prec)
+        # every chunk whole or a box the dense launch takes: no generic walk
+        dense = _lib.REC_DENSE_ONLY if prec and plan.dense_boxes() else 0
+        engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf_ptr, parts_ptr, st, rec=prec | dense)
         return False
 
     def _tie_grid(self, ctx, st, plan, rec, keys_ptr=None):

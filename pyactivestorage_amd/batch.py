@@ -102,16 +102,22 @@ class ReductionPlan:
         half of it with more than one index in its innermost dim: the chunks
         the dense per-chunk kernels walk themselves (pyas_kernels.hpp
         cut_eligible), the promise PYAS_REC_ZERO_SIGN needs."""
+        r = getattr(self, "_dense_boxes", None)   # fixed per plan; replays ask every query
+        if r is not None:
+            return r
         t = self.sel_table_host
         nd = len(self.chunk_shape)
         if self.chunk_shape[-1] < 2:
-            return False
-        if t is None:
-            return True
-        step, cnt = t[:, :nd, 1], t[:, :nd, 2].astype(np.int64)
-        ok = ((step == 1) | (cnt == 1)).all(axis=1) & (cnt >= 1).all(axis=1) & (cnt[:, nd - 1] > 1)
-        ok &= 2 * cnt.prod(axis=1) >= int(np.prod(self.chunk_shape))
-        return bool(ok.all())
+            r = False
+        elif t is None:
+            r = True
+        else:
+            step, cnt = t[:, :nd, 1], t[:, :nd, 2].astype(np.int64)
+            ok = ((step == 1) | (cnt == 1)).all(axis=1) & (cnt >= 1).all(axis=1) & (cnt[:, nd - 1] > 1)
+            ok &= 2 * cnt.prod(axis=1) >= int(np.prod(self.chunk_shape))
+            r = bool(ok.all())
+        self._dense_boxes = r
+        return r
 
     def tie_geom(self, order="C") -> _lib.TieGeom:
         """How NumPy walks these chunks' ``chunk[sel]`` after mask_missing

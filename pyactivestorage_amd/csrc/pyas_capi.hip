@@ -950,7 +950,10 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
                         void *stream) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     const bool want_zs = (rec & PYAS_REC_ZERO_SIGN) != 0;
-    rec &= ~PYAS_REC_ZERO_SIGN;
+    // PYAS_REC_DENSE_ONLY (and PYAS_REC_ZERO_SIGN, which makes the same
+    // promise): every chunk is whole or a box the dense launch takes
+    const bool dense_only = (rec & (PYAS_REC_DENSE_ONLY | PYAS_REC_ZERO_SIGN)) != 0;
+    rec &= ~(PYAS_REC_ZERO_SIGN | PYAS_REC_DENSE_ONLY);
     if (rec < PYAS_REC_FULL || rec > PYAS_REC_MAX) return fail(PYAS_EINVAL, "unknown record form %d", rec);
     pyas::AxesArgs x;
     std::memset(&x, 0, sizeof(x));
@@ -1126,11 +1129,12 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
         if (g >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
         PYAS_HIP(pyas::launch_axes_dense(batch->dtype, x, masked, g, (hipStream_t)stream));
     }
-    if (!x.d.mode || batch->sel) {
+    if (!x.d.mode || (batch->sel && !(dense_only && x.cuts))) {
         // with cut chunks in the dense launch, the generic kernel keeps only
         // boxes under half a chunk and non-box selections: one workgroup per
         // chunk (most of its workgroups only find their chunk taken; at 8 per
-        // chunk that empty launch cost C3 [1:1023]^3 (2,) 74 us)
+        // chunk that empty launch cost C3 [1:1023]^3 (2,) 74 us, at one 13 us;
+        // with the caller's PYAS_REC_DENSE_ONLY it is not launched)
         if (x.cuts) x.bpc = 1;
         const int64_t grid = batch->n_chunks * x.bpc;
         if (grid >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
