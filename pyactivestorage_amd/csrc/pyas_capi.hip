@@ -1057,6 +1057,15 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
         }
         x.zs = rec == PYAS_REC_MIN ? 1 : 2;
     }
+    // LDS row layout, whole chunks or the zero-sign kernel: two tiles per
+    // wave (C3 (2,) records 0.77-0.79 -> 0.73 ms, 4 tiles 0.74, 3 0.75;
+    // the cut kernel's slab (2,) mean measured slower at 2: 1.16 -> 1.23 ms,
+    // gpurun_out/r05/rowlds2); PYAS_ROW_LDS_TPW overrides both
+    if (x.d.mode >= 4 && (!batch->sel || x.zs) && !getenv("PYAS_ROW_LDS_TPW")) {
+        const int64_t per_pass = (pyas::kBlock / pyas::kWave) * (pyas::kWave / x.d.group);
+        const int64_t bpc = (x.d.KO + 2 * per_pass - 1) / (2 * per_pass);
+        x.d.bpc = bpc < 1 ? 1 : bpc;
+    }
     // Streamed column layout (k_axes_col_stream): every chunk whole, one
     // lane per item column (split 1), rows in whole 4-row groups; each
     // workgroup walks cpb chunks as one ring of loads.  Measured on C3
