@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--zeros", type=float, default=0.0,
                     help="fraction of elements set to +-0.0 (random signs; a zero-heavy field)")
     ap.add_argument("--method", default=None, help="override the query's method (e.g. min)")
+    ap.add_argument("--tile-bytes", type=int, default=0, help="pyas_ctx_set_tile_bytes (0: the default)")
     a = ap.parse_args()
     import torch
     from pyactivestorage_amd.active import Active, attach_resident, release_resident
@@ -58,6 +59,9 @@ def main():
     var = ChunkedVariable(name="q", shape=shape, chunks=chunks, dtype=dt, chunk_index=index, attrs=attrs,
                           filename=None, filter_pipeline=None)
     attach_resident(var, data.data_ptr(), device=0, owner=data)
+    if a.tile_bytes:
+        from pyactivestorage_amd.device import get_context
+        get_context(0).set_tile_bytes(a.tile_bytes)
     label, mk, axis, method = bench.ACTIVE_EXTRAS[a.name][a.which]
     method = a.method or method
     ix = mk()
