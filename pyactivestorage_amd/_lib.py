@@ -125,8 +125,8 @@ class TieRule(ctypes.Structure):
 
 # compact per-output records of pyas_reduce_axes_ex (pyas.h PYAS_REC_*)
 REC_FULL, REC_SUM, REC_MIN, REC_MAX = 0, 1, 2, 3
-REC_ZERO_SIGN = 0x100
-REC_DENSE_ONLY = 0x200   # pyas.h PYAS_REC_DENSE_ONLY   # pyas.h PYAS_REC_ZERO_SIGN: the per-chunk walk keys NumPy's zero sign
+REC_ZERO_SIGN = 0x100    # pyas.h PYAS_REC_ZERO_SIGN: the per-chunk walk keys NumPy's zero sign
+REC_DENSE_ONLY = 0x200   # pyas.h PYAS_REC_DENSE_ONLY: every chunk is dense-owned, no generic launch
 TIE_REC = 4
 
 

@@ -168,6 +168,15 @@ class _External:
         self.owner = None
 
 
+def _check_attached(variable, device) -> None:
+    """A caller-attached resident copy serves queries on its own device only
+    (replacing it would drop the caller's allocation behind their back)."""
+    store = getattr(variable, "_pyas_resident", None)
+    if store is not None and store["device"] != device and isinstance(store["buf"], _External):
+        raise ValueError(f"the variable's resident copy was attached on device {store['device']}, "
+                         f"not on this query's device {device} (attach_resident)")
+
+
 def attach_resident(variable, ptr, device: int = 0, owner=None) -> None:
     """Register chunks already decoded in HBM as ``variable``'s resident copy:
     ``ptr`` holds every chunk of the variable's grid in C order, one slot of
@@ -180,6 +189,8 @@ def attach_resident(variable, ptr, device: int = 0, owner=None) -> None:
     ds = variable
     if ds.filter_pipeline:
         raise NotImplementedError("attach_resident: variables with a filter pipeline")
+    if int(ptr) % _ALIGN:
+        raise ValueError(f"attach_resident: ptr must be {_ALIGN}-byte aligned (chunk slots of the resident layout)")
     grid = tuple(-(-s // c) for s, c in zip(ds.shape, ds.chunks))
     n_all = int(np.prod(grid))
     with _RESIDENT_LOCK:
@@ -215,11 +226,20 @@ def _pipeline_groups(sizes, n_groups):
 
 
 
+# PYAS_ZERO_SIGN_FALLBACK=warn: a query whose zero-sign pass the device cannot
+# run returns the reduction with the device's sign of a zero min/max and a
+# RuntimeWarning, instead of raising (the default keeps NumPy's bytes or fails)
+_SIGN_FALLBACK_WARN = os.environ.get("PYAS_ZERO_SIGN_FALLBACK", "") == "warn"
+
+
 def _sign_fallback(err):
     """A zero-sign pass the device cannot run for this query (e.g. 2^31 or
-    more reduced elements per output: its scan keys are 32-bit).  The
-    reduction itself is complete; only the sign of a zero min/max is then
-    the device reduction's rather than NumPy's (storage.py:99-100)."""
+    more reduced elements per output: its scan keys are 32-bit).  Raises
+    ``err`` unless the caller opted in (PYAS_ZERO_SIGN_FALLBACK=warn): the
+    reduction itself is complete, but the sign of a zero min/max would be the
+    device reduction's rather than NumPy's (storage.py:99-100)."""
+    if not _SIGN_FALLBACK_WARN:
+        raise err
     warnings.warn(f"the sign of a zero min/max is not NumPy's for this query ({err})",
                   RuntimeWarning, stacklevel=3)
 
@@ -422,9 +442,11 @@ class Active:
         nbytes = int(np.prod(ds.chunks)) * ds.dtype.itemsize
         stride = -(-nbytes // _ALIGN) * _ALIGN
         grid = tuple(-(-s // c) for s, c in zip(ds.shape, ds.chunks))
+        _check_attached(ds, self.device)
         ctx = get_context(self.device)
         with _RESIDENT_LOCK:
             store = getattr(ds, "_pyas_resident", None)
+            _check_attached(ds, self.device)
             if store is None or store["device"] != self.device:
                 n_all = int(np.prod(grid))
                 store = {"device": self.device, "buf": DeviceBuffer(ctx, max(n_all, 1) * stride),

@@ -164,3 +164,43 @@ def test_resident_plan_replay(gpu, monkeypatch):
     finally:
         release_resident(var)
     assert getattr(var, "_pyas_resident", None) is None
+
+
+def test_attach_resident_matches_file(gpu):
+    """attach_resident: chunks a GPU producer already holds in
+    HBM, in the resident slot layout, answer whole and partial-axis queries
+    exactly as the variable's own bytes do; a misaligned pointer and a query
+    on another device than the attached one raise instead of silently
+    replacing the caller's store."""
+    import torch
+    from pyactivestorage_amd.active import attach_resident
+    var = D.make_variable()
+    ref = D.make_variable()
+    nd = len(var.shape)
+    grid = [-(-s // c) for s, c in zip(var.shape, var.chunks)]
+    nbytes = int(np.prod(var.chunks)) * np.dtype(var.dtype).itemsize
+    stride = -(-nbytes // 256) * 256
+    host = np.zeros(int(np.prod(grid)) * stride, dtype=np.uint8)
+    for k, cc in enumerate(np.ndindex(*grid)):
+        off, size = var.chunk_info(cc)
+        host[k * stride: k * stride + size] = np.frombuffer(var.read(off, size), dtype=np.uint8)
+    data = torch.from_numpy(host).to("cuda:0")
+    with pytest.raises(ValueError, match="aligned"):
+        attach_resident(var, data.data_ptr() + 4, device=0, owner=data)
+    attach_resident(var, data.data_ptr(), device=0, owner=data)
+    try:
+        with pytest.raises(ValueError, match="already has a resident copy"):
+            attach_resident(var, data.data_ptr(), device=0, owner=data)
+        half = tuple(slice(0, max(1, n // 2)) for n in var.shape)
+        for method, axis, index in [("mean", None, (slice(None),) * nd), ("min", (0,), half),
+                                    ("max", (nd - 1,), half), ("mean", (0, nd - 1), (slice(None),) * nd)]:
+            want, _ = _query(ref, method, axis, index, False)
+            got, read = _query(var, method, axis, index, True)
+            assert read == 0, (method, axis)          # nothing from the variable's reader
+            _same(got, want, f"attached {method} {axis}", "exact")
+        from pyactivestorage_amd.active import _check_attached
+        with pytest.raises(ValueError, match="attached on device 0"):
+            _check_attached(var, 1)               # what a device-1 query meets first
+    finally:
+        release_resident(var)
+    assert getattr(var, "_pyas_resident", None) is None
