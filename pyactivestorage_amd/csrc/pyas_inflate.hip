@@ -3,27 +3,33 @@
 // Row f3 of the hot-path table: the reference inflates every compressed chunk
 // on the host, `numcodecs.Zlib.decode` -> `zlib.decompress` (built at
 // activestorage/hdf2numcodec.py:34-35, applied at activestorage/storage.py:
-// 119-120).  Here one wave64 inflates one chunk stream; a launch covers every
-// chunk of a query, so thousands of streams decode concurrently.
+// 119-120).  Here one workgroup of two waves inflates one chunk stream, and a
+// launch covers every chunk of a query, so thousands of streams decode
+// concurrently.  DEFLATE is serial within a stream, so a stream's rate is set
+// by the latency of its dependent steps; the two waves split those steps and
+// run them concurrently:
 //
-// Per wave:
-//   * input: a 128-dword LDS ring refilled 64 dwords at a time from a block
-//     loaded one refill ahead, so the window's bits are two LDS dwords per
-//     lane and the symbol loop never waits on a global load;
-//   * Huffman decode: 10-bit literal/length and 8-bit distance lookup tables
-//     in LDS, canonical walk for longer codes;
-//   * symbols: a speculative window -- every lane decodes the symbol that
-//     would start at its bit offset, one v_readlane per symbol walks the real
-//     chain, and the window's output bytes are produced lane-parallel (one
-//     lane per output byte, matches resolved by pointer jumping);
-//   * output: the most recent 2^WBITS bytes (8-32 KiB) live in an LDS ring,
-//     flushed to HBM in coalesced 1 KiB pieces with Adler-32 folded in per
-//     flush by a wave reduction;
-//   * a match reaching further back than the ring (d > 2^WBITS, up to
-//     DEFLATE's 32 KiB) reads the already-flushed output from HBM after the
-//     wave's stores have drained, with L1-bypassing (agent-scope) loads.
-//     A smaller ring is what buys occupancy: 2^13 B + tables ~= 12.7 KiB of
-//     LDS per wave -> 12 streams per CU instead of 4.
+//   * the DECODER wave (wave 0) turns the bit stream into tokens -- literal,
+//     match (length, distance) or stored block -- with their output offsets,
+//     into an LDS token queue.  Input comes through a 128-dword LDS ring
+//     refilled one 64-dword block ahead.  Compressed blocks are decoded in
+//     speculative windows: lane k decodes, at each bit offset 64 j + k of the
+//     window (j < NG), the whole symbol that WOULD start there (10-bit
+//     literal/length and 8-bit distance root tables whose entries carry the
+//     extra-bit counts and bases), and its successor offset; the real chain
+//     from offset 0 is walked on the scalar unit, one v_readlane per symbol,
+//     and appended to the queue (output offsets from a wave prefix sum).
+//     A code past the root table, end of block, an invalid symbol, a distance
+//     before the output start, output past the capacity or truncation ends
+//     the chain; the serial decoder takes that symbol and reports zlib's error.
+//   * the WRITER wave (wave 1) takes up to 64 queued tokens at a time (one per
+//     lane, at most kBud output bytes) and writes them into the most recent
+//     2^WBITS output bytes, an LDS ring flushed to HBM in coalesced 1 KiB
+//     pieces with Adler-32 folded in per flush.  A token goes once every byte
+//     its source needs is written: lanes write literals and short matches, the
+//     whole wave copies long or overlapping matches, and a match further back
+//     than the ring reads the already-flushed output from HBM (L1-bypassing
+//     loads issued before the batch's LDS work).
 // Error behaviour follows zlib's inflate(): bad header, preset dictionary,
 // invalid block type, stored-length mismatch, over-subscribed or incomplete
 // codes, invalid symbols, distance too far back, truncated input and Adler-32
@@ -34,39 +40,97 @@ namespace pyas {
 namespace {
 
 constexpr int kLitBits = 10, kDistBits = 8;
-
 constexpr uint32_t kFlush = 1024;   // bytes per coalesced flush (16 per lane)
+constexpr uint32_t kQ = 512;        // token queue entries (power of two)
+constexpr uint32_t kStoredTok = 0xffffu;   // len field of a stored-block token (two queue slots)
 
-__constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                        31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t c_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
-                                        2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t c_dist_base[30] = {1,    2,    3,    4,    5,    7,     9,     13,    17,  25,
-                                         33,   49,   65,   97,   129,  193,   257,   385,   513, 769,
-                                         1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
-                                         6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t c_clen_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// Code tables + build scratch (the history window is separate: its size is a
-// template parameter of the kernel).
+// Root-table entry (32 bits): sym | code length << 9 | extra bits << 13 |
+// base << 17, where extra/base are the length (literal/length table) or
+// distance (distance table) fields RFC 1951 3.2.5 attaches to the symbol, so
+// a whole symbol's fields come from one LDS load.  Code length 0: the code
+// is longer than the root table (canonical walk).
 struct Lds {
-    uint16_t lit[1 << kLitBits];    // sym | len << 9; len 0 -> canonical walk
-    uint16_t dist[1 << kDistBits];
+    uint32_t lit[1 << kLitBits];
+    uint32_t dist[1 << kDistBits];
     uint16_t lit_cnt[16], dist_cnt[16];
     uint16_t lit_sym[288], dist_sym[32];
     uint16_t code[320];             // canonical code per symbol (build scratch)
     uint16_t offs[16], next[16];    // build scratch
     uint8_t lens[320];              // code lengths: literal/length then distance
+    int32_t status;                 // build result
+};
+
+// Token queue from the decoder wave to the writer wave.  Token t sits at
+// slot t % kQ: pos = its output offset, w = len << 16 | d (a match of len
+// bytes at distance d), len 0: a literal (d = the byte), len kStoredTok: a
+// stored block of d bytes whose input byte offset is the next slot's pos.
+struct Queue {
+    uint32_t pos[kQ];
+    uint32_t w[kQ];
+    uint32_t prod;      // tokens published by the decoder
+    uint32_t cons;      // tokens the writer is done with
+    uint32_t done;      // 1: the decoder finished (status, adler valid)
+    int32_t status;
+    uint32_t adler;     // the stream's Adler-32 trailer
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t k) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)k);
+}
+
+// LDS written by other lanes of this wave is read after this point (the
+// compiler may not forward a lane's own earlier store across it).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Queue counters between the two waves (LDS, workgroup scope).
+__device__ __forceinline__ uint32_t load_acq(uint32_t *p) {
+    return uni(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void store_rel(uint32_t *p, uint32_t v) {
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Inclusive prefix sum over the wave: DPP shifts inside each 16-lane row,
+// then the row totals (lanes 15, 31, 47) added with three readlanes.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    const uint32_t r0 = rl(x, 15), r1 = rl(x, 31), r2 = rl(x, 47);
+    const uint32_t row = (uint32_t)lane >> 4;
+    return x + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+}
+
+// Phase timing (diagnostic build, -DPYAS_INFLATE_PROF): per-wave cycle sums
+// of the phases and event counts, printed for the first streams of a launch.
+#ifdef PYAS_INFLATE_PROF
+#define PYAS_PROF_INIT uint64_t pf_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t pf_last = clock64(); \
+                       uint64_t pf_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PYAS_STAT(i, v) (pf_st[i] += (v))
+#define PYAS_PROF(i) do { const uint64_t pf_n = clock64(); pf_acc[i] += pf_n - pf_last; pf_last = pf_n; } while (0)
+#else
+#define PYAS_PROF_INIT
+#define PYAS_PROF(i) do { } while (0)
+#define PYAS_STAT(i, v) ((void)0)
+#endif
+
+// ---------------------------------------------------------------------------
+// Decoder side
+// ---------------------------------------------------------------------------
 
 // Bit reader over dword-aligned input, staged through a 128-dword LDS ring:
-// the wave's window bits come from two LDS dwords per lane (no readlanes, no
-// vector-memory wait in the symbol loop).  The ring is refilled 64 dwords at
-// a time from a block loaded into one VGPR per lane a refill earlier, so the
-// global load latency is off the decode path.
+// window bits come from LDS (no vector-memory wait in the symbol loop).  The
+// ring is refilled 64 dwords at a time from a block loaded into one VGPR per
+// lane a refill earlier, so the global load latency is off the decode path.
 constexpr uint32_t kInRing = 128, kInBlock = 64;
 
 struct BitIn {
@@ -103,19 +167,36 @@ struct BitIn {
     // At least 32 valid bits starting at pos (uniform).
     __device__ __forceinline__ uint32_t peek() {
         ensure();
+        wave_lds_sync();
         return uni(bits_at(0));
     }
 };
 
+// Length (kind 1) or distance (kind 2) fields of symbol s for the root-table
+// entry: extra bits << 13 | base << 17 (RFC 1951 3.2.5).
+__device__ __forceinline__ uint32_t sym_fields(int kind, uint32_t s) {
+    if (kind == 1 && s >= 257u && s < 286u) {
+        const uint32_t ls = s - 257u;
+        const uint32_t le = (ls < 8u || ls == 28u) ? 0u : (ls - 4u) >> 2;
+        const uint32_t base = ls < 8u ? ls + 3u : ls == 28u ? 258u : ((4u + (ls & 3u)) << le) + 3u;
+        return (le << 13) | (base << 17);
+    }
+    if (kind == 2 && s < 30u) {
+        const uint32_t de = s < 4u ? 0u : (s - 2u) >> 1;
+        const uint32_t base = s < 4u ? s + 1u : ((2u + (s & 1u)) << de) + 1u;
+        return (de << 13) | (base << 17);
+    }
+    return 0u;
+}
+
 // Canonical Huffman table for `n` code lengths in L.lens[first..first+n).
-// Returns 0, or PYAS_INFLATE_BAD_CODE for over-subscribed / disallowed
-// incomplete sets (zlib inflate_table rules: incomplete only for a single
-// length-1 code in the literal/length and distance trees).
-__device__ int build(Lds &L, int first, int n, uint16_t *cnt, uint16_t *sorted, uint16_t *tab, int P,
-                     bool code_lengths) {
+// kind: 0 code-length code, 1 literal/length, 2 distance.  Returns 0, or
+// PYAS_INFLATE_BAD_CODE for over-subscribed / disallowed incomplete sets
+// (zlib inflate_table rules: incomplete only for a single length-1 code in
+// the literal/length and distance trees).
+__device__ int build(Lds &L, int first, int n, uint16_t *cnt, uint16_t *sorted, uint32_t *tab, int P, int kind) {
     const int lane = threadIdx.x & 63;
     for (int k = lane; k < (1 << P); k += 64) tab[k] = 0;
-    __shared__ int s_status;
     if (lane == 0) {
         for (int l = 0; l < 16; ++l) cnt[l] = 0;
         for (int s = 0; s < n; ++s) cnt[L.lens[first + s]]++;
@@ -128,7 +209,7 @@ __device__ int build(Lds &L, int first, int n, uint16_t *cnt, uint16_t *sorted, 
             left = (left << 1) - cnt[l];
             if (left < 0) status = PYAS_INFLATE_BAD_CODE;
         }
-        if (left > 0 && max > 0 && (code_lengths || max != 1)) status = PYAS_INFLATE_BAD_CODE;
+        if (left > 0 && max > 0 && (kind == 0 || max != 1)) status = PYAS_INFLATE_BAD_CODE;
         uint16_t *offs = L.offs, *next = L.next;
         offs[1] = 0;
         next[1] = 0;
@@ -143,28 +224,28 @@ __device__ int build(Lds &L, int first, int n, uint16_t *cnt, uint16_t *sorted, 
                 L.code[s] = next[l]++;
             }
         }
-        s_status = status;
+        L.status = status;
     }
-    __syncthreads();
+    wave_lds_sync();
     for (int s = lane; s < n; s += 64) {
         const int l = L.lens[first + s];
         if (l && l <= P) {
             const uint32_t rc = __builtin_bitreverse32((uint32_t)L.code[s]) >> (32 - l);
-            const uint16_t e = (uint16_t)(s | (l << 9));
+            const uint32_t e = (uint32_t)s | ((uint32_t)l << 9) | sym_fields(kind, (uint32_t)s);
             for (uint32_t k = rc; k < (1u << P); k += 1u << l) tab[k] = e;
         }
     }
-    __syncthreads();
-    return uni((uint32_t)s_status);
+    wave_lds_sync();
+    return (int)uni((uint32_t)L.status);
 }
 
 // Decode one symbol: table hit, else canonical walk over the peeked bits.
 // Returns sym and sets len (0 on an invalid code).
-__device__ __forceinline__ uint32_t decode(uint32_t bits, const uint16_t *tab, int P, const uint16_t *cnt,
+__device__ __forceinline__ uint32_t decode(uint32_t bits, const uint32_t *tab, int P, const uint16_t *cnt,
                                            const uint16_t *sorted, uint32_t &len) {
     const uint32_t e = uni(tab[bits & ((1u << P) - 1)]);
-    if (e >> 9) {
-        len = e >> 9;
+    if ((e >> 9) & 15u) {
+        len = (e >> 9) & 15u;
         return e & 511u;
     }
     int code = 0, firstc = 0, index = 0;
@@ -182,6 +263,346 @@ __device__ __forceinline__ uint32_t decode(uint32_t bits, const uint16_t *tab, i
     len = 0;
     return 0;
 }
+
+template <int NG>
+__device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ring, Queue &Q) {
+    PYAS_PROF_INIT
+    const int lane = threadIdx.x & 63;
+    const uint8_t *src = x.src + x.src_offsets[c];
+    const int64_t n_in = x.src_sizes[c];
+    const uint32_t mis = (uint32_t)((uintptr_t)src & 3);
+    BitIn in;
+    in.ring = in_ring;
+    in.w = reinterpret_cast<const uint32_t *>(src - mis);
+    in.nbits = (uint32_t)((n_in + mis) * 8);
+    in.nwords = (uint32_t)((n_in + mis + 3) / 4);
+    in.pos = mis * 8;
+    in.seek();
+    const uint32_t cap = (uint32_t)x.dst_capacity[c];
+    uint32_t q = 0;           // output bytes decoded so far
+    uint32_t prod = 0;        // tokens published
+    uint32_t cons_seen = 0;   // the writer's count, last read
+    int status = PYAS_INFLATE_OK;
+    uint32_t adler = 0;
+
+    // wait until n more tokens fit in the queue
+    auto room = [&](uint32_t n) {
+        while (prod + n - cons_seen > kQ) {
+            __builtin_amdgcn_s_sleep(1);
+            cons_seen = load_acq(&Q.cons);
+        }
+    };
+    auto publish = [&](uint32_t n) {
+        prod += n;
+        store_rel(&Q.prod, prod);
+    };
+    auto emit1 = [&](uint32_t pos, uint32_t w) {   // one token from the serial decoder
+        room(1);
+        if (lane == 0) {
+            Q.pos[prod & (kQ - 1)] = pos;
+            Q.w[prod & (kQ - 1)] = w;
+        }
+        publish(1);
+    };
+
+    // zlib header (RFC 1950): CM 8, CINFO <= 7, FCHECK, no preset dictionary
+    if (n_in < 6) status = PYAS_INFLATE_TRUNCATED;
+    if (status == 0) {
+        const uint32_t h = in.peek();
+        const uint32_t cmf = h & 255u, flg = (h >> 8) & 255u;
+        if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u)
+            status = PYAS_INFLATE_BAD_HEADER;
+        else if (flg & 32u)
+            status = PYAS_INFLATE_NEED_DICT;
+        in.pos += 16;
+    }
+    bool last = false;
+    while (status == 0 && !last) {
+        uint32_t h = in.peek();
+        last = h & 1u;
+        const uint32_t type = (h >> 1) & 3u;
+        in.pos += 3;
+        if (type == 0) {   // stored: one token, the writer copies the bytes
+            in.pos = (in.pos + 7) & ~7u;
+            h = in.peek();
+            const uint32_t len = h & 0xffffu, nlen = h >> 16;
+            in.pos += 32;
+            if ((len ^ 0xffffu) != nlen) { status = PYAS_INFLATE_BAD_STORED; break; }
+            if (in.pos + len * 8 > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
+            if (q + len > cap) { status = PYAS_INFLATE_OVERFLOW; break; }
+            if (len) {
+                room(2);
+                if (lane == 0) {
+                    Q.pos[prod & (kQ - 1)] = q;
+                    Q.w[prod & (kQ - 1)] = (kStoredTok << 16) | len;
+                    Q.pos[(prod + 1) & (kQ - 1)] = in.pos >> 3;   // input byte offset from in.w
+                    Q.w[(prod + 1) & (kQ - 1)] = 0u;
+                }
+                publish(2);
+                q += len;
+            }
+            in.pos += len * 8;
+            in.seek();
+            continue;
+        }
+        if (type == 1) {   // fixed codes (RFC 1951 3.2.6)
+            for (int s = lane; s < 320; s += 64)
+                L.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+            wave_lds_sync();
+            build(L, 0, 288, L.lit_cnt, L.lit_sym, L.lit, kLitBits, 1);
+            build(L, 288, 32, L.dist_cnt, L.dist_sym, L.dist, kDistBits, 2);
+        } else if (type == 2) {   // dynamic codes
+            h = in.peek();
+            const uint32_t nlen = (h & 31u) + 257, ndist = ((h >> 5) & 31u) + 1, ncode = ((h >> 10) & 15u) + 4;
+            in.pos += 14;
+            if (nlen > 286 || ndist > 30) { status = PYAS_INFLATE_BAD_CODE; break; }
+            // code-length code: 3 bits per length in c_clen_order
+            h = in.peek();
+            in.pos += 30;
+            const uint32_t h2 = in.peek();
+            in.pos -= 30;
+            for (int s = lane; s < 19; s += 64) {
+                const uint32_t bit = 3u * (uint32_t)s;
+                uint32_t v = 0;
+                if ((uint32_t)s < ncode) v = bit < 30 ? (h >> bit) & 7u : (h2 >> (bit - 30)) & 7u;
+                L.lens[c_clen_order[s]] = (uint8_t)v;
+            }
+            in.pos += 3 * ncode;
+            wave_lds_sync();
+            // the code-length tree uses the distance table slots (7-bit codes)
+            if (build(L, 0, 19, L.dist_cnt, L.dist_sym, L.dist, 7, 0)) { status = PYAS_INFLATE_BAD_CODE; break; }
+            // code lengths for literal/length + distance, serial (<= 316)
+            uint32_t k = 0;
+            uint32_t prev = 0;
+            while (k < nlen + ndist) {
+                const uint32_t bits = in.peek();
+                uint32_t l;
+                const uint32_t sym = decode(bits, L.dist, 7, L.dist_cnt, L.dist_sym, l);
+                if (!l) { status = PYAS_INFLATE_BAD_CODE; break; }
+                in.pos += l;
+                const uint32_t more = bits >> l;
+                uint32_t rep, val;
+                if (sym < 16) {
+                    rep = 1; val = sym; prev = sym;
+                } else if (sym == 16) {
+                    if (k == 0) { status = PYAS_INFLATE_BAD_CODE; break; }
+                    rep = 3 + (more & 3u); val = prev; in.pos += 2;
+                } else if (sym == 17) {
+                    rep = 3 + (more & 7u); val = 0; in.pos += 3;
+                } else {
+                    rep = 11 + (more & 127u); val = 0; in.pos += 7;
+                }
+                if (k + rep > nlen + ndist) { status = PYAS_INFLATE_BAD_CODE; break; }
+                if (sym > 16) prev = 0;   // zlib: repeat-previous after zeros repeats zero
+                for (uint32_t i = lane; i < rep; i += 64) {
+                    const uint32_t s = k + i;
+                    L.lens[s < nlen ? s : 288 + (s - nlen)] = (uint8_t)val;
+                }
+                k += rep;
+            }
+            if (status) break;
+            for (int s = nlen + lane; s < 288; s += 64) L.lens[s] = 0;
+            for (int s = 288 + (int)ndist + lane; s < 320; s += 64) L.lens[s] = 0;
+            wave_lds_sync();
+            if (L.lens[256] == 0) { status = PYAS_INFLATE_BAD_CODE; break; }
+            if (build(L, 0, 288, L.lit_cnt, L.lit_sym, L.lit, kLitBits, 1) ||
+                build(L, 288, 32, L.dist_cnt, L.dist_sym, L.dist, kDistBits, 2)) {
+                status = PYAS_INFLATE_BAD_CODE;
+                break;
+            }
+        } else {
+            status = PYAS_INFLATE_BAD_BLOCK;
+            break;
+        }
+        PYAS_PROF(5);
+        // One symbol, any code length (canonical walk past the root tables),
+        // queued as a token.  Returns 0 = continue, 1 = end of block, 2 =
+        // error (status set).
+        auto one_symbol = [&]() -> int {
+            if (in.pos > in.nbits) { status = PYAS_INFLATE_TRUNCATED; return 2; }
+            uint32_t bits = in.peek();
+            uint32_t l;
+            uint32_t sym = decode(bits, L.lit, kLitBits, L.lit_cnt, L.lit_sym, l);
+            if (!l) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
+            if (sym < 256) {
+                if (q >= cap) { status = PYAS_INFLATE_OVERFLOW; return 2; }
+                emit1(q, sym);
+                q++;
+                in.pos += l;
+                return 0;
+            }
+            if (sym == 256) { in.pos += l; return 1; }
+            if (sym >= 286) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
+            const uint32_t lf = sym_fields(1, sym);
+            const uint32_t le = (lf >> 13) & 15u;
+            const uint32_t len = (lf >> 17) + ((bits >> l) & ((1u << le) - 1u));
+            in.pos += l + le;
+            bits = in.peek();
+            const uint32_t ds = decode(bits, L.dist, kDistBits, L.dist_cnt, L.dist_sym, l);
+            if (!l || ds >= 30) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
+            const uint32_t df = sym_fields(2, ds);
+            const uint32_t de = (df >> 13) & 15u;
+            const uint32_t d = (df >> 17) + ((bits >> l) & ((1u << de) - 1u));
+            in.pos += l + de;
+            if (d > q) { status = PYAS_INFLATE_BAD_DISTANCE; return 2; }
+            if (q + len > cap) { status = PYAS_INFLATE_OVERFLOW; return 2; }
+            emit1(q, (len << 16) | d);
+            q += len;
+            return 0;
+        };
+        // ---- speculative windows ------------------------------------------
+        constexpr uint32_t kStop = 1u << 12;
+        const uint32_t *lit = L.lit, *dist = L.dist;
+        bool eob = false;
+        uint32_t windows_left = in.nbits + 64u;   // every window consumes input; a stuck walk ends here
+        while (!eob) {
+            if (windows_left-- == 0u) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
+            in.ensure();                                 // the ring holds the window's bits
+            wave_lds_sync();
+            const uint32_t t0 = in.pos + (uint32_t)lane;
+            const uint32_t k0 = t0 >> 5, sh = t0 & 31u;
+            uint32_t dw[2 * NG + 1];
+#pragma unroll
+            for (int i = 0; i < 2 * NG + 1; ++i) dw[i] = in_ring[(k0 + (uint32_t)i) & (kInRing - 1)];
+            uint32_t nxt[NG], olen[NG], tw[NG], mdist[NG];
+#pragma unroll
+            for (int j = 0; j < NG; ++j) {
+                const uint32_t lo = __builtin_amdgcn_alignbit(dw[2 * j + 1], dw[2 * j], sh);
+                const uint32_t hi = __builtin_amdgcn_alignbit(dw[2 * j + 2], dw[2 * j + 1], sh);
+                const uint32_t E = lit[lo & ((1u << kLitBits) - 1u)];
+                const uint32_t l = (E >> 9) & 15u, sym = E & 511u, le = (E >> 13) & 15u, lbase = E >> 17;
+                const uint32_t s1 = l + le;
+                const uint32_t db = __builtin_amdgcn_alignbit(hi, lo, s1);   // bits after the length
+                const uint32_t D = dist[db & ((1u << kDistBits) - 1u)];
+                const uint32_t dl = (D >> 9) & 15u, ds = D & 511u, de = (D >> 13) & 15u, dbase = D >> 17;
+                const uint32_t ml = lbase + ((lo >> l) & ((1u << le) - 1u));
+                const uint32_t md = dbase + ((db >> dl) & ((1u << de) - 1u));
+                const uint32_t off = 64u * (uint32_t)j + (uint32_t)lane;
+                const bool is_lit = sym < 256u;
+                const bool stop = in.pos + off > in.nbits || !l || sym == 256u || sym >= 286u ||
+                                  (!is_lit && (!dl || ds >= 30u));
+                nxt[j] = stop ? kStop : is_lit ? off + l : off + s1 + dl + de;
+                olen[j] = is_lit ? 1u : ml;
+                mdist[j] = is_lit ? 0u : md;
+                tw[j] = is_lit ? sym : (ml << 16) | md;
+            }
+            PYAS_PROF(0);
+            // the chain from offset 0, group by group (it only moves forward)
+            uint64_t M[NG];
+            uint32_t off = 0, prev = 0;
+            bool stopped = false;
+#pragma unroll
+            for (int j = 0; j < NG; ++j) {
+                M[j] = 0ull;
+                if (!stopped) {
+                    while (off < 64u * (uint32_t)(j + 1)) {
+                        M[j] |= 1ull << (off - 64u * (uint32_t)j);
+                        prev = off;
+                        off = rl(nxt[j], off - 64u * (uint32_t)j);
+                    }
+                    stopped = off >= kStop;
+                }
+            }
+            if (stopped) {                               // the stop symbol is not consumed
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+                    if ((prev >> 6) == (uint32_t)j) M[j] &= ~(1ull << (prev & 63u));
+                off = prev;
+            }
+            PYAS_PROF(1);
+            // output offsets along the chain: two groups per 32-bit prefix sum
+            uint32_t excl[NG], tot = 0;
+#pragma unroll
+            for (int j = 0; j < NG; j += 2) {
+                const uint32_t va = ((M[j] >> lane) & 1ull) ? olen[j] : 0u;
+                uint32_t vb = 0;
+                if (j + 1 < NG) vb = ((M[j + 1] >> lane) & 1ull) ? olen[j + 1] : 0u;
+                const uint32_t inc = wave_incl_sum(va | (vb << 16));
+                const uint32_t tt = rl(inc, 63);
+                excl[j] = tot + (inc & 0xffffu) - va;
+                tot += tt & 0xffffu;
+                if (j + 1 < NG) {
+                    excl[j + 1] = tot + (inc >> 16) - vb;
+                    tot += tt >> 16;
+                }
+            }
+            // the first chain symbol reaching before the output start or past
+            // the capacity ends the chain (the serial decoder reports it)
+            uint32_t cut = kStop, T = tot;
+#pragma unroll
+            for (int j = 0; j < NG; ++j) {
+                const bool on = (M[j] >> lane) & 1ull;
+                const uint32_t a = q + excl[j];
+                const uint64_t b = __ballot(on && (a + olen[j] > cap || mdist[j] > a));
+                if (b && cut == kStop) {
+                    const uint32_t cc = (uint32_t)__builtin_ctzll(b);
+                    cut = 64u * (uint32_t)j + cc;
+                    T = rl(excl[j], cc);
+                }
+            }
+            if (cut != kStop) {
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    const uint32_t lo = 64u * (uint32_t)j;
+                    M[j] = cut <= lo ? 0ull : cut - lo >= 64u ? M[j] : M[j] & ((1ull << (cut - lo)) - 1ull);
+                }
+                off = cut;
+            }
+            uint32_t count = 0;
+#pragma unroll
+            for (int j = 0; j < NG; ++j) count += (uint32_t)__builtin_popcountll(M[j]);
+            PYAS_PROF(2);
+            room(count);
+            PYAS_PROF(3);
+            uint32_t base = prod;
+#pragma unroll
+            for (int j = 0; j < NG; ++j) {
+                if ((M[j] >> lane) & 1ull) {
+                    const uint32_t idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(M[j] >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)M[j], 0u));
+                    Q.pos[idx & (kQ - 1)] = q + excl[j];
+                    Q.w[idx & (kQ - 1)] = tw[j];
+                }
+                base += (uint32_t)__builtin_popcountll(M[j]);
+            }
+            publish(count);
+            PYAS_STAT(0, 1u);
+            PYAS_STAT(1, count);
+            q += T;
+            in.pos += off;
+            PYAS_PROF(2);
+            if (stopped || cut != kStop) {
+                PYAS_STAT(2, 1u);
+                const int r = one_symbol();
+                PYAS_PROF(4);
+                if (r == 2) break;
+                if (r == 1) eob = true;
+            }
+        }
+    }
+    if (status == 0) {   // the Adler-32 trailer
+        in.pos = (in.pos + 7) & ~7u;
+        if (in.pos + 32 > in.nbits) status = PYAS_INFLATE_TRUNCATED;
+        else adler = __builtin_bswap32(in.peek());
+    }
+    if (lane == 0) {
+        Q.status = status;
+        Q.adler = adler;
+    }
+    store_rel(&Q.done, 1u);
+#ifdef PYAS_INFLATE_PROF
+    PYAS_PROF(7);
+    if (c < 4 && lane == 0)
+        printf("decoder %d: decode %lu walk %lu scan+emit %lu queue-full %lu serial %lu blocks %lu end %lu | windows %lu "
+               "tokens %lu serial %lu\n",
+               (int)c, pf_acc[0], pf_acc[1], pf_acc[2], pf_acc[3], pf_acc[4], pf_acc[5], pf_acc[7], pf_st[0], pf_st[1],
+               pf_st[2]);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Writer side
+// ---------------------------------------------------------------------------
 
 struct Out {
     uint8_t *dst;
@@ -228,89 +649,37 @@ __device__ void flush(const uint8_t *win, Out &o, uint32_t n) {
     o.fpos += n;
 }
 
-}  // namespace
-
-// Inclusive prefix sum over the wave: DPP shifts inside each 16-lane row,
-// then the row totals (lanes 15, 31, 47) added with three readlanes.
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
-    const int lane = threadIdx.x & 63;
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
-    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
-    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
-    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
-    const uint32_t row = (uint32_t)lane >> 4;
-    return x + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
-}
-
-// LDS written by other lanes of this wave is read after this point (the
-// compiler may not forward a lane's own earlier store across it).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
-    const int lane = threadIdx.x & 63;
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true));
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true));
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true));
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true));
-    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 15);
-    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 31);
-    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 47);
-    const uint32_t row = (uint32_t)lane >> 4;
-    uint32_t c = row >= 1 ? r0 : 0u;
-    c = row >= 2 ? max(c, r1) : c;
-    c = row >= 3 ? max(c, r2) : c;
-    return max(x, c);
-}
-
-// Byte of already-flushed output, coherent with this wave's earlier stores.
-__device__ __forceinline__ uint32_t far_byte(const uint8_t *p) {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>((uintptr_t)p & ~(uintptr_t)3);
-    const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (v >> (((uintptr_t)p & 3) * 8)) & 255u;
-}
-
-// Phase timing (diagnostic build, -DPYAS_INFLATE_PROF): per-wave cycle sums
-// of the decode phases, printed for the first streams of a launch.
-#ifdef PYAS_INFLATE_PROF
-#define PYAS_PROF_INIT uint64_t pf_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}; uint64_t pf_last = clock64(); \
-                       uint64_t pf_st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define PYAS_STAT(i, v) (pf_st[i] += (v))
-#define PYAS_PROF(i) do { const uint64_t pf_n = clock64(); pf_acc[i] += pf_n - pf_last; pf_last = pf_n; \
-                          if ((i) == 0) pf_acc[8]++; } while (0)
-#else
-#define PYAS_PROF_INIT
-#define PYAS_PROF(i) do { } while (0)
-#define PYAS_STAT(i, v) ((void)0)
-#endif
+// 16 bytes of already-flushed output at dst + src (realigned from five
+// L1-bypassing dword loads; dwords at or past `lim` are not read).
+struct Far16 {
+    uint32_t v[5], sh;
+    __device__ __forceinline__ void load(const uint8_t *p, const uint8_t *lim) {
+        const uint32_t *wb = reinterpret_cast<const uint32_t *>((uintptr_t)p & ~(uintptr_t)3);
+        sh = (uint32_t)((uintptr_t)p & 3);
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            v[k] = reinterpret_cast<const uint8_t *>(wb + k) < lim
+                       ? __hip_atomic_load(wb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                       : 0u;
+    }
+    __device__ __forceinline__ uint32_t word(int k) const { return __builtin_amdgcn_alignbyte(v[k + 1], v[k], sh); }
+};
 
 template <int WBITS>
-__global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
+__device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) {
     PYAS_PROF_INIT
     constexpr uint32_t kWin = 1u << WBITS, kWinMask = kWin - 1;
-    static_assert(kWin >= 4096, "ring must exceed the unflushed bytes plus one match");
-    __shared__ Lds L;
-    __shared__ alignas(16) uint8_t win[kWin];
-    const int64_t c = blockIdx.x;
-    const int lane = threadIdx.x;
+    // A batch writes at most kBud bytes past o.pos and starts with fewer than
+    // kFlush bytes unflushed, so a source d <= kFar back is still in the ring
+    // and a longer one is already in dst; the ring holds the unflushed bytes.
+    constexpr uint32_t kBud = kWin / 8, kFar = kWin - kBud;
+    static_assert(kFar > 258u + kBud + kFlush, "far sources must be flushed");
+    const int lane = threadIdx.x & 63;
+    uint32_t *win32 = reinterpret_cast<uint32_t *>(win);
     const uint8_t *src = x.src + x.src_offsets[c];
-    const int64_t n_in = x.src_sizes[c];
     const uint32_t mis = (uint32_t)((uintptr_t)src & 3);
-    __shared__ uint32_t in_ring[kInRing];
-    __shared__ uint8_t mark[64];              // symbol starts of one 64-byte output step
-    BitIn in;
-    in.ring = in_ring;
-    in.w = reinterpret_cast<const uint32_t *>(src - mis);
-    in.nbits = (uint32_t)((n_in + mis) * 8);
-    in.nwords = (uint32_t)((n_in + mis + 3) / 4);
-    in.pos = mis * 8;
-    in.seek();
+    const uint32_t *inw = reinterpret_cast<const uint32_t *>(src - mis);
+    const uint32_t in_words = (uint32_t)((x.src_sizes[c] + mis + 3) / 4);
     Out o;
     o.dst = x.dst + x.dst_offsets[c];
     o.cap = (uint32_t)x.dst_capacity[c];
@@ -319,463 +688,188 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
     o.b = 0;
     o.aligned = (((uintptr_t)o.dst) & 15) == 0;
     int status = PYAS_INFLATE_OK;
+    uint32_t cons = 0;
 
-    // zlib header (RFC 1950): CM 8, CINFO <= 7, FCHECK, no preset dictionary
-    if (n_in < 6) status = PYAS_INFLATE_TRUNCATED;
-    if (status == 0) {
-        const uint32_t h = in.peek();
-        const uint32_t cmf = h & 255u, flg = (h >> 8) & 255u;
-        if ((cmf & 15u) != 8u || (cmf >> 4) > 7u || ((cmf << 8) | flg) % 31u != 0u)
-            status = PYAS_INFLATE_BAD_HEADER;
-        else if (flg & 32u)
-            status = PYAS_INFLATE_NEED_DICT;
-        in.pos += 16;
-    }
-    bool last = false;
-    while (status == 0 && !last) {
-        uint32_t h = in.peek();
-        last = h & 1u;
-        const uint32_t type = (h >> 1) & 3u;
-        in.pos += 3;
-        if (type == 0) {   // stored
-            in.pos = (in.pos + 7) & ~7u;
-            h = in.peek();
-            const uint32_t len = h & 0xffffu, nlen = h >> 16;
-            in.pos += 32;
-            if ((len ^ 0xffffu) != nlen) { status = PYAS_INFLATE_BAD_STORED; break; }
-            if (in.pos + len * 8 > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
-            if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
-            // 16 bytes per lane per 1 KiB step: five independent dword loads
-            // (the stream is dword-aligned at in.w), realigned with alignbyte
-            const uint32_t byte0 = in.pos >> 3;
-            for (uint32_t done = 0; done < len;) {
+    // Whole-wave copy of one match (tp, td, tl): every source byte lies before
+    // tp (td >= tl) or repeats the period [tp - td, tp) (td < tl).
+    auto wave_copy = [&](uint32_t tp, uint32_t td, uint32_t tl) {
+        const uint32_t ts = tp - td;
+        uint32_t v[5];
+        if (td >= tl) {
+#pragma unroll
+            for (uint32_t k = 0; k < 5u; ++k)
+                if (64u * k < tl) v[k] = win[(ts + (uint32_t)lane + 64u * k) & kWinMask];
+        } else {
+            const uint32_t r64 = 64u % td;
+            uint32_t m = (uint32_t)lane % td;
+#pragma unroll
+            for (uint32_t k = 0; k < 5u; ++k) {
+                if (64u * k < tl) v[k] = win[(ts + m) & kWinMask];
+                m += r64;
+                m = m >= td ? m - td : m;
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 5u; ++k) {
+            const uint32_t ii = (uint32_t)lane + 64u * k;
+            if (64u * k < tl && ii < tl) win[(tp + ii) & kWinMask] = (uint8_t)v[k];
+        }
+    };
+
+    for (;;) {
+        uint32_t prod = 0, done = 0;
+        for (;;) {
+            done = load_acq(&Q.done);
+            prod = load_acq(&Q.prod);
+            if (prod - cons >= 64u || done) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        PYAS_PROF(0);
+        if (done && Q.status != PYAS_INFLATE_OK) {
+            status = Q.status;
+            break;
+        }
+        if (prod == cons) break;   // done, every token written
+        const uint32_t avail = prod - cons;
+        const bool act = (uint32_t)lane < avail;
+        const uint32_t slot = (cons + (uint32_t)lane) & (kQ - 1);
+        const uint32_t p = act ? Q.pos[slot] : 0u;
+        const uint32_t w = act ? Q.w[slot] : 0u;
+        uint32_t len = w >> 16, d = w & 0xffffu;
+        const uint64_t stored = __ballot(act && len == kStoredTok);
+        if (stored & 1ull) {   // a stored block: 16 bytes per lane per 1 KiB step
+            const uint32_t slen = rl(d, 0);
+            const uint32_t byte0 = Q.pos[(cons + 1) & (kQ - 1)];
+            for (uint32_t dn = 0; dn < slen;) {
                 while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
-                const uint32_t step = min(len - done, kFlush);
+                const uint32_t step = min(slen - dn, kFlush);
                 const uint32_t mine = (uint32_t)lane * 16u;
                 if (mine < step) {
-                    const uint32_t b = byte0 + done + mine;
+                    const uint32_t b = byte0 + dn + mine;
                     const uint32_t wi = b >> 2, sh = b & 3u;
                     uint32_t dw[5];
 #pragma unroll
                     for (uint32_t k = 0; k < 5; ++k)
-                        dw[k] = wi + k < in.nwords ? __builtin_nontemporal_load(in.w + wi + k) : 0u;
+                        dw[k] = wi + k < in_words ? __builtin_nontemporal_load(inw + wi + k) : 0u;
                     const uint32_t n = min(step - mine, 16u);
 #pragma unroll
                     for (uint32_t k = 0; k < 4; ++k) {
-                        const uint32_t q = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
+                        const uint32_t qv = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
 #pragma unroll
                         for (uint32_t m = 0; m < 4; ++m)
-                            if (k * 4 + m < n) win[(o.pos + mine + k * 4 + m) & kWinMask] = (uint8_t)(q >> (8 * m));
+                            if (k * 4 + m < n) win[(o.pos + mine + k * 4 + m) & kWinMask] = (uint8_t)(qv >> (8 * m));
                     }
                 }
                 o.pos += step;
-                done += step;
-                __syncthreads();
+                dn += step;
+                wave_lds_sync();
             }
-            in.pos += len * 8;
-            in.seek();
+            cons += 2;
+            store_rel(&Q.cons, cons);
+            PYAS_PROF(3);
             continue;
         }
-        const uint16_t *lit = L.lit, *dist = L.dist;
-        if (type == 1) {   // fixed codes (RFC 1951 3.2.6)
-            for (int s = lane; s < 320; s += 64)
-                L.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
-            __syncthreads();
-            build(L, 0, 288, L.lit_cnt, L.lit_sym, L.lit, kLitBits, false);
-            build(L, 288, 32, L.dist_cnt, L.dist_sym, L.dist, kDistBits, false);
-        } else if (type == 2) {   // dynamic codes
-            h = in.peek();
-            const uint32_t nlen = (h & 31u) + 257, ndist = ((h >> 5) & 31u) + 1, ncode = ((h >> 10) & 15u) + 4;
-            in.pos += 14;
-            if (nlen > 286 || ndist > 30) { status = PYAS_INFLATE_BAD_CODE; break; }
-            // code-length code: 3 bits per length in c_clen_order
-            h = in.peek();
-            const uint32_t h2 = [&] { in.pos += 30; const uint32_t r = in.peek(); in.pos -= 30; return r; }();
-            for (int s = lane; s < 19; s += 64) {
-                const uint32_t bit = 3u * (uint32_t)s;
-                uint32_t v = 0;
-                if ((uint32_t)s < ncode) v = bit < 30 ? (h >> bit) & 7u : (h2 >> (bit - 30)) & 7u;
-                L.lens[c_clen_order[s]] = (uint8_t)v;
-            }
-            in.pos += 3 * ncode;
-            __syncthreads();
-            // the code-length tree uses the distance table slots (7-bit codes)
-            if (build(L, 0, 19, L.dist_cnt, L.dist_sym, L.dist, 7, true)) { status = PYAS_INFLATE_BAD_CODE; break; }
-            // code lengths for literal/length + distance, serial (<= 316)
-            uint32_t k = 0;
-            uint32_t prev = 0;
-            while (k < nlen + ndist) {
-                const uint32_t bits = in.peek();
-                uint32_t l;
-                const uint32_t sym = decode(bits, L.dist, 7, L.dist_cnt, L.dist_sym, l);
-                if (!l) { status = PYAS_INFLATE_BAD_CODE; break; }
-                in.pos += l;
-                const uint32_t more = bits >> l;
-                uint32_t rep, val;
-                if (sym < 16) {
-                    rep = 1; val = sym; prev = sym;
-                } else if (sym == 16) {
-                    if (k == 0) { status = PYAS_INFLATE_BAD_CODE; break; }
-                    rep = 3 + (more & 3u); val = prev; in.pos += 2;
-                } else if (sym == 17) {
-                    rep = 3 + (more & 7u); val = 0; in.pos += 3;
-                } else {
-                    rep = 11 + (more & 127u); val = 0; in.pos += 7;
-                }
-                if (k + rep > nlen + ndist) { status = PYAS_INFLATE_BAD_CODE; break; }
-                if (sym > 16) prev = 0;   // zlib: repeat-previous after zeros repeats zero
-                for (uint32_t i = lane; i < rep; i += 64) {
-                    const uint32_t s = k + i;
-                    L.lens[s < nlen ? s : 288 + (s - nlen)] = (uint8_t)val;
-                }
-                k += rep;
-            }
-            if (status) break;
-            for (int s = nlen + lane; s < 288; s += 64) L.lens[s] = 0;
-            for (int s = 288 + (int)ndist + lane; s < 320; s += 64) L.lens[s] = 0;
-            __syncthreads();
-            if (L.lens[256] == 0) { status = PYAS_INFLATE_BAD_CODE; break; }
-            if (build(L, 0, 288, L.lit_cnt, L.lit_sym, L.lit, kLitBits, false) ||
-                build(L, 288, 32, L.dist_cnt, L.dist_sym, L.dist, kDistBits, false)) {
-                status = PYAS_INFLATE_BAD_CODE;
-                break;
-            }
-        } else {
-            status = PYAS_INFLATE_BAD_BLOCK;
-            break;
+        // this batch: the tokens before the first stored one, at most kBud
+        // output bytes (tokens are contiguous from o.pos)
+        uint32_t n = min(avail, 64u);
+        if (stored) n = min(n, (uint32_t)__builtin_ctzll(stored));
+        const uint32_t olen = len ? len : 1u;
+        const uint64_t over = __ballot(act && p + olen - o.pos > kBud);
+        if (over) n = min(n, (uint32_t)__builtin_ctzll(over));
+        const bool mine = (uint32_t)lane < n;
+        if (!mine) len = d = 0u;
+        const uint32_t src_b = p - d;
+        const bool far = mine && len && d > kFar;
+        const uint32_t need = mine && len ? min(src_b + len, p) : 0u;   // [src, need) must be written
+        bool done_t = !mine;
+        // far sources: issue their first 16 bytes now (flushed; ready at once)
+        Far16 fv;
+        const bool any_far = __ballot(far) != 0ull;
+        if (any_far) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's flush stores have landed
+            if (far) fv.load(o.dst + src_b, o.dst + o.fpos);
         }
-        // Match copy out[p+i] = out[p-d+(i mod d)], lane-parallel (all
-        // sources precede p); beyond the ring every source byte is in dst.
-        auto copy_match = [&](uint32_t d, uint32_t len) {
-            const uint32_t from = o.pos - d;
-            if (d > kWin) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                for (uint32_t r = 0; r < len; r += 64) {
-                    const uint32_t i = r + lane;
-                    if (i < len) win[(o.pos + i) & kWinMask] = (uint8_t)far_byte(o.dst + from + i);
+        PYAS_STAT(0, 1u);
+        PYAS_STAT(1, n);
+        for (;;) {
+            const uint64_t und = __ballot(!done_t);
+            if (!und) break;
+            PYAS_STAT(2, 1u);
+            const uint32_t W = rl(p, (uint32_t)__builtin_ctzll(und));
+            const bool ready = !done_t && need <= W;
+            if (ready && !len) win[p & kWinMask] = (uint8_t)d;
+            // short non-overlapping matches, one lane each: 16 source bytes
+            // from five ring dwords
+            const uint32_t ns = (ready && len && !far && len <= 16u && d >= len) ? len : 0u;
+            if (__ballot(ns != 0u)) {
+                const uint32_t wi = src_b >> 2, sh = src_b & 3u;
+                uint32_t r[5];
+#pragma unroll
+                for (uint32_t k = 0; k < 5; ++k) r[k] = win32[(wi + k) & (kWin / 4 - 1)];
+#pragma unroll
+                for (uint32_t k = 0; k < 16u; ++k) {
+                    if (!__ballot(k < ns)) break;
+                    const uint32_t qv = __builtin_amdgcn_alignbyte(r[(k >> 2) + 1], r[k >> 2], sh);
+                    if (k < ns) win[(p + k) & kWinMask] = (uint8_t)(qv >> (8 * (k & 3u)));
                 }
-            } else {
-                for (uint32_t r = 0; r < len; r += 64) {
-                    const uint32_t i = r + lane;
-                    if (i < len) {
-                        const uint32_t srcp = from + (d >= len ? i : i % d);
-                        win[(o.pos + i) & kWinMask] = win[srcp & kWinMask];
+            }
+            // far matches (ready in the first round): the prefetched 16 bytes,
+            // then 16-byte steps for longer ones
+            if (any_far && __ballot(ready && far)) {
+                PYAS_STAT(3, __builtin_popcountll(__ballot(ready && far)));
+                const uint32_t nf = (ready && far) ? len : 0u;
+#pragma unroll
+                for (uint32_t k = 0; k < 16u; ++k)
+                    if (k < nf) win[(p + k) & kWinMask] = (uint8_t)(fv.word((int)(k >> 2)) >> (8 * (k & 3u)));
+                for (uint32_t fo = 16; __ballot(fo < nf); fo += 16u) {
+                    if (fo < nf) {
+                        Far16 g;
+                        g.load(o.dst + src_b + fo, o.dst + o.fpos);
+                        const uint32_t m = min(nf - fo, 16u);
+#pragma unroll
+                        for (uint32_t k = 0; k < 16u; ++k)
+                            if (k < m) win[(p + fo + k) & kWinMask] = (uint8_t)(g.word((int)(k >> 2)) >> (8 * (k & 3u)));
                     }
                 }
             }
-            o.pos += len;
-        };
-        // A short match (len <= 64, source in the ring) is split: its ring
-        // read is issued at once, its write is deferred until the next ring
-        // read or flush, so the LDS round trip overlaps the decode of the
-        // symbols that follow (they only write later positions).
-        uint32_t pend_v = 0, pend_p = 0, pend_n = 0;
-        auto issue_pending = [&]() {
-            if (pend_n) {
-                if ((uint32_t)lane < pend_n) win[(pend_p + lane) & kWinMask] = (uint8_t)pend_v;
-                pend_n = 0;
+            // long or overlapping matches: the whole wave, one at a time
+            uint64_t coop = __ballot(ready && len && !far && (len > 16u || d < len));
+            PYAS_STAT(4, __builtin_popcountll(coop));
+            while (coop) {
+                const uint32_t t = (uint32_t)__builtin_ctzll(coop);
+                coop &= coop - 1ull;
+                wave_copy(rl(p, t), rl(d, t), rl(len, t));
             }
-        };
-        auto start_match = [&](uint32_t d, uint32_t len) {
-            issue_pending();
-            if (len <= 64 && d <= kWin) {
-                const uint32_t from = o.pos - d;
-                const uint32_t i = (uint32_t)lane < len ? (uint32_t)lane : 0u;
-                pend_v = win[(from + (d >= len ? i : i % d)) & kWinMask];
-                pend_p = o.pos;
-                pend_n = len;
-                o.pos += len;
-            } else {
-                copy_match(d, len);
-            }
-        };
-        // One symbol, any code length (canonical walk past the root tables).
-        // Returns 0 = continue, 1 = end of block, 2 = error (status set).
-        auto one_symbol = [&]() -> int {
-            issue_pending();
-            if (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
-            if (in.pos > in.nbits) { status = PYAS_INFLATE_TRUNCATED; return 2; }
-            uint32_t bits = in.peek();
-            uint32_t l;
-            uint32_t sym = decode(bits, lit, kLitBits, L.lit_cnt, L.lit_sym, l);
-            if (!l) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
-            if (sym < 256) {
-                if (o.pos >= o.cap) { status = PYAS_INFLATE_OVERFLOW; return 2; }
-                if (lane == 0) win[o.pos & kWinMask] = (uint8_t)sym;
-                o.pos++;
-                in.pos += l;
-                return 0;
-            }
-            if (sym == 256) { in.pos += l; return 1; }
-            sym -= 257;
-            if (sym >= 29) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
-            const uint32_t le = c_len_extra[sym];
-            const uint32_t len = c_len_base[sym] + ((bits >> l) & ((1u << le) - 1u));
-            in.pos += l + le;
-            bits = in.peek();
-            const uint32_t ds = decode(bits, dist, kDistBits, L.dist_cnt, L.dist_sym, l);
-            if (!l || ds >= 30) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
-            const uint32_t de = c_dist_extra[ds];
-            const uint32_t d = c_dist_base[ds] + ((bits >> l) & ((1u << de) - 1u));
-            in.pos += l + de;
-            if (d > o.pos) { status = PYAS_INFLATE_BAD_DISTANCE; return 2; }
-            if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; return 2; }
-            copy_match(d, len);
-            return 0;
-        };
-        // Symbol loop over speculative windows.  Lane k holds the 32 bits
-        // at pos + k and looks up both root tables there (one LDS round trip
-        // for the whole wave).
-        //
-        // Parallel walk (the common case): every lane decodes the symbol
-        // that WOULD start at its bit offset -- literal, or length plus the
-        // distance code read from lane k + l + le -- and its successor
-        // offset nxt.  Only the chain of successors from offset 0 is then
-        // walked on the scalar unit (one v_readlane per symbol); the chain's
-        // output offsets come from one wave prefix sum, its literals are
-        // written by their own lanes, and its matches are copied in order
-        // (literals between two matches are written before the later match
-        // reads the ring, as a serial decoder would).  A lane whose symbol
-        // cannot be finished inside the window ends the chain there: a code
-        // longer than its root table (one_symbol), end of block, or a
-        // distance code past the window (next window).  Anything else
-        // unusual -- an invalid symbol, truncated input, a distance before
-        // the output start, output past capacity -- sends the whole window
-        // to the serial walk below, which reports zlib's error at the right
-        // symbol.  At most kBudget output bytes per window keep the ring
-        // invariants of the serial decoder (unflushed bytes + window output
-        // fit the ring; a match source further back than the ring is
-        // already flushed to dst).
-        constexpr uint32_t kBudget = kWin / 4;
-        bool eob = false;
-        uint32_t windows_left = in.nbits + 64u;   // every window consumes input; a stuck walk ends here
-        while (!eob) {
-            PYAS_PROF(7);
-            if (windows_left-- == 0u) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
-            while (o.pos - o.fpos >= kFlush) {
-                issue_pending();
-                flush<kWinMask>(win, o, kFlush);
-            }
-            PYAS_PROF(5);
-            in.ensure();                                 // the ring holds the window
-            const uint32_t v = in.bits_at((uint32_t)lane);
-            const uint32_t E = lit[v & ((1u << kLitBits) - 1u)];
-            const uint32_t D = dist[v & ((1u << kDistBits) - 1u)];
-            auto rl = [](uint32_t x, uint32_t k) {
-                return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)k);
-            };
-            PYAS_PROF(0);
-
-            // ---- per-lane speculative symbol -------------------------------
-            enum : uint32_t { kLit = 0, kMatch = 1, kStop = 2 };
-            enum : uint32_t { rSlow = 1, rEob = 2, rNewWin = 3, rSerial = 4 };
-            const uint32_t l = E >> 9;
-            const uint32_t sym = E & 511u;
-            const uint32_t ls = sym - 257u;              // length symbol index (wraps for < 257)
-            const uint32_t le = (ls < 8u || ls == 28u) ? 0u : (ls - 4u) >> 2;
-            const uint32_t doff = (uint32_t)lane + l + le;
-            const uint32_t dsrc = doff < 64u ? doff : 63u;
-            const uint32_t f = (uint32_t)__shfl((int)D, (int)dsrc, 64);
-            const uint32_t vd = (uint32_t)__shfl((int)v, (int)dsrc, 64);
-            // every lane computes all fields; selects pick the symbol's kind
-            const uint32_t dl = f >> 9, ds = f & 511u;
-            const uint32_t lec = le < 5u ? le : 5u;
-            const uint32_t lbase = ls < 8u ? ls + 3u : ls == 28u ? 258u : ((4u + (ls & 3u)) << lec) + 3u;
-            const uint32_t de0 = ds < 4u ? 0u : (ds - 2u) >> 1;
-            const uint32_t de = de0 < 13u ? de0 : 13u;
-            const uint32_t dbase = ds < 4u ? ds + 1u : ((2u + (ds & 1u)) << de) + 1u;
-            const uint32_t mlen = lbase + ((v >> l) & ((1u << lec) - 1u));
-            const uint32_t mdist = dbase + ((vd >> dl) & ((1u << de) - 1u));
-            const bool trunc = in.pos + (uint32_t)lane > in.nbits;
-            const uint32_t why = trunc ? rSerial
-                               : !l ? rSlow
-                               : sym < 256u ? 0u
-                               : sym == 256u ? rEob
-                               : ls >= 29u ? rSerial
-                               : doff > 63u ? rNewWin
-                               : !dl ? rSlow
-                               : ds >= 30u ? rSerial : 0u;
-            const bool is_lit = why == 0u && sym < 256u;
-            const uint32_t kind = why ? kStop : is_lit ? kLit : kMatch;
-            const uint32_t olen = why ? 0u : is_lit ? 1u : mlen;
-            const uint32_t dd = mdist;
-            uint32_t nxt = is_lit ? (uint32_t)lane + l : doff + dl + de;
-            if (kind == kStop) nxt = 128u + why;         // >= 128: the chain stops here
-            PYAS_PROF(1);
-
-            // ---- the chain from offset 0 (scalar) --------------------------
-            uint64_t M = 0;
-            uint32_t off = 0, prev = 0, stop = 0;
-            do {
-                M |= 1ull << off;
-                prev = off;
-                off = rl(nxt, off);
-            } while (off < 64u);
-            if (off >= 128u) {                           // ended on a stop lane: not consumed
-                stop = off - 128u;
-                off = prev;
-                M &= ~(1ull << prev);
-            }
-            PYAS_PROF(2);
-            const bool on = (M >> lane) & 1ull;
-            const uint32_t incl = wave_incl_sum(on ? olen : 0u);   // output bytes up to this lane
-            const uint32_t excl = incl - (on ? olen : 0u);
-            uint32_t T = rl(incl, 63);
-            bool par = stop != rSerial || off > 0;
-            if (par && T > kBudget) {                    // end the window before the first symbol past it
-                const uint64_t over = __ballot(on && incl > kBudget);
-                const uint32_t cut = (uint32_t)__builtin_ctzll(over);
-                M &= (1ull << cut) - 1ull;
-                off = cut;
-                stop = 0;
-                T = rl(excl, cut);
-            }
-            const bool on2 = (M >> lane) & 1ull;
-            if (par) {
-                if (o.pos + T > o.cap) par = false;
-                if (__ballot(on2 && kind == kMatch && dd > o.pos + excl)) par = false;
-            }
-            PYAS_PROF(3);
-            if (par) {
-                issue_pending();
-                const uint32_t pos0 = o.pos;
-                uint64_t mm = __ballot(on2 && kind == kMatch);
-                PYAS_STAT(0, __builtin_popcountll(M));
-                PYAS_STAT(1, __builtin_popcountll(mm));
-                PYAS_STAT(2, __builtin_popcountll(__ballot(on2 && kind == kMatch && olen > 64u)));
-                PYAS_STAT(3, __builtin_popcountll(__ballot(on2 && kind == kMatch && dd < olen)));
-                PYAS_STAT(4, __builtin_popcountll(__ballot(on2 && kind == kMatch && dd < excl + 1u)));
-                PYAS_STAT(5, stop == rSlow ? 1u : 0u);
-                PYAS_STAT(6, T);
-                PYAS_STAT(7, __builtin_popcountll(__ballot(on2 && kind == kMatch && dd > kWin)));
-                (void)mm;
-                // The window's output, 64 positions per step, one per lane.
-                // Lane j takes position p = c + j: the symbol covering p is
-                // the last one starting at or before p (start marks in LDS,
-                // then a max scan).  A literal gives its byte.  A match byte
-                // p copies byte p - d: from the ring when p - d precedes this
-                // step (from dst when d exceeds the ring: those bytes are
-                // flushed), else from the lane producing p - d in this step;
-                // pointer jumping over those lanes ends at a lane whose byte
-                // is known (an overlapping match, d < len, chains this way).
-                const bool any_far = __ballot(on2 && kind == kMatch && dd > kWin) != 0;
-                if (any_far) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const uint32_t pk = (kind << 16) | (sym & 255u);
-                uint32_t carry = 0;                      // lane + 1 of the symbol covering position c
-                for (uint32_t c = 0; c < T; c += 64) {
-                    const uint32_t p = c + (uint32_t)lane;
-                    mark[lane] = 0;
-                    if (on2 && excl >= c && excl < c + 64u) mark[excl - c] = (uint8_t)(lane + 1);
-                    wave_lds_sync();                     // other lanes' marks (no store forwarding)
-                    uint32_t S = wave_incl_max(mark[lane]);
-                    S = S > carry ? S : carry;
-                    carry = rl(S, 63);
-                    const uint32_t k = (S - 1u) & 63u;
-                    const uint32_t s_d = (uint32_t)__shfl((int)dd, (int)k, 64);
-                    const uint32_t s_pk = (uint32_t)__shfl((int)pk, (int)k, 64);
-                    const bool valid = p < T;
-                    const bool is_m = (s_pk >> 16) == kMatch;
-                    const int32_t src = (int32_t)p - (int32_t)s_d;   // window-relative source
-                    const bool inner = is_m && src >= (int32_t)c;
-                    uint32_t val = s_pk & 255u;
-                    if (valid && is_m && !inner)
-                        val = s_d > kWin ? far_byte(o.dst + (pos0 + src)) : (uint32_t)win[(pos0 + src) & kWinMask];
-                    if (__ballot(valid && inner)) {
-                        // pd = lane whose byte this lane copies | 64 once that
-                        // lane's byte is known (a root); undone lanes jump
-                        // to their target's pd until every lane has a root
-                        uint32_t pd = inner ? (uint32_t)(src - (int32_t)c) : ((uint32_t)lane | 64u);
-                        while (__ballot(!(pd & 64u))) {
-                            const uint32_t q = (uint32_t)__shfl((int)pd, (int)(pd & 63u), 64);
-                            if (!(pd & 64u)) pd = q;
-                        }
-                        val = (uint32_t)__shfl((int)val, (int)(pd & 63u), 64);
-                    }
-                    if (valid) win[(pos0 + p) & kWinMask] = (uint8_t)val;
-                    wave_lds_sync();
-                }
-                o.pos = pos0 + T;
-                in.pos += off;
-                if (stop == rEob) {
-                    in.pos += rl(l, off);
-                    eob = true;
-                } else if (stop == rSlow) {
-                    const int r = one_symbol();
-                    if (r == 2) break;
-                    if (r == 1) eob = true;
-                }
-                // rNewWin / rSerial past offset 0 / budget cut: next window
-                PYAS_PROF(4);
-                continue;
-            }
-
-            // ---- serial walk of the same window ----------------------------
-            off = 0;
-            bool slow = false;
+            done_t = done_t || ready;
+            wave_lds_sync();
+            // a chain of long/overlapping matches each reading the one before
+            // (runs): take them in order by the whole wave
             for (;;) {
-                if (o.pos - o.fpos >= kFlush) {
-                    issue_pending();
-                    flush<kWinMask>(win, o, kFlush);
-                }
-                if (off > 63) break;
-                if (in.pos + off > in.nbits) { status = PYAS_INFLATE_TRUNCATED; break; }
-                const uint32_t e = rl(E, off);
-                const uint32_t el = e >> 9;
-                if (!el) { slow = true; break; }
-                uint32_t es = e & 511u;
-                if (es < 256) {
-                    if (o.pos >= o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
-                    if (lane == 0) win[o.pos & kWinMask] = (uint8_t)es;
-                    o.pos++;
-                    off += el;
-                    continue;
-                }
-                if (es == 256) { off += el; eob = true; break; }
-                es -= 257;
-                if (es >= 29) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
-                const uint32_t sle = (es < 8 || es == 28) ? 0u : (es - 4u) >> 2;
-                const uint32_t lbase = es < 8 ? es + 3u : es == 28 ? 258u : ((4u + (es & 3u)) << sle) + 3u;
-                const uint32_t sdoff = off + el + sle;
-                if (sdoff > 63) break;                   // next window starts at this symbol
-                const uint32_t len = lbase + ((rl(v, off) >> el) & ((1u << sle) - 1u));
-                const uint32_t sf = rl(D, sdoff);
-                const uint32_t dl = sf >> 9;
-                if (!dl) { slow = true; break; }         // long distance code
-                const uint32_t ds = sf & 511u;
-                if (ds >= 30) { status = PYAS_INFLATE_BAD_SYMBOL; break; }
-                const uint32_t de = ds < 4 ? 0u : (ds - 2u) >> 1;
-                const uint32_t dbase = ds < 4 ? ds + 1u : ((2u + (ds & 1u)) << de) + 1u;
-                const uint32_t d = dbase + ((rl(v, sdoff) >> dl) & ((1u << de) - 1u));
-                if (d > o.pos) { status = PYAS_INFLATE_BAD_DISTANCE; break; }
-                if (o.pos + len > o.cap) { status = PYAS_INFLATE_OVERFLOW; break; }
-                off = sdoff + dl + de;
-                start_match(d, len);
+                const uint64_t u2 = __ballot(!done_t);
+                if (!u2) break;
+                const uint32_t t = (uint32_t)__builtin_ctzll(u2);
+                const uint32_t tl = rl(len, t), td = rl(d, t);
+                if (!(tl > 16u || (tl && td < tl)) || td > kFar) break;
+                PYAS_STAT(5, 1u);
+                wave_copy(rl(p, t), td, tl);
+                done_t = done_t || (uint32_t)lane == t;
+                wave_lds_sync();
             }
-            if (status) break;
-            in.pos += off;
-            if (eob) break;
-            if (slow) {
-                const int r = one_symbol();
-                if (r == 2) break;
-                if (r == 1) eob = true;
-            }
-            PYAS_PROF(6);
         }
-        issue_pending();
-        if (status) break;
+        cons += n;
+        store_rel(&Q.cons, cons);
+        o.pos = rl(p, n - 1) + rl(olen, n - 1);
+        PYAS_PROF(1);
+        while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
+        PYAS_PROF(2);
     }
     if (status == 0) {
-        __syncthreads();
-        while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
-        if (o.pos > o.fpos) flush<kWinMask>(win, o, o.pos - o.fpos);
-        in.pos = (in.pos + 7) & ~7u;
-        if (in.pos + 32 > in.nbits) {
-            status = PYAS_INFLATE_TRUNCATED;
-        } else {
-            const uint32_t v = in.peek();
-            const uint32_t want = __builtin_bswap32(v);
-            if (want != ((o.b << 16) | o.a)) status = PYAS_INFLATE_BAD_CHECKSUM;
+        if (o.pos > o.fpos) {
+            wave_lds_sync();
+            while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
+            if (o.pos > o.fpos) flush<kWinMask>(win, o, o.pos - o.fpos);
         }
+        if (Q.adler != ((o.b << 16) | o.a)) status = PYAS_INFLATE_BAD_CHECKSUM;
     }
     if (lane == 0) {
         x.status[c] = status;
@@ -784,21 +878,59 @@ __global__ __launch_bounds__(64) void k_inflate(InflateArgs x) {
 #ifdef PYAS_INFLATE_PROF
     PYAS_PROF(7);
     if (c < 4 && lane == 0)
-    {
-        printf("inflate stream %d out %u windows %lu: setup %lu decode %lu walk %lu scan %lu write %lu flush %lu serial %lu other %lu\n",
-               (int)c, o.pos, pf_acc[8], pf_acc[0], pf_acc[1], pf_acc[2], pf_acc[3], pf_acc[4], pf_acc[5], pf_acc[6],
-               pf_acc[7]);
-        printf("inflate stream %d stats: symbols %lu matches %lu long %lu overlapping %lu src_in_window %lu slow %lu bytes %lu far %lu\n",
-               (int)c, pf_st[0], pf_st[1], pf_st[2], pf_st[3], pf_st[4], pf_st[5], pf_st[6], pf_st[7]);
-    }
+        printf("writer  %d out %u: wait %lu resolve %lu flush %lu stored %lu end %lu | batches %lu tokens %lu rounds %lu "
+               "far %lu coop %lu chain %lu\n",
+               (int)c, o.pos, pf_acc[0], pf_acc[1], pf_acc[2], pf_acc[3], pf_acc[7], pf_st[0], pf_st[1], pf_st[2],
+               pf_st[3], pf_st[4], pf_st[5]);
 #endif
+}
+
+}  // namespace
+
+// One stream per workgroup: wave 0 decodes, wave 1 writes.  NG bit-offset
+// groups per decoder window; 2^WBITS bytes of output ring.
+template <int WBITS, int NG>
+__global__ __launch_bounds__(128) void k_inflate(InflateArgs x) {
+    __shared__ Lds L;
+    __shared__ alignas(16) uint8_t win[1u << WBITS];
+    __shared__ uint32_t in_ring[kInRing];
+    __shared__ Queue Q;
+    const int64_t c = blockIdx.x;
+    if (threadIdx.x == 0) {
+        Q.prod = Q.cons = Q.done = 0u;
+        Q.status = 0;
+        Q.adler = 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) decoder<NG>(x, c, L, in_ring, Q);
+    else writer<WBITS>(x, c, win, Q);
+}
+
+// PYAS_INFLATE_NG: bit-offset groups per decoder window (1, 2 or 4).  Read
+// once per process.
+static int inflate_ng() {
+    static const int ng = [] {
+        const char *v = getenv("PYAS_INFLATE_NG");
+        const int g = v ? atoi(v) : 2;
+        return (g == 1 || g == 2 || g == 4) ? g : 2;
+    }();
+    return ng;
+}
+
+template <int WBITS>
+static void launch_ng(const InflateArgs &x, int64_t n, hipStream_t stream) {
+    switch (inflate_ng()) {
+    case 1: hipLaunchKernelGGL((k_inflate<WBITS, 1>), dim3((uint32_t)n), dim3(128), 0, stream, x); break;
+    case 4: hipLaunchKernelGGL((k_inflate<WBITS, 4>), dim3((uint32_t)n), dim3(128), 0, stream, x); break;
+    default: hipLaunchKernelGGL((k_inflate<WBITS, 2>), dim3((uint32_t)n), dim3(128), 0, stream, x); break;
+    }
 }
 
 hipError_t launch_inflate(const InflateArgs &x, int64_t n, int wbits, hipStream_t stream) {
     switch (wbits) {
-    case 15: hipLaunchKernelGGL(k_inflate<15>, dim3((uint32_t)n), dim3(64), 0, stream, x); break;
-    case 14: hipLaunchKernelGGL(k_inflate<14>, dim3((uint32_t)n), dim3(64), 0, stream, x); break;
-    default: hipLaunchKernelGGL(k_inflate<13>, dim3((uint32_t)n), dim3(64), 0, stream, x); break;
+    case 15: launch_ng<15>(x, n, stream); break;
+    case 14: launch_ng<14>(x, n, stream); break;
+    default: launch_ng<13>(x, n, stream); break;
     }
     return hipGetLastError();
 }
