@@ -370,17 +370,22 @@ int pyas_combine_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
  * Asynchronous like every launch: synchronise streams[k] before reading.
  * Bounded wait: with the environment variable PYAS_SHARD_TIMEOUT_MS set to
  * a number >= 0 the call instead waits for the exchange up to that many
- * milliseconds, polling the streams and ncclCommGetAsyncError; on expiry or
- * an RCCL error it aborts the device list's communicators (ncclCommAbort),
- * drops them from the cache and returns PYAS_EDEVICE naming the devices that
- * had not finished.
+ * milliseconds (0: one poll), polling the streams and ncclCommGetAsyncError.
+ * On an RCCL or stream error, or on expiry once every device has reached
+ * its collectives (a stalled peer), it aborts the device list's
+ * communicators (ncclCommAbort), drops them from the cache and returns
+ * PYAS_EDEVICE naming the devices that had not finished; the streams and
+ * out buffers of that call are then to be discarded.  On expiry while a
+ * device is still reducing (its collectives queued, not started) it keeps
+ * the communicators -- aborting would free them under queued RCCL kernels
+ * -- and returns PYAS_EDEVICE naming the busy devices; the exchange then
+ * completes on the streams.  Verified on hardware at ndev = 1.
  * Thread safety: calls on the same device list are serialised from group
  * start to group end (RCCL allows one group on a communicator at a time);
  * pyas_shard_release waits for a call still using a set.
- * Zero sign: a float min/max whose result is a zero keeps the sign the
- * device reduction gives; storage.py/active.py's +0.0/-0.0 rule is applied
- * by the per-device path (pyas_tie_chunks_total + pyas_tie_finalize) and by
- * pyactivestorage_amd.distributed, not by this entry.
+ * Zero sign: this entry returns the combined partial as the devices reduce
+ * it; pyas_reduce_sharded_tie below applies storage.py/active.py's
+ * +0.0/-0.0 rule (as pyactivestorage_amd.distributed does).
  * RCCL is resolved from the process first (an RCCL already mapped, e.g.
  * torch's), then librccl.so.1.
  * The multi-process equivalent (one process per GPU) is
@@ -388,6 +393,21 @@ int pyas_combine_partials(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in,
 int pyas_reduce_sharded(pyas_ctx *const *ctx, const pyas_batch *const *per_dev,
                         const pyas_mask *const *mask, int32_t ndev, uint32_t combine_flags,
                         pyas_partial *const *out, void *const *streams);
+/* pyas_reduce_sharded with NumPy's sign of a zero min (which = 1) or max
+ * (which = 2) of a float variable (storage.py:99-100 per chunk, active.py:594
+ * over the per-chunk results): device k's chunks are positions
+ * [sum of earlier devices' n_chunks, + n_chunks) of the query's chunk order
+ * (the `out` array); each device keeps its per-chunk partials (per-call
+ * scratch), keys its two candidate chunks (pyas_tie_chunks_total) and its
+ * total (pyas_tie_segments), the 16-byte keys travel in the same RCCL group
+ * as the totals, and every device applies pyas_tie_finalize to out[k][0].
+ * The tie rule of the dtype must be set on every ctx
+ * (pyas_ctx_set_tie_rule); without one, and for integer dtypes or which = 0,
+ * this is pyas_reduce_sharded.  `geom` as for pyas_tie_chunks. */
+int pyas_reduce_sharded_tie(pyas_ctx *const *ctx, const pyas_batch *const *per_dev,
+                            const pyas_mask *const *mask, int32_t ndev, uint32_t combine_flags,
+                            const pyas_tie_geom *geom, uint32_t which,
+                            pyas_partial *const *out, void *const *streams);
 /* Destroy the cached RCCL communicators of pyas_reduce_sharded (waits for a
  * call still using them). */
 int pyas_shard_release(void);

@@ -189,6 +189,7 @@ SIGNATURES = {
                             _vp, _vp, _vp],
     "pyas_combine_partials": [_vp, _i32, _vp, _i64, _u32, _vp, _vp],
     "pyas_reduce_sharded": [_vp, _vp, _vp, _i32, _u32, _vp, _vp],
+    "pyas_reduce_sharded_tie": [_vp, _vp, _vp, _i32, _u32, _vp, _u32, _vp, _vp],
     "pyas_shard_release": [],
     "pyas_combine_segments": [_vp, _i32, _vp, _vp, _vp, _i64, _u32, _vp, _vp],
     "pyas_combine_grid": [_vp, _i32, _vp, ctypes.POINTER(Grid), _u32, _vp, _vp],

@@ -148,3 +148,75 @@ def test_bounded_wait(gpu, monkeypatch):
     monkeypatch.delenv("PYAS_SHARD_TIMEOUT_MS")
     got = _sharded([gpu], [plan], [st])[0]
     assert got[0].tobytes() == want.tobytes()
+
+
+def _sharded_tie(ctxs, plans, streams, which, geom, flags=1):
+    n = len(ctxs)
+    outs = [DeviceBuffer(c, (n + 1) * _lib.PARTIAL_NBYTES) for c in ctxs]
+    lib = ctxs[0].lib
+    rc = lib.pyas_reduce_sharded_tie(
+        _arr(ctypes.c_void_p, [c.handle for c in ctxs]),
+        _arr(ctypes.c_void_p, [ctypes.addressof(p.batch) for p in plans]),
+        _arr(ctypes.c_void_p, [ctypes.addressof(p.mask_up.struct) for p in plans]),
+        n, flags, ctypes.addressof(geom), which, _arr(ctypes.c_void_p, [o.ptr for o in outs]),
+        _arr(ctypes.c_void_p, streams))
+    _lib.check(rc, "pyas_reduce_sharded_tie")
+    res = []
+    for c, o, s, p in zip(ctxs, outs, streams, plans):
+        host = np.zeros(n + 1, dtype=engine.partial_dtype(p.dtype))
+        c.d2h(host, o.ptr, s)
+        c.synchronize(s)
+        res.append(host)
+    return res
+
+
+@pytest.mark.parametrize("dt", ["<f4", "<f8"])
+@pytest.mark.parametrize("kind", ["min", "max"])
+@pytest.mark.parametrize("dens", [0.2, 0.002])
+def test_sharded_zero_sign(gpu, dt, kind, dens):
+    """pyas_reduce_sharded_tie gives a zero min/max NumPy's
+    sign (storage.py:99-100 per chunk, active.py:594 over the per-chunk
+    results), byte for byte against the oracle's reduce_chunk composed as
+    active.py does; at ndev = 1 here, and split over every visible GPU on a
+    multi-GPU node.  Without the sign (pyas_reduce_sharded) the value and
+    count are the same."""
+    from tests.test_gpu_zero_sign import _chunk, _reference_active, _variable
+    from pyactivestorage_amd.distributed import equal_ranges
+    from pyactivestorage_amd.zerosign import tie_rule
+    if tie_rule(dt) is None:
+        pytest.skip("no NumPy tie rule derived on this host")
+    rng = np.random.default_rng(11 + len(kind) + int(dens * 1000) + len(dt))
+    shape, chunks = (16, 24, 80), (4, 8, 20)
+    a = _chunk(rng, shape, np.dtype(dt), "min0" if kind == "min" else "max0", dens=dens, n_fill=10)
+    missing = (np.dtype(dt).type(-999.0), None, None, None)
+    var, data = _variable(a, chunks, {"_FillValue": np.array([-999.0], dtype=dt)})
+    data_of = lambda cc: data[var.chunk_index[cc][0]: var.chunk_index[cc][0] + var.chunk_index[cc][1]]
+    want = _reference_active(a, chunks, (slice(None),) * 3, (0, 1, 2), kind, missing, data_of)
+    wv = np.ma.getdata(want).reshape(-1)[0]
+    assert wv == 0                                    # the case the sign matters for
+    n = ctypes.c_int(0)
+    _lib.check(gpu.lib.pyas_device_count(ctypes.byref(n)), "pyas_device_count")
+    cb = int(np.prod(chunks)) * np.dtype(dt).itemsize
+    n_chunks = len(var.chunk_index)
+    host = np.frombuffer(data, dtype=np.uint8)
+    ctxs, plans, streams, keep = [], [], [], []
+    for k, (lo, hi) in enumerate(equal_ranges(n_chunks, max(1, n.value))):
+        c = get_context(k)
+        st = c.thread_stream()
+        d = DeviceBuffer(c, max((hi - lo) * cb, 16))
+        c.h2d(d.ptr, host[lo * cb: hi * cb], st)
+        c.synchronize(st)
+        plans.append(ReductionPlan(c, np.dtype(dt), chunks, d.ptr, np.arange(hi - lo, dtype=np.int64) * cb,
+                                   missing=missing, stream=st))
+        ctxs.append(c)
+        streams.append(st)
+        keep.append(d)
+    which = 1 if kind == "min" else 2
+    got = _sharded_tie(ctxs, plans, streams, which, plans[0].tie_geom())
+    plain = _sharded(ctxs, plans, streams) if dt == "<f4" else None
+    for r in got:
+        g = r[0][kind]
+        assert g == wv and np.signbit(g) == np.signbit(wv), (kind, dens, g, wv)
+        assert r[0].tobytes() == got[0][0].tobytes()
+        if plain is not None:
+            assert r[0]["count"] == plain[0][0]["count"] and r[0][kind] == plain[0][0][kind]
