@@ -120,9 +120,11 @@ def test_several_devices_equal_one(gpu):
 
 def test_bounded_wait(gpu, monkeypatch):
     """PYAS_SHARD_TIMEOUT_MS: with a deadline the call waits for the exchange;
-    a zero deadline on a stream still busy with a long reduce aborts the
-    communicators and returns PYAS_EDEVICE naming the device, and the next
-    call builds new communicators and succeeds."""
+    a zero deadline on a stream still busy with a long reduce returns
+    PYAS_EDEVICE naming the device, and -- its collective queued but not
+    started -- keeps the communicators (aborting would free them
+    under the queued RCCL kernel); the exchange completes on the stream and
+    the next call succeeds on the same communicators."""
     st = gpu.thread_stream()
     data, offsets = _data(gpu, st)
     plan = ReductionPlan(gpu, np.float32, CHUNKS, data.ptr, offsets, missing=MISSING, stream=st)
@@ -145,6 +147,11 @@ def test_bounded_wait(gpu, monkeypatch):
     assert rc == _lib.EDEVICE, rc
     msg = lib.pyas_last_error()
     assert b"did not finish" in msg and b"device(s) %d" % gpu.device in msg, msg
+    assert b"communicators were kept" in msg, msg
+    host = np.zeros(n + 1, dtype=engine.partial_dtype(np.float32))
+    gpu.d2h(host, outs[0].ptr, st)
+    gpu.synchronize(st)
+    assert host[0]["count"] == 256 * want["count"][0]   # the queued exchange finished
     monkeypatch.delenv("PYAS_SHARD_TIMEOUT_MS")
     got = _sharded([gpu], [plan], [st])[0]
     assert got[0].tobytes() == want.tobytes()
