@@ -593,6 +593,19 @@ int pyas_inflate(pyas_ctx *ctx, const uint8_t *src, const int64_t *src_offsets,
 int pyas_read_ranges(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offsets,
                      const int64_t *sizes, void *dst, const int64_t *dst_offsets,
                      int32_t threads, void *stream);
+/* pyas_read_ranges for zlib-compressed chunks inflated on the HOST: each
+ * range is one zlib stream (storage.py:119-120 through numcodecs.Zlib,
+ * hdf2numcodec.py:34-35) that the reader thread preads and inflates
+ * straight into its pinned staging slot; the inflated out_bytes are copied
+ * H2D to dst + dst_offsets[i].  status (host, n entries) receives a
+ * pyas_inflate_status per stream (PYAS_INFLATE_OVERFLOW also for an output
+ * shorter or longer than out_bytes); a failed stream's bytes in dst are
+ * undefined and the caller raises (re-running zlib gives zlib's message).
+ * Few streams inflate faster here than with pyas_inflate, whose per-stream
+ * rate is one serial DEFLATE decoder; Active picks the side per query. */
+int pyas_read_ranges_zlib(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offsets,
+                          const int64_t *sizes, void *dst, const int64_t *dst_offsets,
+                          int64_t out_bytes, int32_t *status, int32_t threads, void *stream);
 /* Staging ring of pyas_read_ranges: n_slots x slot_bytes of pinned host
  * memory (default 16 x 64 MiB; each slot is pinned on first use). */
 int pyas_ctx_set_ingest_slots(pyas_ctx *ctx, int32_t n_slots, int64_t slot_bytes);

@@ -200,6 +200,7 @@ SIGNATURES = {
     "pyas_unshuffle_chunks": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "pyas_inflate": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "pyas_read_ranges": [_vp, ctypes.c_int, _i64, _vp, _vp, _vp, _vp, _i32, _vp],
+    "pyas_read_ranges_zlib": [_vp, ctypes.c_int, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp],
     "pyas_ctx_set_ingest_slots": [_vp, _i32, _i64],
     "pyas_coalescer_create": [_vp, _i64, _i32, ctypes.POINTER(_vp)],
     "pyas_coalescer_destroy": [_vp],

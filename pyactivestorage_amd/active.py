@@ -40,7 +40,7 @@ from .batch import ReductionPlan, _all_full
 from .device import DeviceBuffer, get_context
 from .dtypes import native, sum_dtype
 from .indexing import OrthogonalIndexer
-from .ingest import read_ranges
+from .ingest import read_ranges, read_ranges_zlib
 from .inflate import InflateBatch, is_zlib, pack_streams
 from .masking import compile_missing
 from .storage import _decompress, _shuffle_sizes
@@ -213,6 +213,32 @@ def _unhold(store) -> None:
 # read -> inflate pipeline stages of a compressed query (PYAS_INFLATE_GROUPS)
 _INFLATE_GROUPS = int(os.environ.get("PYAS_INFLATE_GROUPS", "3"))
 
+# Where Active inflates zlib chunks when device_inflate="auto" (row f3).  One
+# pyas_inflate stream is one serial DEFLATE decoder (~135 MB/s, two waves per
+# stream), so the device finishes up to ~2048 streams in about one stream's
+# time, while the host inflates on its reader threads -- one per pinned
+# staging slot in flight, min(threads, 16) -- at zlib's per-core rate and
+# takes ceil(n / lanes) stream times: the device wins from about lanes x
+# (host rate / device rate) streams.  Measured on MI355X with
+# tools/bench_inflate_crossover.py (profiles/r06/crossover/);
+# PYAS_INFLATE_CROSSOVER overrides the streams per host lane below which the
+# host inflates.
+_INFLATE_CROSSOVER = float(os.environ.get("PYAS_INFLATE_CROSSOVER", "8"))
+_INGEST_LANES = 16   # pinned staging slots of pyas_read_ranges (ingest.py set_slots)
+
+
+def inflate_on_device(n_streams: int, threads: int, mode="auto") -> bool:
+    """The device/host choice for one query's zlib chunks: ``mode`` True /
+    False force it; "auto" inflates on the device from ``_INFLATE_CROSSOVER``
+    streams per host inflate lane (PYAS_ACTIVE_INFLATE=device|host overrides
+    "auto")."""
+    if mode == "auto":
+        mode = {"device": True, "host": False}.get(os.environ.get("PYAS_ACTIVE_INFLATE", ""), "auto")
+    if mode != "auto":
+        return bool(mode)
+    lanes = max(1, min(int(threads), _INGEST_LANES))
+    return n_streams >= _INFLATE_CROSSOVER * lanes
+
 
 def _pipeline_groups(sizes, n_groups):
     """Up to ``n_groups`` contiguous index ranges of about equal total size."""
@@ -253,7 +279,7 @@ class Active:
 
     def __init__(self, dataset, ncvar=None, axis=None, interface_type=None, max_threads: int = 30,
                  storage_options=None, active_storage_url=None, option_disable_chunk_cache=False,
-                 *, device: int = 0, device_inflate: bool = True, group=None, resident: bool = False):
+                 *, device: int = 0, device_inflate="auto", group=None, resident: bool = False):
         """``dataset``: a netCDF4/HDF5 file path with ``ncvar`` naming the
         variable (``active.py:185-280``: same signature, checks and errors),
         or a :class:`ChunkedVariable` (the reference accepts a pyfive
@@ -289,7 +315,12 @@ class Active:
         self._method = None
         self._max_threads = int(max_threads)
         self.device = device
-        self.device_inflate = bool(device_inflate)   # f3: zlib chunks inflate on the GPU
+        # f3: zlib chunks inflate on the GPU (True), on the host reader threads
+        # straight into the pinned ring (False), or whichever is faster for the
+        # query's stream count ("auto", inflate_on_device)
+        if device_inflate not in (True, False, "auto"):
+            raise ValueError(f"device_inflate must be True, False or 'auto'. Got {device_inflate!r}")
+        self.device_inflate = device_inflate
         # row (e): a torch.distributed process group (one process per GPU).
         # Each rank reads and reduces a contiguous range of the query's chunks
         # from its own GPU; one all-gather of the per-rank partial grids and a
@@ -515,7 +546,8 @@ class Active:
         ds = self.ds
         nbytes = int(np.prod(ds.chunks)) * ds.dtype.itemsize
 
-        device_inflate = self.device_inflate and is_zlib(compressor)
+        zlib_chunks = is_zlib(compressor)
+        device_inflate = zlib_chunks and inflate_on_device(len(coords), self._max_threads, self.device_inflate)
         ctx = get_context(self.device)
         st = ctx.thread_stream()
         stride = -(-nbytes // _ALIGN) * _ALIGN
@@ -526,8 +558,7 @@ class Active:
         if n == 0:
             buf = dst if dst is not None else DeviceBuffer(ctx, stride)
             return ctx, st, buf, doffs, self._fused_shuffle(filters)
-        native_io = ds.reader is None and ds.filename is not None and (
-            device_inflate or compressor is None)
+        native_io = ds.reader is None and ds.filename is not None and (zlib_chunks or compressor is None)
         if native_io:
             # f2: native pread ring -> pinned slots -> H2D, no Python per chunk
             foff = np.array([o for o, _ in infos], dtype=np.int64)
@@ -548,7 +579,11 @@ class Active:
                 copy_st = ctx.thread_aux_stream(0)
                 ctx.stream_wait(copy_st, st)      # order after prior work on st
                 batches = []
-                groups = _pipeline_groups(fsize, _INFLATE_GROUPS)
+                # one launch per ~2048 streams: below that a launch inflates
+                # every stream at once (a stream's time is the latency of one
+                # serial decoder), so splitting the read/inflate pipeline into
+                # launches would only queue them one after another
+                groups = _pipeline_groups(fsize, max(1, min(_INFLATE_GROUPS, -(-n // 2048))))
                 for g, (lo, hi) in enumerate(groups):
                     read_ranges(ctx, ds.filename, foff[lo:hi], fsize[lo:hi], src.ptr, soffs[lo:hi],
                                 copy_st, self._max_threads)
@@ -562,6 +597,13 @@ class Active:
                     ib.check(inf_st, base=lo)
                     ctx.stream_wait(st, inf_st)
                 del src
+            elif zlib_chunks:
+                # f3 on the host: the reader threads inflate each chunk straight
+                # into its pinned staging slot (pyas_read_ranges_zlib), the
+                # inflated bytes go H2D
+                buf = dst if dst is not None else DeviceBuffer(ctx, max(n, 1) * stride)
+                read_ranges_zlib(ctx, ds.filename, foff, fsize, buf.ptr, doffs, nbytes, st, self._max_threads,
+                                 reshape=(ds.dtype.itemsize, ds.chunks))
             else:
                 bad = np.nonzero(fsize != nbytes)[0]
                 if bad.size:   # storage.py:57-62 reshape of a wrongly sized chunk

@@ -343,6 +343,17 @@ int pyas_read_ranges(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offse
     return rc ? fail(rc, "%s", msg.c_str()) : PYAS_OK;
 }
 
+int pyas_read_ranges_zlib(pyas_ctx *ctx, int fd, int64_t n, const int64_t *file_offsets,
+                          const int64_t *sizes, void *dst, const int64_t *dst_offsets, int64_t out_bytes,
+                          int32_t *status, int32_t threads, void *stream) {
+    if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
+    if (out_bytes <= 0) return fail(PYAS_EINVAL, "out_bytes must be > 0");
+    std::string msg;
+    const int rc = pyas::ingest_read(ingest_of(ctx), fd, n, file_offsets, sizes, (uint8_t *)dst,
+                                     dst_offsets, threads, (hipStream_t)stream, msg, out_bytes, status);
+    return rc ? fail(rc, "%s", msg.c_str()) : PYAS_OK;
+}
+
 int pyas_ctx_set_tie_rule(pyas_ctx *ctx, int32_t dtype, const pyas_tie_rule *rule) {
     if (!ctx) return fail(PYAS_EINVAL, "ctx is NULL");
     if (dtype != PYAS_F32 && dtype != PYAS_F64) return fail(PYAS_EINVAL, "tie rules are for f32/f64");

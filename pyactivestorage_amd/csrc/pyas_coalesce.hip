@@ -65,29 +65,6 @@ int64_t now_ns() {
                std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// zlib.decompress of one stream (RFC 1950) into exactly `cap` bytes of dst
-// (storage.py:119-120 through numcodecs.Zlib): a pyas_inflate_status; any
-// failure sends the call back to the per-call path, which raises zlib's own
-// error.  Bytes after the stream's end are ignored, as zlib.decompress does.
-int host_inflate(const uint8_t *src, int64_t n_src, uint8_t *dst, int64_t cap, int64_t &n_out) {
-    z_stream zs;
-    std::memset(&zs, 0, sizeof(zs));
-    n_out = 0;
-    if (inflateInit(&zs) != Z_OK) return PYAS_INFLATE_BAD_HEADER;
-    zs.next_in = const_cast<Bytef *>(src);
-    zs.avail_in = (uInt)n_src;
-    zs.next_out = dst;
-    zs.avail_out = (uInt)cap;
-    const int r = inflate(&zs, Z_FINISH);
-    n_out = (int64_t)zs.total_out;
-    int st = PYAS_INFLATE_OK;
-    if (r == Z_NEED_DICT) st = PYAS_INFLATE_NEED_DICT;
-    else if (r == Z_DATA_ERROR) st = PYAS_INFLATE_BAD_CODE;
-    else if (r != Z_STREAM_END) st = zs.avail_out == 0 ? PYAS_INFLATE_OVERFLOW : PYAS_INFLATE_TRUNCATED;
-    inflateEnd(&zs);
-    return st;
-}
-
 int es_of(int dtype) {
     switch (dtype) {
         case PYAS_I8: case PYAS_U8: return 1;
@@ -750,7 +727,7 @@ int pyas_coalesced_reduce(pyas_coalescer *c, const char *path, int64_t offset, i
     bool inflated = true;
     if (inflate_here && got == size && !read_errno) {
         int64_t n_dec = 0;
-        const int zst = host_inflate(zbuf.data(), size, c->hring + off, r.chunk_bytes, n_dec);
+        const int zst = pyas::host_inflate(zbuf.data(), size, c->hring + off, r.chunk_bytes, n_dec);
         info[1] = zst;
         info[2] = n_dec;
         inflated = zst == PYAS_INFLATE_OK && n_dec == r.chunk_bytes;

@@ -227,9 +227,13 @@ __device__ int build(Lds &L, int first, int n, uint16_t *cnt, uint16_t *sorted, 
         L.status = status;
     }
     wave_lds_sync();
+    // end of block and the invalid symbols (literal/length 286-287, distance
+    // 30-31) get no root entry: they take the canonical walk, so a root hit
+    // is always an ordinary literal, length or distance
+    const int n_fast = kind == 1 ? 286 : kind == 2 ? 30 : n;
     for (int s = lane; s < n; s += 64) {
         const int l = L.lens[first + s];
-        if (l && l <= P) {
+        if (l && l <= P && s < n_fast && !(kind == 1 && s == 256)) {
             const uint32_t rc = __builtin_bitreverse32((uint32_t)L.code[s]) >> (32 - l);
             const uint32_t e = (uint32_t)s | ((uint32_t)l << 9) | sym_fields(kind, (uint32_t)s);
             for (uint32_t k = rc; k < (1u << P); k += 1u << l) tab[k] = e;
@@ -464,7 +468,7 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
             uint32_t dw[2 * NG + 1];
 #pragma unroll
             for (int i = 0; i < 2 * NG + 1; ++i) dw[i] = in_ring[(k0 + (uint32_t)i) & (kInRing - 1)];
-            uint32_t nxt[NG], olen[NG], tw[NG], mdist[NG];
+            uint32_t nxt[NG], olen[NG], tw[NG];
 #pragma unroll
             for (int j = 0; j < NG; ++j) {
                 const uint32_t lo = __builtin_amdgcn_alignbit(dw[2 * j + 1], dw[2 * j], sh);
@@ -479,11 +483,10 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
                 const uint32_t md = dbase + ((db >> dl) & ((1u << de) - 1u));
                 const uint32_t off = 64u * (uint32_t)j + (uint32_t)lane;
                 const bool is_lit = sym < 256u;
-                const bool stop = in.pos + off > in.nbits || !l || sym == 256u || sym >= 286u ||
-                                  (!is_lit && (!dl || ds >= 30u));
+                (void)ds;
+                const bool stop = in.pos + off > in.nbits || !l || (!is_lit && !dl);
                 nxt[j] = stop ? kStop : is_lit ? off + l : off + s1 + dl + de;
                 olen[j] = is_lit ? 1u : ml;
-                mdist[j] = is_lit ? 0u : md;
                 tw[j] = is_lit ? sym : (ml << 16) | md;
             }
             PYAS_PROF(0);
@@ -529,15 +532,24 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
             // the first chain symbol reaching before the output start or past
             // the capacity ends the chain (the serial decoder reports it)
             uint32_t cut = kStop, T = tot;
+            bool bad_any = false;
 #pragma unroll
             for (int j = 0; j < NG; ++j) {
-                const bool on = (M[j] >> lane) & 1ull;
                 const uint32_t a = q + excl[j];
-                const uint64_t b = __ballot(on && (a + olen[j] > cap || mdist[j] > a));
-                if (b && cut == kStop) {
-                    const uint32_t cc = (uint32_t)__builtin_ctzll(b);
-                    cut = 64u * (uint32_t)j + cc;
-                    T = rl(excl[j], cc);
+                bad_any = bad_any || (((M[j] >> lane) & 1ull) &&
+                                      (a + olen[j] > cap || (olen[j] > 1u && (tw[j] & 0xffffu) > a)));
+            }
+            if (__ballot(bad_any)) {   // rare: find the first such symbol in chain order
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    const bool on = (M[j] >> lane) & 1ull;
+                    const uint32_t a = q + excl[j];
+                    const uint64_t b = __ballot(on && (a + olen[j] > cap || (olen[j] > 1u && (tw[j] & 0xffffu) > a)));
+                    if (b && cut == kStop) {
+                        const uint32_t cc = (uint32_t)__builtin_ctzll(b);
+                        cut = 64u * (uint32_t)j + cc;
+                        T = rl(excl[j], cc);
+                    }
                 }
             }
             if (cut != kStop) {
@@ -692,27 +704,34 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
 
     // Whole-wave copy of one match (tp, td, tl): every source byte lies before
     // tp (td >= tl) or repeats the period [tp - td, tp) (td < tl).
+    // (All reads are issued unconditionally -- ring indices are masked -- so
+    // they are in flight together; the writes are predicated.)
     auto wave_copy = [&](uint32_t tp, uint32_t td, uint32_t tl) {
         const uint32_t ts = tp - td;
-        uint32_t v[5];
-        if (td >= tl) {
-#pragma unroll
-            for (uint32_t k = 0; k < 5u; ++k)
-                if (64u * k < tl) v[k] = win[(ts + (uint32_t)lane + 64u * k) & kWinMask];
-        } else {
-            const uint32_t r64 = 64u % td;
-            uint32_t m = (uint32_t)lane % td;
-#pragma unroll
-            for (uint32_t k = 0; k < 5u; ++k) {
-                if (64u * k < tl) v[k] = win[(ts + m) & kWinMask];
-                m += r64;
-                m = m >= td ? m - td : m;
-            }
+        uint32_t m = (uint32_t)lane, r64 = 64u;
+        if (td < tl) {
+            r64 = 64u % td;
+            m = (uint32_t)lane % td;
         }
+        if (tl <= 64u) {
+            const uint32_t v = win[(ts + m) & kWinMask];
+            if ((uint32_t)lane < tl) win[(tp + (uint32_t)lane) & kWinMask] = (uint8_t)v;
+            return;
+        }
+        uint32_t idx[5];
+#pragma unroll
+        for (uint32_t k = 0; k < 5u; ++k) {
+            idx[k] = ts + m;
+            m += r64;
+            m = (td < tl && m >= td) ? m - td : m;
+        }
+        uint32_t v[5];
+#pragma unroll
+        for (uint32_t k = 0; k < 5u; ++k) v[k] = win[idx[k] & kWinMask];
 #pragma unroll
         for (uint32_t k = 0; k < 5u; ++k) {
             const uint32_t ii = (uint32_t)lane + 64u * k;
-            if (64u * k < tl && ii < tl) win[(tp + ii) & kWinMask] = (uint8_t)v[k];
+            if (ii < tl) win[(tp + ii) & kWinMask] = (uint8_t)v[k];
         }
     };
 
@@ -730,6 +749,11 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
             break;
         }
         if (prod == cons) break;   // done, every token written
+#ifdef PYAS_INFLATE_DECODE_ONLY
+        cons = prod;               // diagnostic: the decoder alone
+        store_rel(&Q.cons, cons);
+        continue;
+#endif
         const uint32_t avail = prod - cons;
         const bool act = (uint32_t)lane < avail;
         const uint32_t slot = (cons + (uint32_t)lane) & (kQ - 1);
@@ -791,6 +815,7 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
         }
         PYAS_STAT(0, 1u);
         PYAS_STAT(1, n);
+        PYAS_PROF(1);
         for (;;) {
             const uint64_t und = __ballot(!done_t);
             if (!und) break;
@@ -813,6 +838,7 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
                     if (k < ns) win[(p + k) & kWinMask] = (uint8_t)(qv >> (8 * (k & 3u)));
                 }
             }
+            PYAS_PROF(4);
             // far matches (ready in the first round): the prefetched 16 bytes,
             // then 16-byte steps for longer ones
             if (any_far && __ballot(ready && far)) {
@@ -832,6 +858,7 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
                     }
                 }
             }
+            PYAS_PROF(5);
             // long or overlapping matches: the whole wave, one at a time
             uint64_t coop = __ballot(ready && len && !far && (len > 16u || d < len));
             PYAS_STAT(4, __builtin_popcountll(coop));
@@ -842,19 +869,28 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
             }
             done_t = done_t || ready;
             wave_lds_sync();
-            // a chain of long/overlapping matches each reading the one before
-            // (runs): take them in order by the whole wave
-            for (;;) {
+            // the first token not written is ready now; tokens that read the
+            // one before them (runs of long/overlapping matches, and short
+            // ones) are taken in order by the whole wave -- any number of long
+            // or overlapping ones, up to kHead others -- before the next
+            // parallel round
+            constexpr uint32_t kHead = 4;
+            for (uint32_t h = 0;;) {
                 const uint64_t u2 = __ballot(!done_t);
                 if (!u2) break;
                 const uint32_t t = (uint32_t)__builtin_ctzll(u2);
                 const uint32_t tl = rl(len, t), td = rl(d, t);
-                if (!(tl > 16u || (tl && td < tl)) || td > kFar) break;
+                const bool longish = tl > 16u || (tl && td < tl);
+                if (td > kFar || (!longish && h == kHead)) break;
+                h += longish ? 0u : 1u;
                 PYAS_STAT(5, 1u);
-                wave_copy(rl(p, t), td, tl);
+                const uint32_t tp = rl(p, t);
+                if (tl) wave_copy(tp, td, tl);
+                else if ((uint32_t)lane == t) win[tp & kWinMask] = (uint8_t)td;
                 done_t = done_t || (uint32_t)lane == t;
                 wave_lds_sync();
             }
+            PYAS_PROF(6);
         }
         cons += n;
         store_rel(&Q.cons, cons);
@@ -878,10 +914,10 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
 #ifdef PYAS_INFLATE_PROF
     PYAS_PROF(7);
     if (c < 4 && lane == 0)
-        printf("writer  %d out %u: wait %lu resolve %lu flush %lu stored %lu end %lu | batches %lu tokens %lu rounds %lu "
-               "far %lu coop %lu chain %lu\n",
-               (int)c, o.pos, pf_acc[0], pf_acc[1], pf_acc[2], pf_acc[3], pf_acc[7], pf_st[0], pf_st[1], pf_st[2],
-               pf_st[3], pf_st[4], pf_st[5]);
+        printf("writer  %d out %u: wait %lu setup %lu lit+short %lu far %lu coop+chain %lu flush %lu stored %lu end %lu | "
+               "batches %lu tokens %lu rounds %lu far %lu coop %lu chain %lu\n",
+               (int)c, o.pos, pf_acc[0], pf_acc[1], pf_acc[4], pf_acc[5], pf_acc[6], pf_acc[2], pf_acc[3], pf_acc[7],
+               pf_st[0], pf_st[1], pf_st[2], pf_st[3], pf_st[4], pf_st[5]);
 #endif
 }
 
@@ -911,8 +947,8 @@ __global__ __launch_bounds__(128) void k_inflate(InflateArgs x) {
 static int inflate_ng() {
     static const int ng = [] {
         const char *v = getenv("PYAS_INFLATE_NG");
-        const int g = v ? atoi(v) : 2;
-        return (g == 1 || g == 2 || g == 4) ? g : 2;
+        const int g = v ? atoi(v) : 4;
+        return (g == 1 || g == 2 || g == 4) ? g : 4;
     }();
     return ng;
 }
@@ -921,8 +957,8 @@ template <int WBITS>
 static void launch_ng(const InflateArgs &x, int64_t n, hipStream_t stream) {
     switch (inflate_ng()) {
     case 1: hipLaunchKernelGGL((k_inflate<WBITS, 1>), dim3((uint32_t)n), dim3(128), 0, stream, x); break;
-    case 4: hipLaunchKernelGGL((k_inflate<WBITS, 4>), dim3((uint32_t)n), dim3(128), 0, stream, x); break;
-    default: hipLaunchKernelGGL((k_inflate<WBITS, 2>), dim3((uint32_t)n), dim3(128), 0, stream, x); break;
+    case 2: hipLaunchKernelGGL((k_inflate<WBITS, 2>), dim3((uint32_t)n), dim3(128), 0, stream, x); break;
+    default: hipLaunchKernelGGL((k_inflate<WBITS, 4>), dim3((uint32_t)n), dim3(128), 0, stream, x); break;
     }
 }
 

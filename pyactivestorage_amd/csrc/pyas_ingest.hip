@@ -12,6 +12,7 @@
 // after that slot's previous copy.
 #include <errno.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
@@ -25,6 +26,30 @@
 #include "pyas_internal.hpp"
 
 namespace pyas {
+
+// zlib.decompress of one stream (storage.py:119-120 through numcodecs.Zlib,
+// hdf2numcodec.py:34-35) into at most `cap` bytes of dst: a
+// pyas_inflate_status.  Bytes after the stream's end are ignored, as
+// zlib.decompress does; the caller re-runs a failed stream through zlib to
+// raise zlib's own error.
+int host_inflate(const uint8_t *src, int64_t n_src, uint8_t *dst, int64_t cap, int64_t &n_out) {
+    z_stream zs;
+    std::memset(&zs, 0, sizeof(zs));
+    n_out = 0;
+    if (inflateInit(&zs) != Z_OK) return PYAS_INFLATE_BAD_HEADER;
+    zs.next_in = const_cast<Bytef *>(src);
+    zs.avail_in = (uInt)n_src;
+    zs.next_out = dst;
+    zs.avail_out = (uInt)cap;
+    const int r = inflate(&zs, Z_FINISH);
+    n_out = (int64_t)zs.total_out;
+    int st = PYAS_INFLATE_OK;
+    if (r == Z_NEED_DICT) st = PYAS_INFLATE_NEED_DICT;
+    else if (r == Z_DATA_ERROR) st = PYAS_INFLATE_BAD_CODE;
+    else if (r != Z_STREAM_END) st = zs.avail_out == 0 ? PYAS_INFLATE_OVERFLOW : PYAS_INFLATE_TRUNCATED;
+    inflateEnd(&zs);
+    return st;
+}
 
 namespace {
 
@@ -126,13 +151,18 @@ static int pread_full(int fd, uint8_t *dst, int64_t size, int64_t off) {
 
 int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const int64_t *sizes,
                 uint8_t *dst, const int64_t *dst_offsets, int32_t threads, hipStream_t st,
-                std::string &msg) {
+                std::string &msg, int64_t zlib_out, int32_t *status) {
     std::lock_guard<std::mutex> lk(g->call_mu);
     if (n < 0 || (n > 0 && (!file_offsets || !sizes || !dst || !dst_offsets))) {
         msg = "read_ranges: NULL array or negative count";
         return PYAS_EINVAL;
     }
     if (fd < 0) { msg = "read_ranges: invalid file descriptor"; return PYAS_EINVAL; }
+    if (zlib_out < 0 || (zlib_out > 0 && !status)) { msg = "read_ranges: zlib output size or status"; return PYAS_EINVAL; }
+    if (zlib_out > g->slot_bytes) {
+        msg = "read_ranges: inflated chunk larger than a staging slot (pyas_ctx_set_ingest_slots)";
+        return PYAS_ENOTSUP;
+    }
     if (threads < 1) threads = 1;
     if (threads > 64) threads = 64;
     // ranges -> pieces of at most one slot -> groups (one slot each)
@@ -143,20 +173,35 @@ int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const
             msg = "read_ranges: negative offset or size at range " + std::to_string(i);
             return PYAS_EINVAL;
         }
+        if (zlib_out) {   // one piece per stream: its inflated bytes fill the slot space
+            status[i] = PYAS_INFLATE_OK;
+            pieces.push_back({file_offsets[i], sizes[i], dst_offsets[i], 0});
+            continue;
+        }
         for (int64_t p = 0; p < sizes[i]; p += g->slot_bytes)
             pieces.push_back({file_offsets[i] + p, std::min(g->slot_bytes, sizes[i] - p), dst_offsets[i] + p, 0});
     }
+    auto footprint = [&](const Piece &pc) { return zlib_out ? zlib_out : pc.size; };
     if (pieces.empty()) return PYAS_OK;
+    // a group fills one slot; in zlib mode the inflating is the work, so
+    // the streams are spread over as many groups as can be in flight at once
+    // (one per slot, one reader thread each)
+    int64_t group_cap = g->slot_bytes;
+    if (zlib_out) {
+        const int64_t lanes = std::max<int64_t>(1, std::min<int64_t>(threads, g->n_slots));
+        const int64_t per = (n + lanes - 1) / lanes;
+        group_cap = std::min<int64_t>(g->slot_bytes, std::max<int64_t>(1, per) * zlib_out);
+    }
     std::vector<Group> groups;
     {
         Group cur{0, 0, 0};
         for (size_t k = 0; k < pieces.size(); ++k) {
-            if (cur.count && cur.bytes + pieces[k].size > g->slot_bytes) {
+            if (cur.count && cur.bytes + footprint(pieces[k]) > group_cap) {
                 groups.push_back(cur);
                 cur = Group{k, 0, 0};
             }
             pieces[k].slot_off = cur.bytes;
-            cur.bytes += pieces[k].size;
+            cur.bytes += footprint(pieces[k]);
             cur.count++;
         }
         groups.push_back(cur);
@@ -177,6 +222,7 @@ int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const
 
     auto worker = [&]() {
         (void)hipSetDevice(g->device);
+        std::vector<uint8_t> zbuf;   // this thread's compressed bytes (zlib mode)
         for (;;) {
             const int64_t gi = next.fetch_add(1);
             if (gi >= G || err_code.load()) break;
@@ -198,8 +244,20 @@ int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const
             int rc = 0;
             size_t bad = 0;
             for (size_t k = gr.first; k < gr.first + gr.count && !rc; ++k) {
-                rc = pread_full(fd, slot + pieces[k].slot_off, pieces[k].size, pieces[k].file_off);
                 bad = k;
+                if (!zlib_out) {
+                    rc = pread_full(fd, slot + pieces[k].slot_off, pieces[k].size, pieces[k].file_off);
+                    continue;
+                }
+                // zlib: pread the stream, inflate it on this thread straight
+                // into the pinned slot
+                if ((int64_t)zbuf.size() < pieces[k].size) zbuf.resize((size_t)pieces[k].size);
+                rc = pread_full(fd, zbuf.data(), pieces[k].size, pieces[k].file_off);
+                if (rc) break;
+                int64_t n_out = 0;
+                int zs = host_inflate(zbuf.data(), pieces[k].size, slot + pieces[k].slot_off, zlib_out, n_out);
+                if (zs == PYAS_INFLATE_OK && n_out != zlib_out) zs = PYAS_INFLATE_OVERFLOW;
+                status[k] = zs;   // pieces are the streams, in order
             }
             std::lock_guard<std::mutex> l(mu);
             if (rc) {
@@ -215,10 +273,10 @@ int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const
             size_t k = gr.first;
             while (k < gr.first + gr.count && e == hipSuccess) {
                 size_t j = k + 1;
-                int64_t len = pieces[k].size;
+                int64_t len = footprint(pieces[k]);
                 while (j < gr.first + gr.count && pieces[j].dst_off == pieces[k].dst_off + len &&
                        pieces[j].slot_off == pieces[k].slot_off + len) {
-                    len += pieces[j].size;
+                    len += footprint(pieces[j]);
                     ++j;
                 }
                 e = hipMemcpyAsync(dst + pieces[k].dst_off, slot + pieces[k].slot_off, (size_t)len,

@@ -251,9 +251,15 @@ struct Ingest;
 Ingest *ingest_create(int device);
 void ingest_destroy(Ingest *g);
 int ingest_configure(Ingest *g, int32_t n_slots, int64_t slot_bytes, std::string &msg);
+// zlib_out > 0: every range is a zlib stream inflated on the reader thread
+// into exactly zlib_out bytes of its staging slot (status[i] != 0 when it is
+// not: a pyas_inflate_status, or PYAS_INFLATE_OVERFLOW for a short output).
 int ingest_read(Ingest *g, int fd, int64_t n, const int64_t *file_offsets, const int64_t *sizes,
                 uint8_t *dst, const int64_t *dst_offsets, int32_t threads, hipStream_t st,
-                std::string &msg);
+                std::string &msg, int64_t zlib_out = 0, int32_t *status = nullptr);
+// zlib.decompress of one stream (RFC 1950) into at most `cap` bytes of dst;
+// a pyas_inflate_status, n_out = bytes written (pyas_ingest.hip).
+int host_inflate(const uint8_t *src, int64_t n_src, uint8_t *dst, int64_t cap, int64_t &n_out);
 
 // pyas_capi.hip: the thread-local pyas_last_error() message, and the device a
 // context is bound to (for runtime pieces in other translation units)

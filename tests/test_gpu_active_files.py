@@ -24,7 +24,24 @@ def P(name):
     return os.path.join(NC, name)
 
 
-def test_known_answers_from_files(gpu):
+def test_inflate_choice():
+    """Active's device/host inflate choice (row f3): forced either way, or
+    by stream count against the measured crossover (active.py
+    inflate_on_device)."""
+    from pyactivestorage_amd import active as A
+    assert A.inflate_on_device(1, 30, True) and not A.inflate_on_device(10_000, 30, False)
+    n_cross = A._INFLATE_CROSSOVER * min(30, A._INGEST_LANES)
+    assert not A.inflate_on_device(int(n_cross) - 1, 30, "auto")
+    assert A.inflate_on_device(int(n_cross) + 1, 30, "auto")
+    with pytest.raises(ValueError):
+        Active(P("test1.nc"), "tas", device_inflate="gpu")
+
+
+@pytest.mark.parametrize("inflate", ["device", "host"])
+def test_known_answers_from_files(gpu, inflate, monkeypatch):
+    """zlib chunks inflated by pyas_inflate and by the host reader threads
+    (pyas_read_ranges_zlib) give the reference's literals alike."""
+    monkeypatch.setenv("PYAS_ACTIVE_INFLATE", inflate)
     a = Active(P("cesm2_native.nc"), "TREFHT")             # test_bigger_data.py:261-284
     a.method = "mean"
     a.components = True
@@ -47,8 +64,9 @@ def test_known_answers_from_files(gpu):
     assert a[0:2, 4:6, 7:9] == 124.0
 
 
+@pytest.mark.parametrize("inflate", [True, False, "auto"])
 @pytest.mark.parametrize("key", ["test1.nc:tas", "cesm2_native.nc:TREFHT", "CMIP6-test.nc:tas"])
-def test_file_path_equals_variable_path(gpu, key):
+def test_file_path_equals_variable_path(gpu, key, inflate):
     f, name = key.split(":")
     v = variable(key)
     nd = len(v.shape)
@@ -56,6 +74,6 @@ def test_file_path_equals_variable_path(gpu, key):
         for method in ("mean", "min", "max"):
             index = tuple(slice(n // 4, n) for n in v.shape)
             want = getattr(Active(v), method)(axis=axis)[index]
-            got = getattr(Active(P(f), name), method)(axis=axis)[index]
+            got = getattr(Active(P(f), name, device_inflate=inflate), method)(axis=axis)[index]
             np.testing.assert_array_equal(np.ma.getmaskarray(got), np.ma.getmaskarray(want))
             np.testing.assert_array_equal(np.ma.getdata(got), np.ma.getdata(want))
