@@ -223,7 +223,7 @@ _INFLATE_GROUPS = int(os.environ.get("PYAS_INFLATE_GROUPS", "3"))
 # tools/bench_inflate_crossover.py (profiles/r06/crossover/);
 # PYAS_INFLATE_CROSSOVER overrides the streams per host lane below which the
 # host inflates.
-_INFLATE_CROSSOVER = float(os.environ.get("PYAS_INFLATE_CROSSOVER", "8"))
+_INFLATE_CROSSOVER = float(os.environ.get("PYAS_INFLATE_CROSSOVER", "10"))
 _INGEST_LANES = 16   # pinned staging slots of pyas_read_ranges (ingest.py set_slots)
 
 

@@ -172,8 +172,8 @@ def test_attach_resident_matches_file(gpu):
     exactly as the variable's own bytes do; a misaligned pointer and a query
     on another device than the attached one raise instead of silently
     replacing the caller's store."""
-    import torch
     from pyactivestorage_amd.active import attach_resident
+    from pyactivestorage_amd.device import DeviceBuffer
     var = D.make_variable()
     ref = D.make_variable()
     nd = len(var.shape)
@@ -184,13 +184,18 @@ def test_attach_resident_matches_file(gpu):
     for k, cc in enumerate(np.ndindex(*grid)):
         off, size = var.chunk_info(cc)
         host[k * stride: k * stride + size] = np.frombuffer(var.read(off, size), dtype=np.uint8)
-    data = torch.from_numpy(host).to("cuda:0")
+    # the producer's buffer (the library's own allocation: this process's HIP
+    # runtime is libpyas_hip's, no torch here)
+    data = DeviceBuffer(gpu, host.nbytes)
+    st = gpu.thread_stream()
+    gpu.h2d(data.ptr, host, st)
+    gpu.synchronize(st)
     with pytest.raises(ValueError, match="aligned"):
-        attach_resident(var, data.data_ptr() + 4, device=0, owner=data)
-    attach_resident(var, data.data_ptr(), device=0, owner=data)
+        attach_resident(var, data.ptr + 4, device=0, owner=data)
+    attach_resident(var, data.ptr, device=0, owner=data)
     try:
         with pytest.raises(ValueError, match="already has a resident copy"):
-            attach_resident(var, data.data_ptr(), device=0, owner=data)
+            attach_resident(var, data.ptr, device=0, owner=data)
         half = tuple(slice(0, max(1, n // 2)) for n in var.shape)
         for method, axis, index in [("mean", None, (slice(None),) * nd), ("min", (0,), half),
                                     ("max", (nd - 1,), half), ("mean", (0, nd - 1), (slice(None),) * nd)]:
