@@ -317,6 +317,11 @@ int pyas_reduce_axes(pyas_ctx *ctx, const pyas_batch *batch,
  * dense launch leaves (there are none).  A broken promise leaves those
  * chunks' outputs unwritten. */
 #define PYAS_REC_DENSE_ONLY 0x200
+/* The opposite promise: no chunk is whole or such a box (e.g. a strided or
+ * listed selection in every chunk), so the dense launch, which would find no
+ * chunk of its own, is not made.  A broken promise leaves the whole and box
+ * chunks' outputs unwritten. */
+#define PYAS_REC_GENERIC_ONLY 0x400
 /* pyas_reduce_axes writing `rec` records (PYAS_REC_*; PYAS_REC_FULL is
  * pyas_reduce_axes itself): out[out_offsets[c] + o] in record units.  A
  * chunk's outputs must count < 2^31 elements each. */

@@ -127,6 +127,7 @@ class TieRule(ctypes.Structure):
 REC_FULL, REC_SUM, REC_MIN, REC_MAX = 0, 1, 2, 3
 REC_ZERO_SIGN = 0x100    # pyas.h PYAS_REC_ZERO_SIGN: the per-chunk walk keys NumPy's zero sign
 REC_DENSE_ONLY = 0x200   # pyas.h PYAS_REC_DENSE_ONLY: every chunk is dense-owned, no generic launch
+REC_GENERIC_ONLY = 0x400  # pyas.h PYAS_REC_GENERIC_ONLY: no chunk is dense-owned, no dense launch
 TIE_REC = 4
 
 

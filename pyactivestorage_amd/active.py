@@ -838,7 +838,10 @@ class Active:
             except NotImplementedError:
                 pass   # another layout: the scan pass keys the sign
         # every chunk whole or a box the dense launch takes: no generic walk
-        dense = _lib.REC_DENSE_ONLY if prec and plan.dense_boxes() else 0
+        # every chunk whole or a box the dense launch takes: no generic walk;
+        # no chunk of the dense launch's: no dense launch
+        dense = _lib.REC_DENSE_ONLY if prec and plan.dense_boxes() else \
+            _lib.REC_GENERIC_ONLY if prec and plan.no_dense_boxes() else 0
         engine.reduce_axes(ctx, plan.batch, plan.mask_up.struct, axes_mask, obuf_ptr, parts_ptr, st, rec=prec | dense)
         return False
 

@@ -103,21 +103,32 @@ class ReductionPlan:
         the dense per-chunk kernels walk themselves (pyas_kernels.hpp
         cut_eligible), the promise PYAS_REC_ZERO_SIGN needs."""
         r = getattr(self, "_dense_boxes", None)   # fixed per plan; replays ask every query
-        if r is not None:
-            return r
+        if r is None:
+            self._dense_class()
+        return self._dense_boxes
+
+    def no_dense_boxes(self) -> bool:
+        """Whether NO chunk is whole or such a box (every chunk's selection is
+        strided, listed or small): the dense launch would find nothing, so
+        PYAS_REC_GENERIC_ONLY skips it."""
+        if getattr(self, "_no_dense", None) is None:
+            self._dense_class()
+        return self._no_dense
+
+    def _dense_class(self):
         t = self.sel_table_host
         nd = len(self.chunk_shape)
-        if self.chunk_shape[-1] < 2:
-            r = False
-        elif t is None:
-            r = True
-        else:
-            step, cnt = t[:, :nd, 1], t[:, :nd, 2].astype(np.int64)
-            ok = ((step == 1) | (cnt == 1)).all(axis=1) & (cnt >= 1).all(axis=1) & (cnt[:, nd - 1] > 1)
-            ok &= 2 * cnt.prod(axis=1) >= int(np.prod(self.chunk_shape))
-            r = bool(ok.all())
-        self._dense_boxes = r
-        return r
+        if t is None:
+            self._dense_boxes, self._no_dense = self.chunk_shape[-1] >= 2, False
+            return
+        step, cnt = t[:, :nd, 1], t[:, :nd, 2].astype(np.int64)
+        # the kernels' cut_eligible (pyas_kernels.hpp), and chunk_is_full
+        box = ((step == 1) | (cnt == 1)).all(axis=1) & (cnt >= 1).all(axis=1)
+        box &= 2 * cnt.prod(axis=1) >= int(np.prod(self.chunk_shape))
+        full = ((step == 1) & (cnt == np.asarray(self.chunk_shape, dtype=np.int64)[None, :])).all(axis=1)
+        # DENSE_ONLY also wants more than one index in the innermost dim
+        self._dense_boxes = self.chunk_shape[-1] >= 2 and bool((box & (cnt[:, nd - 1] > 1)).all())
+        self._no_dense = not bool((box | full).any())
 
     def tie_geom(self, order="C") -> _lib.TieGeom:
         """How NumPy walks these chunks' ``chunk[sel]`` after mask_missing

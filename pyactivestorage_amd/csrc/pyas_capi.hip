@@ -964,7 +964,10 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
     // PYAS_REC_DENSE_ONLY (and PYAS_REC_ZERO_SIGN, which makes the same
     // promise): every chunk is whole or a box the dense launch takes
     const bool dense_only = (rec & (PYAS_REC_DENSE_ONLY | PYAS_REC_ZERO_SIGN)) != 0;
-    rec &= ~(PYAS_REC_ZERO_SIGN | PYAS_REC_DENSE_ONLY);
+    // PYAS_REC_GENERIC_ONLY: no chunk is the dense launch's (none is made)
+    const bool generic_only = (rec & PYAS_REC_GENERIC_ONLY) != 0;
+    if (dense_only && generic_only) return fail(PYAS_EINVAL, "PYAS_REC_DENSE_ONLY and PYAS_REC_GENERIC_ONLY together");
+    rec &= ~(PYAS_REC_ZERO_SIGN | PYAS_REC_DENSE_ONLY | PYAS_REC_GENERIC_ONLY);
     if (rec < PYAS_REC_FULL || rec > PYAS_REC_MAX) return fail(PYAS_EINVAL, "unknown record form %d", rec);
     pyas::AxesArgs x;
     std::memset(&x, 0, sizeof(x));
@@ -1144,7 +1147,7 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
             return PYAS_OK;
         }
     }
-    if (x.d.mode) {
+    if (x.d.mode && !(generic_only && batch->sel)) {
         const int64_t g = (x.d.cpb > 0 ? (batch->n_chunks + x.d.cpb - 1) / x.d.cpb : batch->n_chunks) * x.d.bpc;
         if (g >= (int64_t(1) << 31)) return fail(PYAS_ENOTSUP, "grid too large");
         PYAS_HIP(pyas::launch_axes_dense(batch->dtype, x, masked, g, (hipStream_t)stream));
