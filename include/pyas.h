@@ -484,10 +484,12 @@ int pyas_reduce_axes_grid(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mas
  * another fold kernel, a reduction the kernel cannot key, or no rule is set:
  * fold without the flag and run the zero-sign passes then.
  * pyas_combine_grid takes the same flags over records that already carry
- * level 1's signs (pyas_reduce_axes_ex with PYAS_REC_ZERO_SIGN): where the
- * `out` array's calls are elementwise (its innermost non-1 dim kept) each
- * output takes the sign of its last layer whose min (max) is a zero, so
- * pyas_tie_grid is not needed; PYAS_ENOTSUP (nothing launched) otherwise. */
+ * level 1's signs (pyas_reduce_axes_ex with PYAS_REC_ZERO_SIGN) and keys
+ * level 2 itself, so pyas_tie_grid is not needed: where the `out` array's
+ * calls are elementwise (its innermost non-1 dim kept) each output takes the
+ * sign of its last layer whose min (max) is a zero; where they run over the
+ * trailing reduced dims (calls of lr layers), the context's tie rule keys the
+ * zero layers at their positions in the call (pyas_tie_grid's keys). */
 #define PYAS_FOLD_ZERO_SIGN_MIN 0x100u
 #define PYAS_FOLD_ZERO_SIGN_MAX 0x200u
 
