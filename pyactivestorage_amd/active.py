@@ -136,8 +136,7 @@ class _CachedQuery:
             g["rec"] = engine.method_rec(act._method)
             g["zs1"] = act._reduce_axes_zs(ctx, st, self.plan, g["axes_mask"], g["obuf"].ptr, g["parts"].ptr,
                                            g["rec"], g.get("zs_ok1", False))
-            g["zs2"] = act._combine_zs(ctx, st, g["parts"].ptr, g["g"], g["fin"].ptr, g["rec"],
-                                       g["zs1"] and g["tie"]["lr"] == 1)
+            g["zs2"] = act._combine_zs(ctx, st, g["parts"].ptr, g["g"], g["fin"].ptr, g["rec"], g["zs1"])
         act._tie_grid(ctx, st, self.plan, g)
         return act._format_device(ctx, st, g["fin"], g["n_final"], shape, bufs=self.fmt)
 
@@ -1011,7 +1010,7 @@ class Active:
             zs1 = self._reduce_axes_zs(ctx, st, plan, axes_mask, obuf.ptr, parts.ptr, prec, zs_ok1)
             # level 2 in the combine where the `out` calls are elementwise
             # (group queries key it across ranks: pyas_tie_grid below)
-            zs2 = self._combine_zs(ctx, st, parts.ptr, g, fin.ptr, prec, zs1 and lr == 1 and keys is None)
+            zs2 = self._combine_zs(ctx, st, parts.ptr, g, fin.ptr, prec, zs1 and keys is None)
         r = rec if rec is not None else {}
         if folded:
             zs_ok1 = zs1 = False
@@ -1037,8 +1036,8 @@ class Active:
 
     def _combine_zs(self, ctx, st, parts_ptr, g, fin_ptr, prec, keyed) -> bool:
         """pyas_combine_grid of the per-chunk records; ``keyed`` (level 1
-        keyed by the walk, the `out` calls elementwise): level 2 of NumPy's
-        zero sign keyed in the same launch.  Returns whether it was."""
+        keyed by the walk): level 2 of NumPy's zero sign keyed in the same
+        launch, for `out` calls of any length.  Returns whether it was."""
         dt = self.ds.dtype
         which = self._tie_which() if keyed else 0
         if which:

@@ -1423,8 +1423,11 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, cons
                           PYAS_FOLD_ZERO_SIGN_MAX))
         return fail(PYAS_EINVAL, "unknown combine flags 0x%x", combine_flags);
     // PYAS_FOLD_ZERO_SIGN_*: `in` carries level 1's signs (PYAS_REC_ZERO_SIGN);
-    // the combine keys level 2 itself when the `out` array's calls are
-    // elementwise (its trailing non-1 dims kept): the last zero layer wins
+    // the combine keys level 2 itself: when the `out` array's calls are
+    // elementwise (its trailing non-1 dims kept) the last zero layer wins,
+    // else the keys over each call's zero layers decide (tie_keys)
+    pyas::CombineTie ct;
+    std::memset(&ct, 0, sizeof(ct));
     if (combine_flags & (PYAS_FOLD_ZERO_SIGN_MIN | PYAS_FOLD_ZERO_SIGN_MAX)) {
         if ((combine_flags & (PYAS_FOLD_ZERO_SIGN_MIN | PYAS_FOLD_ZERO_SIGN_MAX)) ==
             (PYAS_FOLD_ZERO_SIGN_MIN | PYAS_FOLD_ZERO_SIGN_MAX))
@@ -1439,7 +1442,13 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, cons
             if (!red) break;
             lr2 *= ext;
         }
-        if (lr2 != 1) return fail(PYAS_ENOTSUP, "zero sign in the combine: the out calls are not elementwise");
+        // calls of lr2 > 1 layers: the keys of NumPy's reduce over each call
+        // (k_tie_grid_t's, in the same pass instead of a second launch)
+        if (lr2 != 1) {
+            ct.on = 1;
+            ct.t = *tie_of(ctx, dtype);
+            ct.c = grid_call(ct.t, lr2);
+        }
         combine_flags |= pyas::kCombineThreadOnly;   // the per-thread form keys it
     }
     int64_t n_out = 1, n_layers = 1;
@@ -1460,7 +1469,7 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, cons
     // per-thread fold for every layer count
     const char *e_wave = getenv("PYAS_COMBINE_WAVE");
     if (e_wave && std::strcmp(e_wave, "0") == 0) combine_flags |= pyas::kCombineThreadOnly;
-    PYAS_HIP(pyas::launch_combine_grid(dtype, in, *g, n_out, n_layers, combine_flags, out,
+    PYAS_HIP(pyas::launch_combine_grid(dtype, in, *g, ct, n_out, n_layers, combine_flags, out,
                                        (hipStream_t)stream));
     return PYAS_OK;
 }

@@ -135,8 +135,9 @@ hipError_t launch_combine_segments_t(const pyas_partial *in, const int64_t *inde
                                      pyas_partial *out, hipStream_t st);
 template <typename T>
 hipError_t launch_axes_t(const AxesArgs &a, int64_t grid, hipStream_t st);
+struct CombineTie;   // below, after the tie structs it carries
 template <typename T>
-hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, int64_t n_out,
+hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, const CombineTie &ct, int64_t n_out,
                                  int64_t n_layers, uint32_t flags, pyas_partial *out,
                                  hipStream_t st);
 template <typename T>
@@ -156,6 +157,13 @@ struct TieCall {
     uint32_t block;                   // acc: kept dims of NumPy's copied first buffer fill
     int64_t lr, npr;                  // call length (1: elementwise), pieces per call
     int64_t n_copy;                   // acc: runs of that fill (contiguous calls), 0: none
+};
+// k_combine_grid keying level 2 of NumPy's zero sign itself for `out` calls
+// of any length (on = 1): the call and the host's rule
+struct CombineTie {
+    TieCall c;
+    TieRule t;
+    int32_t on;
 };
 struct FoldGrid {
     int64_t n_coords[PYAS_MAX_DIMS];  // chunk coordinates per dim (chunk n = C-order position)
@@ -228,7 +236,7 @@ hipError_t launch_combine_segments(int dtype, const pyas_partial *in, const int6
                                    const int64_t *seg, int64_t n_seg, uint32_t flags,
                                    pyas_partial *out, hipStream_t st);
 hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStream_t st);
-hipError_t launch_combine_grid(int dtype, const pyas_partial *in, const pyas_grid &g,
+hipError_t launch_combine_grid(int dtype, const pyas_partial *in, const pyas_grid &g, const CombineTie &ct,
                                int64_t n_out, int64_t n_layers, uint32_t flags,
                                pyas_partial *out, hipStream_t st);
 hipError_t launch_axes_dense(int dtype, const AxesArgs &a, bool masked, int64_t grid, hipStream_t st);

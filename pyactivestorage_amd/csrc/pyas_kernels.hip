@@ -111,10 +111,10 @@ hipError_t launch_reduce_axes(int dtype, const AxesArgs &a, int64_t grid, hipStr
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_combine_grid(int dtype, const pyas_partial *in, const pyas_grid &g,
+hipError_t launch_combine_grid(int dtype, const pyas_partial *in, const pyas_grid &g, const CombineTie &ct,
                                int64_t n_out, int64_t n_layers, uint32_t flags,
                                pyas_partial *out, hipStream_t st) {
-    PYAS_DISPATCH_T(dtype, return launch_combine_grid_t<T>(in, g, n_out, n_layers, flags, out, st));
+    PYAS_DISPATCH_T(dtype, return launch_combine_grid_t<T>(in, g, ct, n_out, n_layers, flags, out, st));
     return hipErrorInvalidValue;
 }
 

@@ -205,8 +205,7 @@ def combine_grid(ctx: Context, dt, in_ptr, grid: _lib.Grid, out_ptr, round_to_va
                  rec: int = 0, zero_sign: int = 0) -> None:
     """pyas_combine_grid.  ``zero_sign`` (1 min, 2 max): the records carry
     level 1's NumPy sign (PYAS_REC_ZERO_SIGN) and the combine keys level 2
-    (PYAS_FOLD_ZERO_SIGN_*); NotImplementedError where the `out` array's
-    calls are not elementwise."""
+    (PYAS_FOLD_ZERO_SIGN_*) over the `out` array's calls."""
     flags = (_lib.COMBINE_ROUND_TO_VAR if round_to_var else 0) | _lib.combine_rec(rec) | (int(zero_sign) << 8)
     _lib.check(ctx.lib.pyas_combine_grid(ctx.handle, dtype_code(dt), in_ptr, ctypes.byref(grid), flags,
                                          out_ptr, stream), "pyas_combine_grid")
