@@ -24,19 +24,6 @@ def P(name):
     return os.path.join(NC, name)
 
 
-def test_inflate_choice():
-    """Active's device/host inflate choice (row f3): forced either way, or
-    by stream count against the measured crossover (active.py
-    inflate_on_device)."""
-    from pyactivestorage_amd import active as A
-    assert A.inflate_on_device(1, 30, True) and not A.inflate_on_device(10_000, 30, False)
-    n_cross = A._INFLATE_CROSSOVER * min(30, A._INGEST_LANES)
-    assert not A.inflate_on_device(int(n_cross) - 1, 30, "auto")
-    assert A.inflate_on_device(int(n_cross) + 1, 30, "auto")
-    with pytest.raises(ValueError):
-        Active(P("test1.nc"), "tas", device_inflate="gpu")
-
-
 @pytest.mark.parametrize("inflate", ["device", "host"])
 def test_known_answers_from_files(gpu, inflate, monkeypatch):
     """zlib chunks inflated by pyas_inflate and by the host reader threads

@@ -300,3 +300,54 @@ def test_build_one_matches_build(dt):
                         got = results.build_one(p[0], shape, kind, is_ma, np.dtype(dt), rule, n_sel, n_sel)
                         assert _state(got[0]) == _state(want[0]), (dt, cnt, kind, is_ma, rule)
                         assert _state(got[1]) == _state(want[1])
+
+
+def test_inflate_choice(monkeypatch):
+    """Active's device/host inflate choice (row f3): forced
+    either way, or by stream count against the measured crossover per host
+    lane (active.py inflate_on_device), PYAS_ACTIVE_INFLATE overriding auto."""
+    from pyactivestorage_amd import active as A
+    monkeypatch.delenv("PYAS_ACTIVE_INFLATE", raising=False)
+    assert A.inflate_on_device(1, 30, True) and not A.inflate_on_device(10_000, 30, False)
+    n_cross = int(A._INFLATE_CROSSOVER * min(30, A._INGEST_LANES))
+    assert not A.inflate_on_device(n_cross - 1, 30, "auto")
+    assert A.inflate_on_device(n_cross, 30, "auto")
+    assert not A.inflate_on_device(n_cross - 1, 4, "auto") or n_cross - 1 >= A._INFLATE_CROSSOVER * 4
+    monkeypatch.setenv("PYAS_ACTIVE_INFLATE", "device")
+    assert A.inflate_on_device(1, 30, "auto")
+    monkeypatch.setenv("PYAS_ACTIVE_INFLATE", "host")
+    assert not A.inflate_on_device(10_000, 30, "auto") and A.inflate_on_device(1, 30, True)
+    nc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "nc", "test1.nc")
+    with pytest.raises(ValueError):
+        A.Active(nc, "tas", device_inflate="gpu")
+
+
+def _sel_table(rows):
+    t = np.zeros((len(rows), 8, 3), dtype=np.int32)
+    for i, r in enumerate(rows):
+        for d in range(8):
+            t[i, d] = r[d] if d < len(r) else (0, 1, 1)
+    return t
+
+
+@pytest.mark.parametrize("rows,dense,none", [
+    ([[(0, 1, 4), (0, 1, 8), (0, 1, 16)]], True, False),            # whole chunk
+    ([[(1, 1, 3), (0, 1, 8), (0, 1, 16)]], True, False),            # a box over half of it
+    ([[(0, 1, 4), (0, 1, 8), (3, 1, 1)]], False, True),             # a thin box: generic walk
+    ([[(0, 1, 4), (0, 3, 3), (0, 1, 16)]], False, True),            # strided kept dim
+    ([[(0, 1, 4), (0, 0, 2), (0, 1, 16)]], False, True),            # an index list
+    ([[(0, 1, 4), (0, 3, 3), (0, 1, 16)], [(0, 1, 4), (0, 1, 8), (0, 1, 16)]], False, False),   # mixed
+    ([[(0, 1, 4), (0, 1, 8), (0, 1, 1)]], False, True),             # one innermost index: under half
+])
+def test_dense_classes(rows, dense, none):
+    """ReductionPlan's promises to pyas_reduce_axes_ex (PYAS_REC_DENSE_ONLY /
+    PYAS_REC_GENERIC_ONLY): they must mirror the kernels' chunk ownership
+    (pyas_kernels.hpp chunk_is_full / cut_eligible), or outputs go unwritten."""
+    from pyactivestorage_amd.batch import ReductionPlan
+
+    class P:
+        chunk_shape = (4, 8, 16)
+    p = P()
+    p.sel_table_host = _sel_table(rows)
+    ReductionPlan._dense_class(p)
+    assert p._dense_boxes == dense and p._no_dense == none
