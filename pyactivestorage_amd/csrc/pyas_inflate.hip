@@ -97,17 +97,17 @@ __device__ __forceinline__ void store_rel(uint32_t *p, uint32_t v) {
     if ((threadIdx.x & 63) == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Inclusive prefix sum over the wave: DPP shifts inside each 16-lane row,
-// then the row totals (lanes 15, 31, 47) added with three readlanes.
+// Inclusive prefix sum over the wave, all in DPP: shifts inside each 16-lane
+// row, then row_bcast:15 (rows 1 and 3 add lane 15 of the row before) and
+// row_bcast:31 (rows 2 and 3 add lane 31) -- no readlanes, no SGPR round trip.
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
-    const int lane = threadIdx.x & 63;
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
-    const uint32_t r0 = rl(x, 15), r1 = rl(x, 31), r2 = rl(x, 47);
-    const uint32_t row = (uint32_t)lane >> 4;
-    return x + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
 }
 
 // Phase timing (diagnostic build, -DPYAS_INFLATE_PROF): per-wave cycle sums
@@ -127,11 +127,13 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
 // Decoder side
 // ---------------------------------------------------------------------------
 
-// Bit reader over dword-aligned input, staged through a 128-dword LDS ring:
-// window bits come from LDS (no vector-memory wait in the symbol loop).  The
-// ring is refilled 64 dwords at a time from a block loaded into one VGPR per
-// lane a refill earlier, so the global load latency is off the decode path.
-constexpr uint32_t kInRing = 128, kInBlock = 64;
+// Bit reader over dword-aligned input, staged through a 256-dword LDS ring
+// refilled 128 dwords (two per lane) at a time: window bits come from LDS, so
+// the symbol loop waits on a global load once per refill (every ~4 KiB of
+// input).  (A block loaded one refill ahead into a VGPR did not hide that
+// latency: the no-refill path's copy of the loop-carried register waited on
+// the load in the very next window.)
+constexpr uint32_t kInRing = 256, kInBlock = 128;
 
 struct BitIn {
     const uint32_t *w;
@@ -139,25 +141,24 @@ struct BitIn {
     uint32_t nbits;    // valid bits from w (stream end)
     uint32_t pos;      // bit position from w
     uint32_t filled;   // dwords [filled - kInRing, filled) are in the ring
-    uint32_t stage;    // w[filled + lane], loaded ahead
     uint32_t *ring;    // LDS
 
     __device__ __forceinline__ uint32_t load(uint32_t k) const {
         const uint32_t i = k + (threadIdx.x & 63);
         return i < nwords ? __builtin_nontemporal_load(w + i) : 0u;
     }
+    __device__ __forceinline__ void refill() {
+        const uint32_t a = load(filled), b = load(filled + 64u);
+        ring[(filled + (threadIdx.x & 63)) & (kInRing - 1)] = a;
+        ring[(filled + 64u + (threadIdx.x & 63)) & (kInRing - 1)] = b;
+        filled += kInBlock;
+    }
     __device__ __forceinline__ void seek() {   // at the start and after stored blocks
         filled = pos >> 5;
-        ring[(filled + (threadIdx.x & 63)) & (kInRing - 1)] = load(filled);
-        filled += kInBlock;
-        stage = load(filled);
+        refill();
     }
     __device__ __forceinline__ void ensure() {
-        if ((pos >> 5) + 32u > filled) {
-            ring[(filled + (threadIdx.x & 63)) & (kInRing - 1)] = stage;
-            filled += kInBlock;
-            stage = load(filled);
-        }
+        if ((pos >> 5) + 64u > filled) refill();
     }
     // 32 bits at pos + off (LSB first), per lane
     __device__ __forceinline__ uint32_t bits_at(uint32_t off) const {

@@ -20,3 +20,7 @@ for q in "c3_slab 7" "c3_slab 6" "c3_whole 2"; do
     done
   done
 done
+cd $R
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_inflate.py > $O/inflate_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/bench_inflate.py --sweep 1,30,256 > $O/inflate_bench.json 2> $O/inflate_bench.err || exit 1
+PYAS_LIB=$R/pyactivestorage_amd/lib/prof/libpyas_prof.so timeout -k 10 300 python -u tools/bench_inflate.py --chunks 4 --reps 1 > $O/inflate_prof.txt 2>&1 || exit 1
