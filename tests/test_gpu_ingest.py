@@ -108,3 +108,48 @@ def test_truncated_chunk_file(gpu, tmp_path):
     a.method = "mean"
     with pytest.raises(OSError):
         a[...]
+
+
+def test_read_ranges_zlib(gpu, tmp_path):
+    """pyas_read_ranges_zlib (host inflate into the pinned ring, row f3 below
+    the crossover): the bytes zlib.decompress gives (storage.py:119-120),
+    zlib's own error for a broken stream, and the reference's reshape
+    ValueError for a stream of the wrong inflated size."""
+    import zlib
+    rng = np.random.default_rng(4)
+    chunk = 4096
+    plains = [np.cumsum(rng.normal(size=chunk // 4)).astype("<f4").tobytes() for _ in range(40)]
+    comps = [zlib.compress(p, int(lvl)) for p, lvl in zip(plains, rng.integers(0, 10, len(plains)))]
+    path = tmp_path / "z.bin"
+    blob = b"".join(comps)
+    path.write_bytes(blob)
+    foff = np.concatenate([[0], np.cumsum([len(c) for c in comps])[:-1]]).astype(np.int64)
+    size = np.array([len(c) for c in comps], dtype=np.int64)
+    stride = 4096 + 256
+    doff = np.arange(len(comps), dtype=np.int64) * stride
+    dev = DeviceBuffer(gpu, len(comps) * stride)
+    st = gpu.thread_stream()
+    for threads in (1, 4, 30):
+        assert ingest.read_ranges_zlib(gpu, str(path), foff, size, dev.ptr, doff, chunk, st, threads) == size.sum()
+        host = np.zeros(len(comps) * stride, dtype=np.uint8)
+        gpu.d2h(host, dev.ptr, st)
+        gpu.synchronize(st)
+        for k, p in enumerate(plains):
+            assert host[k * stride: k * stride + chunk].tobytes() == p, (threads, k)
+    bad = bytearray(blob)
+    bad[foff[7] + 20] ^= 0xFF                        # corrupt one stream's compressed bytes
+    bpath = tmp_path / "bad.bin"
+    bpath.write_bytes(bytes(bad))
+    try:
+        zlib.decompress(bytes(bad[foff[7]: foff[7] + size[7]]))
+        broken = False
+    except zlib.error:
+        broken = True
+    if broken:
+        with pytest.raises(zlib.error):
+            ingest.read_ranges_zlib(gpu, str(bpath), foff, size, dev.ptr, doff, chunk, st, 4)
+    with pytest.raises(ValueError, match="cannot reshape"):   # inflates to 4096, not 8192
+        ingest.read_ranges_zlib(gpu, str(path), foff, size, dev.ptr, doff // stride * 8448, 8192, st, 4,
+                                reshape=(4, (2048,)))
+    # the context still works after the failures
+    assert ingest.read_ranges_zlib(gpu, str(path), foff[:3], size[:3], dev.ptr, doff[:3], chunk, st) == size[:3].sum()
