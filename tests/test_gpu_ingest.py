@@ -148,8 +148,9 @@ def test_read_ranges_zlib(gpu, tmp_path):
     if broken:
         with pytest.raises(zlib.error):
             ingest.read_ranges_zlib(gpu, str(bpath), foff, size, dev.ptr, doff, chunk, st, 4)
+    big = DeviceBuffer(gpu, len(comps) * 8448)       # room for 8192 inflated bytes per stream
     with pytest.raises(ValueError, match="cannot reshape"):   # inflates to 4096, not 8192
-        ingest.read_ranges_zlib(gpu, str(path), foff, size, dev.ptr, doff // stride * 8448, 8192, st, 4,
+        ingest.read_ranges_zlib(gpu, str(path), foff, size, big.ptr, doff // stride * 8448, 8192, st, 4,
                                 reshape=(4, (2048,)))
     # the context still works after the failures
     assert ingest.read_ranges_zlib(gpu, str(path), foff[:3], size[:3], dev.ptr, doff[:3], chunk, st) == size[:3].sum()
