@@ -41,7 +41,10 @@ namespace {
 
 constexpr int kLitBits = 10, kDistBits = 8;
 constexpr uint32_t kFlush = 1024;   // bytes per coalesced flush (16 per lane)
-constexpr uint32_t kQ = 512;        // token queue entries (power of two)
+#ifndef PYAS_INFLATE_Q
+#define PYAS_INFLATE_Q 1024
+#endif
+constexpr uint32_t kQ = PYAS_INFLATE_Q;   // token queue entries (power of two)
 constexpr uint32_t kStoredTok = 0xffffu;   // len field of a stored-block token (two queue slots)
 
 __constant__ uint8_t c_clen_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
@@ -63,11 +66,14 @@ struct Lds {
 };
 
 // Token queue from the decoder wave to the writer wave.  Token t sits at
-// slot t % kQ: pos = its output offset, w = len << 16 | d (a match of len
-// bytes at distance d), len 0: a literal (d = the byte), len kStoredTok: a
-// stored block of d bytes whose input byte offset is the next slot's pos.
+// slot t % kQ: w = len << 16 | d (a match of len bytes at distance d), len
+// 0: a literal (d = the byte), len kStoredTok: a stored block of d bytes
+// whose input byte offset is the next slot's w.  Output offsets are not
+// queued: tokens are contiguous, so the writer takes them as a prefix sum of
+// the lengths from its own position -- which doubles the queue in the same
+// LDS (512 -> 1024 tokens: the decoder waited 3.3M cycles per 1 MiB stream
+// on a full queue of 512, profiles/r06/inflate).
 struct Queue {
-    uint32_t pos[kQ];
     uint32_t w[kQ];
     uint32_t prod;      // tokens published by the decoder
     uint32_t cons;      // tokens the writer is done with
@@ -301,12 +307,9 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
         prod += n;
         store_rel(&Q.prod, prod);
     };
-    auto emit1 = [&](uint32_t pos, uint32_t w) {   // one token from the serial decoder
+    auto emit1 = [&](uint32_t w) {   // one token from the serial decoder
         room(1);
-        if (lane == 0) {
-            Q.pos[prod & (kQ - 1)] = pos;
-            Q.w[prod & (kQ - 1)] = w;
-        }
+        if (lane == 0) Q.w[prod & (kQ - 1)] = w;
         publish(1);
     };
 
@@ -338,10 +341,8 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
             if (len) {
                 room(2);
                 if (lane == 0) {
-                    Q.pos[prod & (kQ - 1)] = q;
                     Q.w[prod & (kQ - 1)] = (kStoredTok << 16) | len;
-                    Q.pos[(prod + 1) & (kQ - 1)] = in.pos >> 3;   // input byte offset from in.w
-                    Q.w[(prod + 1) & (kQ - 1)] = 0u;
+                    Q.w[(prod + 1) & (kQ - 1)] = in.pos >> 3;   // input byte offset from in.w
                 }
                 publish(2);
                 q += len;
@@ -431,7 +432,7 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
             if (!l) { status = PYAS_INFLATE_BAD_SYMBOL; return 2; }
             if (sym < 256) {
                 if (q >= cap) { status = PYAS_INFLATE_OVERFLOW; return 2; }
-                emit1(q, sym);
+                emit1(sym);
                 q++;
                 in.pos += l;
                 return 0;
@@ -451,7 +452,7 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
             in.pos += l + de;
             if (d > q) { status = PYAS_INFLATE_BAD_DISTANCE; return 2; }
             if (q + len > cap) { status = PYAS_INFLATE_OVERFLOW; return 2; }
-            emit1(q, (len << 16) | d);
+            emit1((len << 16) | d);
             q += len;
             return 0;
         };
@@ -573,7 +574,6 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
                 if ((M[j] >> lane) & 1ull) {
                     const uint32_t idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(M[j] >> 32),
                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)M[j], 0u));
-                    Q.pos[idx & (kQ - 1)] = q + excl[j];
                     Q.w[idx & (kQ - 1)] = tw[j];
                 }
                 base += (uint32_t)__builtin_popcountll(M[j]);
@@ -758,36 +758,53 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
         const uint32_t avail = prod - cons;
         const bool act = (uint32_t)lane < avail;
         const uint32_t slot = (cons + (uint32_t)lane) & (kQ - 1);
-        const uint32_t p = act ? Q.pos[slot] : 0u;
         const uint32_t w = act ? Q.w[slot] : 0u;
         uint32_t len = w >> 16, d = w & 0xffffu;
+        // output offsets: the lengths' prefix sum from o.pos (lanes past a
+        // stored token sum garbage; the batch ends before them)
+        const uint32_t olen = act ? (len ? len : 1u) : 0u;
+        const uint32_t p = o.pos + wave_incl_sum(olen) - olen;
         const uint64_t stored = __ballot(act && len == kStoredTok);
         if (stored & 1ull) {   // a stored block: 16 bytes per lane per 1 KiB step
             const uint32_t slen = rl(d, 0);
-            const uint32_t byte0 = Q.pos[(cons + 1) & (kQ - 1)];
+            const uint32_t byte0 = Q.w[(cons + 1) & (kQ - 1)];
+            const uint32_t mine = (uint32_t)lane * 16u;
+            // kStoredSteps steps' input loads in flight at once (one HBM
+            // round trip per 1 KiB step cost the writer 1.7M cycles per
+            // 1 MiB stream, profiles/r06/inflate)
+            constexpr uint32_t kStoredSteps = 4;
             for (uint32_t dn = 0; dn < slen;) {
-                while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
-                const uint32_t step = min(slen - dn, kFlush);
-                const uint32_t mine = (uint32_t)lane * 16u;
-                if (mine < step) {
-                    const uint32_t b = byte0 + dn + mine;
-                    const uint32_t wi = b >> 2, sh = b & 3u;
-                    uint32_t dw[5];
+                const uint32_t span = min(slen - dn, kStoredSteps * kFlush);
+                uint32_t dw[kStoredSteps][5];
+#pragma unroll
+                for (uint32_t s = 0; s < kStoredSteps; ++s) {
+                    const uint32_t b = byte0 + dn + s * kFlush + mine;
+                    const uint32_t wi = b >> 2;
+                    const bool on = s * kFlush + mine < span;
 #pragma unroll
                     for (uint32_t k = 0; k < 5; ++k)
-                        dw[k] = wi + k < in_words ? __builtin_nontemporal_load(inw + wi + k) : 0u;
-                    const uint32_t n = min(step - mine, 16u);
-#pragma unroll
-                    for (uint32_t k = 0; k < 4; ++k) {
-                        const uint32_t qv = __builtin_amdgcn_alignbyte(dw[k + 1], dw[k], sh);
-#pragma unroll
-                        for (uint32_t m = 0; m < 4; ++m)
-                            if (k * 4 + m < n) win[(o.pos + mine + k * 4 + m) & kWinMask] = (uint8_t)(qv >> (8 * m));
-                    }
+                        dw[s][k] = on && wi + k < in_words ? __builtin_nontemporal_load(inw + wi + k) : 0u;
                 }
-                o.pos += step;
-                dn += step;
-                wave_lds_sync();
+                const uint32_t sh = (byte0 + dn + mine) & 3u;   // the same for every step (steps of 1 KiB)
+#pragma unroll
+                for (uint32_t s = 0; s < kStoredSteps; ++s) {
+                    if (s * kFlush >= span) break;
+                    while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
+                    const uint32_t step = min(span - s * kFlush, kFlush);
+                    if (mine < step) {
+                        const uint32_t n = min(step - mine, 16u);
+#pragma unroll
+                        for (uint32_t k = 0; k < 4; ++k) {
+                            const uint32_t qv = __builtin_amdgcn_alignbyte(dw[s][k + 1], dw[s][k], sh);
+#pragma unroll
+                            for (uint32_t m = 0; m < 4; ++m)
+                                if (k * 4 + m < n) win[(o.pos + mine + k * 4 + m) & kWinMask] = (uint8_t)(qv >> (8 * m));
+                        }
+                    }
+                    o.pos += step;
+                    wave_lds_sync();
+                }
+                dn += span;
             }
             cons += 2;
             store_rel(&Q.cons, cons);
@@ -798,7 +815,6 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
         // output bytes (tokens are contiguous from o.pos)
         uint32_t n = min(avail, 64u);
         if (stored) n = min(n, (uint32_t)__builtin_ctzll(stored));
-        const uint32_t olen = len ? len : 1u;
         const uint64_t over = __ballot(act && p + olen - o.pos > kBud);
         if (over) n = min(n, (uint32_t)__builtin_ctzll(over));
         const bool mine = (uint32_t)lane < n;

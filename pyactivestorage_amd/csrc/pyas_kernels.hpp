@@ -1356,7 +1356,7 @@ __device__ __forceinline__ int tie_finalize(uint64_t k1, uint64_t w, uint64_t ka
 
 // box-query combine (pyas_combine_grid): one thread per final output element,
 // chunk layers folded in C order of the reduced dims' coordinates
-template <typename T>
+template <typename T, bool KEY>
 __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in, pyas_grid g, CombineTie ct,
                                                          int64_t n_out, int64_t n_layers,
                                                          uint32_t flags, pyas_partial *out) {
@@ -1406,7 +1406,7 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
     int64_t n = nk;
     // PYAS_FOLD_ZERO_SIGN_* (flags bits 8-9; the records carry level 1): the
     // sign of the last layer whose min (max) is a zero (elementwise `out`
-    // calls), or (ct.on) NumPy's level-2 keys over the zero layers at their
+    // calls), or (KEY) NumPy's level-2 keys over the zero layers at their
     // positions in the `out` call, as k_tie_grid_t would take them
     const uint32_t zs = (flags >> 8) & 3u;
     bool zneg = false;
@@ -1461,7 +1461,7 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
                             const double v = zs == 1 ? pu.min.f : pu.max.f;
                             if (v == 0.0) {
                                 zneg = __builtin_signbit(v) != 0;
-                                if (ct.on) {
+                                if constexpr (KEY) {
                                     uint64_t x1, xw, xa;
                                     tie_keys(l0 + u, zneg ? 1u : 0u, ct.c, ct.t, true, x1, xw, xa);
                                     zk1 = x1 > zk1 ? x1 : zk1;
@@ -1483,7 +1483,7 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
     if constexpr (TT<T>::kind == 0) {
         if (zs && (zs == 1 ? acc.mn : acc.mx) == (T)0) {
             bool neg = zneg;
-            if (ct.on) {
+            if constexpr (KEY) {
                 const int sg = tie_finalize(zk1, zkw, 0, ct.c, ct.t);
                 neg = sg > 0;
                 if (sg < 0) neg = __builtin_signbit(zs == 1 ? acc.mn : acc.mx) != 0;
@@ -2790,8 +2790,7 @@ constexpr int kRowLdsStride = 17;   // 16-B vectors per LDS run (V <= 16, + 1 pa
 // the lowest lane-rank class holding one.  Its sign goes into the record.
 // Zero-free tiles cost one ballot.
 __device__ __forceinline__ int msb64(uint64_t v) { return 63 - __builtin_clzll(v); }   // v != 0
-constexpr int kRowZsWords = 4 + 64 + 1;   // rem, top, vec, box run, the rank classes, lane 0's positions
-constexpr int kRowZsRep = 4 + 64;         // zm[kRowZsRep]: bits k * lanes (lane 0's positions, from e = 1)
+constexpr int kRowZsWords = 4 + 64;   // rem, top, vec, box run, then the rank classes
 
 // The masks ZT reads (LDS, zm[kRowZsWords]) for a call of L positions e
 // (e = 0 the seed, then m = L - 1 elements: the first nv in t.lanes lanes, the
@@ -2804,7 +2803,6 @@ __device__ __forceinline__ void row_zs_masks(const TieRule &t, int L, uint64_t *
     const int rk = vec ? (int)t.rank[(e - 1) % lanes] : -1;
     const uint64_t rem = __ballot(e > nv && e < L), top = __ballot(vec && rk == 0), vm = __ballot(vec);
     const uint64_t run = __ballot(e < L);
-    const uint64_t rep = __ballot(vec && (e - 1) % lanes == 0) >> 1;
     for (int k = 0; k < lanes && k < 64; ++k) {
         const uint64_t cm = __ballot(rk == k);
         if (e == 0) zm[4 + k] = cm;
@@ -2814,51 +2812,25 @@ __device__ __forceinline__ void row_zs_masks(const TieRule &t, int L, uint64_t *
         zm[1] = top;
         zm[2] = vm;
         zm[3] = run;
-        zm[kRowZsRep] = rep;
     }
-}
-
-// Lane-class sets -> rank sets, per byte of the class set (pt[256 h + byte]:
-// the ranks of lanes 8 h + i for the byte's bits i), and rank -> lane
-// (ord), for row_zs_pick with at most 16 lanes (k_axes_fold_row's tables).
-__device__ __forceinline__ void row_zs_tables(const TieRule &t, uint16_t *pt, uint8_t *ord) {
-    for (int x = threadIdx.x; x < 512; x += kBlock) {
-        const int hh = x >> 8, byte = x & 255;
-        uint32_t m = 0;
-        for (int i = 0; i < 8; ++i)
-            if (((byte >> i) & 1) && 8 * hh + i < t.lanes) m |= 1u << t.rank[8 * hh + i];
-        pt[x] = (uint16_t)m;
-    }
-    if ((int)threadIdx.x < t.lanes) ord[t.rank[threadIdx.x]] = (uint8_t)threadIdx.x;
 }
 
 // The winning zero of a row call (box positions Z, bit e = position e).
-// Up to 16 lanes: the lowest rank holding a zero from the lane-class set
-// through the tables (row_zs_tables) -- a few VALU ops however sparse the
-// zeros; a search over the rank classes (one LDS mask each, until the
-// first class holding a zero) took longest exactly when zeros are few.
-__device__ __forceinline__ int row_zs_pick(uint64_t Z, const uint64_t *zm, int lanes, const uint16_t *pt,
-                                           const uint8_t *ord) {
+// (Round 6 measured a table pick of the lowest rank -- two LDS lookups
+// from the lane-class set -- slower than this search: 1.40 vs 1.20-1.32 ms
+// on the C3 slab (2,), profiles/r06/zeros2.)
+__device__ __forceinline__ int row_zs_pick(uint64_t Z, const uint64_t *zm, int lanes) {
     const uint64_t zr = Z & zm[0];
     if (zr) return msb64(zr);
     const uint64_t sig = Z & (zm[1] | 1u);
     const int e1 = sig ? msb64(sig) : -1;
     int ew = -1;
-    const uint64_t Zv = Z & zm[2];   // the zeros in the lanes
-    if (!(Z & 1u) && Zv) {
-        if (lanes <= 16) {
-            uint32_t C = 0;          // lanes holding a zero
-            for (int bb = 0; 1 + bb * lanes < 64; ++bb) C |= (uint32_t)(Zv >> (1 + bb * lanes)) & ((1u << lanes) - 1u);
-            const uint32_t P = (uint32_t)pt[C & 0xFFu] | (uint32_t)pt[256 + (C >> 8)];
-            const int jj = ord[__builtin_ctz(P)];
-            ew = msb64(Zv & (zm[kRowZsRep] << (1 + jj)));
-        } else {
-            for (int k = 0; k < lanes; ++k) {
-                const uint64_t cz = Z & zm[4 + k];
-                if (cz) {
-                    ew = msb64(cz);
-                    break;
-                }
+    if (!(Z & 1u) && (Z & zm[2])) {
+        for (int k = 0; k < lanes; ++k) {
+            const uint64_t cz = Z & zm[4 + k];
+            if (cz) {
+                ew = msb64(cz);
+                break;
             }
         }
     }
@@ -2868,8 +2840,7 @@ __device__ __forceinline__ int row_zs_pick(uint64_t Z, const uint64_t *zm, int l
 template <typename T, bool SHUF, bool BSWAP, int MASKED, bool AL, int H, bool CUT = false, bool ZT = false>
 __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uint8_t *base,
                               const MaskT<T> &mk, uint4 *tile, const CutBox *cb = nullptr,
-                              const uint32_t *rmap = nullptr, const uint64_t *zm = nullptr, int zs0 = 0,
-                              const uint16_t *zpt = nullptr, const uint8_t *zord = nullptr) {
+                              const uint32_t *rmap = nullptr, const uint64_t *zm = nullptr, int zs0 = 0) {
     const int64_t n = a.r.chunk_elems;
     constexpr int ES = sizeof(T), N = 16 / ES, RPW = kWave / H, VPL = Unit<T, SHUF>::VPL;
     // load units per lane per tile (64 * UL * VPL >= the tile's RPW * 16 vectors)
@@ -2972,7 +2943,7 @@ __device__ void dense_row_lds(const AxesArgs &a, int64_t c, int64_t j, const uin
                 for (int mm = H / 2; mm >= 1; mm >>= 1) Z |= shfl_xor(Z, mm);
                 if (zrow && h == 0) {
                     // the box's run along the innermost dim: positions from its start zs0
-                    const int e = row_zs_pick((Z >> zs0) & zm[3], zm, a.t.lanes, zpt, zord);
+                    const int e = row_zs_pick((Z >> zs0) & zm[3], zm, a.t.lanes);
                     if (e >= 0) {
                         const int x = zs0 + e;
                         T xe[N];
@@ -3055,9 +3026,6 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
     // ZS row layouts: the masks of the row call's positions (row_zs_masks)
     constexpr bool kRowZs = ZS && MODE >= 4;
     __shared__ uint64_t zm[kRowZs ? kRowZsWords : 1];
-    __shared__ uint16_t zpt[kRowZs ? 512 : 1];
-    __shared__ uint8_t zord[kRowZs ? 64 : 1];
-    if constexpr (kRowZs) row_zs_tables(a.t, zpt, zord);   // (made visible by the __syncthreads below)
     if constexpr (CUTS) {
         // a cut chunk (a.cuts launches): read as its whole chunk, the box
         // applied through the reduced-position map and the output remap
@@ -3085,10 +3053,8 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
                 if (al) dense_col<T, SHUF, BSWAP, MASKED, true, true, ZS>(a, c, j, base, mk, lds, &cb, cmap);
                 else dense_col<T, SHUF, BSWAP, MASKED, false, true, ZS>(a, c, j, base, mk, lds, &cb, cmap);
             } else if constexpr (MODE >= 4) {
-                if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H, true, ZS>(a, c, j, base, mk, lds, &cb, cmap, zm, zs0,
-                                                                               zpt, zord);
-                else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H, true, ZS>(a, c, j, base, mk, lds, &cb, cmap, zm, zs0,
-                                                                                zpt, zord);
+                if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H, true, ZS>(a, c, j, base, mk, lds, &cb, cmap, zm, zs0);
+                else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H, true, ZS>(a, c, j, base, mk, lds, &cb, cmap, zm, zs0);
             } else {
                 constexpr int UO = MODE == 2 ? 1 : 4;
                 if (al) dense_row<T, SHUF, BSWAP, MASKED, true, UO, true>(a, c, j, base, mk, &cb, cmap);
@@ -3106,10 +3072,8 @@ __device__ __forceinline__ void axes_dense_body(const AxesArgs &a) {
             row_zs_masks(a.t, (int)a.d.RI, zm);
             __syncthreads();
         }
-        if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H, false, ZS>(a, c, j, base, mk, lds, nullptr, nullptr, zm, 0,
-                                                                           zpt, zord);
-        else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H, false, ZS>(a, c, j, base, mk, lds, nullptr, nullptr, zm, 0,
-                                                                            zpt, zord);
+        if (al) dense_row_lds<T, SHUF, BSWAP, MASKED, true, H, false, ZS>(a, c, j, base, mk, lds, nullptr, nullptr, zm);
+        else dense_row_lds<T, SHUF, BSWAP, MASKED, false, H, false, ZS>(a, c, j, base, mk, lds, nullptr, nullptr, zm);
     } else if constexpr (MODE == 2) {
         if (al) dense_row<T, SHUF, BSWAP, MASKED, true, 1>(a, c, j, base, mk);
         else dense_row<T, SHUF, BSWAP, MASKED, false, 1>(a, c, j, base, mk);
@@ -5183,7 +5147,10 @@ hipError_t launch_combine_grid_t(const pyas_partial *in, const pyas_grid &g, con
         return hipGetLastError();
     }
     const dim3 grid((unsigned)((n_out + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL((k_combine_grid<T>), grid, blk, 0, st, in, g, ct, n_out, n_layers, flags, out);
+    // the keyed form only when level 2 is keyed: its keys cost the plain
+    // combine 49 -> 71 us on the C3 slab (2,) (profiles/r06/zeros2)
+    if (ct.on) hipLaunchKernelGGL((k_combine_grid<T, true>), grid, blk, 0, st, in, g, ct, n_out, n_layers, flags, out);
+    else hipLaunchKernelGGL((k_combine_grid<T, false>), grid, blk, 0, st, in, g, ct, n_out, n_layers, flags, out);
     return hipGetLastError();
 }
 
