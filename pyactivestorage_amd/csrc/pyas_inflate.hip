@@ -633,13 +633,14 @@ __device__ void flush(const uint8_t *win, Out &o, uint32_t n) {
         const uint32_t off = o.fpos + lane * 16;
         const uint4 v = *reinterpret_cast<const uint4 *>(&win[off & MASK]);
         *reinterpret_cast<uint4 *>(o.dst + off) = v;
-        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t byte = (w4[k >> 2] >> ((k & 3) * 8)) & 255u;
-            s += byte;
-            t += (n - (lane * 16 + k)) * byte;
-        }
+        // s = sum b_k, t = sum (n - 16 lane - k) b_k: byte dot products
+        s = __builtin_amdgcn_udot4(v.x, 0x01010101u, 0u, false) + __builtin_amdgcn_udot4(v.y, 0x01010101u, 0u, false) +
+            __builtin_amdgcn_udot4(v.z, 0x01010101u, 0u, false) + __builtin_amdgcn_udot4(v.w, 0x01010101u, 0u, false);
+        uint32_t kb = __builtin_amdgcn_udot4(v.x, 0x03020100u, 0u, false);
+        kb = __builtin_amdgcn_udot4(v.y, 0x07060504u, kb, false);
+        kb = __builtin_amdgcn_udot4(v.z, 0x0b0a0908u, kb, false);
+        kb = __builtin_amdgcn_udot4(v.w, 0x0f0e0d0cu, kb, false);
+        t = (n - (uint32_t)lane * 16u) * s - kb;
     } else {
         for (uint32_t i = lane; i < n; i += 64) {
             const uint32_t byte = win[(o.fpos + i) & MASK];
@@ -648,17 +649,14 @@ __device__ void flush(const uint8_t *win, Out &o, uint32_t n) {
             t += (n - i) * byte;
         }
     }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        s += (uint32_t)__shfl_xor((int)s, m, 64);
-        t += (uint32_t)__shfl_xor((int)t, m, 64);
-    }
-    s = uni(s);
-    t = uni(t);
+    // wave sums in DPP (shfl_xor steps are LDS round trips: ~1k cycles a
+    // flush); n <= 1024 keeps every sum below 2^32 (t <= 1024^2 * 255 / 2)
+    s = rl(wave_incl_sum(s), 63);
+    t = rl(wave_incl_sum(t), 63);
     // a' = a + sum b_i;  b' = b + n*a + sum (n - i) b_i   (mod 65521)
-    const uint64_t bb = (uint64_t)o.b + (uint64_t)n * o.a + t;
+    const uint32_t bb = o.b + n * o.a + t;
     o.a = (o.a + s) % 65521u;
-    o.b = (uint32_t)(bb % 65521u);
+    o.b = bb % 65521u;
     o.fpos += n;
 }
 
@@ -769,11 +767,26 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
             const uint32_t slen = rl(d, 0);
             const uint32_t byte0 = Q.w[(cons + 1) & (kQ - 1)];
             const uint32_t mine = (uint32_t)lane * 16u;
-            // kStoredSteps steps' input loads in flight at once (one HBM
-            // round trip per 1 KiB step cost the writer 1.7M cycles per
-            // 1 MiB stream, profiles/r06/inflate)
+            uint32_t dn = 0;
+            // head: single bytes up to a dword boundary of the output
+            const uint32_t head = min((4u - (o.pos & 3u)) & 3u, slen);
+            if (head) {
+                while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
+                if ((uint32_t)lane < head) {
+                    const uint32_t b = byte0 + (uint32_t)lane;
+                    const uint32_t v = __builtin_nontemporal_load(inw + (b >> 2));
+                    win[(o.pos + (uint32_t)lane) & kWinMask] = (uint8_t)(v >> (8 * (b & 3u)));
+                }
+                o.pos += head;
+                dn = head;
+                wave_lds_sync();
+            }
+            // then 16 bytes per lane per 1 KiB step as four dword writes (the
+            // output is dword-aligned; a last partial dword writes ring bytes
+            // past o.pos that nothing reads before the next tokens write them),
+            // kStoredSteps steps' input loads in flight at once
             constexpr uint32_t kStoredSteps = 4;
-            for (uint32_t dn = 0; dn < slen;) {
+            while (dn < slen) {
                 const uint32_t span = min(slen - dn, kStoredSteps * kFlush);
                 uint32_t dw[kStoredSteps][5];
 #pragma unroll
@@ -785,22 +798,17 @@ __device__ void writer(const InflateArgs &x, int64_t c, uint8_t *win, Queue &Q) 
                     for (uint32_t k = 0; k < 5; ++k)
                         dw[s][k] = on && wi + k < in_words ? __builtin_nontemporal_load(inw + wi + k) : 0u;
                 }
-                const uint32_t sh = (byte0 + dn + mine) & 3u;   // the same for every step (steps of 1 KiB)
+                const uint32_t sh = (byte0 + dn) & 3u;   // the same for every lane and step
 #pragma unroll
                 for (uint32_t s = 0; s < kStoredSteps; ++s) {
                     if (s * kFlush >= span) break;
                     while (o.pos - o.fpos >= kFlush) flush<kWinMask>(win, o, kFlush);
                     const uint32_t step = min(span - s * kFlush, kFlush);
-                    if (mine < step) {
-                        const uint32_t n = min(step - mine, 16u);
 #pragma unroll
-                        for (uint32_t k = 0; k < 4; ++k) {
-                            const uint32_t qv = __builtin_amdgcn_alignbyte(dw[s][k + 1], dw[s][k], sh);
-#pragma unroll
-                            for (uint32_t m = 0; m < 4; ++m)
-                                if (k * 4 + m < n) win[(o.pos + mine + k * 4 + m) & kWinMask] = (uint8_t)(qv >> (8 * m));
-                        }
-                    }
+                    for (uint32_t k = 0; k < 4; ++k)
+                        if (mine + 4u * k < step)
+                            win32[(((o.pos + mine) >> 2) + k) & (kWin / 4 - 1)] =
+                                __builtin_amdgcn_alignbyte(dw[s][k + 1], dw[s][k], sh);
                     o.pos += step;
                     wave_lds_sync();
                 }
