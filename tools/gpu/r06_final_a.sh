@@ -15,3 +15,11 @@ timeout -k 10 300 python -u tools/bench_inflate.py --sweep 1,30,256 > $O/inflate
 PYAS_INFLATE_NG=2 timeout -k 10 300 python -u tools/bench_inflate.py --sweep 1,256 > $O/inflate_bench_ng2.json 2> $O/inflate_bench_ng2.err || exit 1
 PYAS_LIB=$R/pyactivestorage_amd/lib/prof/libpyas_prof.so timeout -k 10 300 python -u tools/bench_inflate.py --chunks 4 --reps 1 > $O/inflate_phase.txt 2>&1 || exit 1
 timeout -k 10 600 python -u tools/bench_inflate_crossover.py --reps 5 > $O/inflate_crossover.json 2> $O/inflate_crossover.err || exit 1
+# zero sign on the slab's full reduction against mean (same variable)
+cd /tmp
+for m in mean min; do
+  for z in 0.02 0.5; do
+    q=0; [ $m = min ] && q=1
+    timeout -k 10 240 python3 $R/tools/query_c3.py c3_slab $q --method $m --zeros $z --reps 10 > $R/$O/zs_c3_slab_full_${m}_z$z.json 2> $R/$O/zs_c3_slab_full_${m}_z$z.err || exit 1
+  done
+done
