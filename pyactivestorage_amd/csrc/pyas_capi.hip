@@ -1464,6 +1464,8 @@ int pyas_combine_grid(pyas_ctx *ctx, int32_t dtype, const pyas_partial *in, cons
         }
     }
     if (!in || !out || !g->chunk_out_offsets) return fail(PYAS_EINVAL, "NULL argument");
+    if (ct.on && n_layers >= (int64_t(1) << 31))   // the keyed combine's 32-bit layer positions
+        return fail(PYAS_ENOTSUP, "zero sign: more than 2^31 chunk layers");
     PYAS_HIP(hipSetDevice(ctx->device));
     // PYAS_COMBINE_WAVE=0 (read per call: tests switch it) keeps the
     // per-thread fold for every layer count

@@ -500,10 +500,11 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
             for (int j = 0; j < NG; ++j) {
                 M[j] = 0ull;
                 if (!stopped) {
-                    while (off < 64u * (uint32_t)(j + 1)) {
-                        M[j] |= 1ull << (off - 64u * (uint32_t)j);
+                    const uint32_t gb = 64u * (uint32_t)j, ge = gb + 64u;
+                    while (off < ge) {
+                        M[j] |= 1ull << (off - gb);
                         prev = off;
-                        off = rl(nxt[j], off - 64u * (uint32_t)j);
+                        off = rl(nxt[j], off - gb);
                     }
                     stopped = off >= kStop;
                 }
@@ -967,7 +968,8 @@ __global__ __launch_bounds__(128) void k_inflate(InflateArgs x) {
     else writer<WBITS>(x, c, win, Q);
 }
 
-// PYAS_INFLATE_NG: bit-offset groups per decoder window (1, 2 or 4).  Read
+// PYAS_INFLATE_NG: bit-offset groups per decoder window (1, 2 or 4; 8 took
+// 150 VGPRs for the same 147 MB/s per stream, profiles/r06/inflate).  Read
 // once per process.
 static int inflate_ng() {
     static const int ng = [] {

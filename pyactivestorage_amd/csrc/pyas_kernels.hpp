@@ -1353,6 +1353,9 @@ __device__ __forceinline__ void tie_keys(int64_t e, uint64_t sg, const TieCall &
                                          uint64_t &k1, uint64_t &w, uint64_t &ka);
 __device__ __forceinline__ int tie_finalize(uint64_t k1, uint64_t w, uint64_t ka, const TieCall &c,
                                             const TieRule &t);
+__device__ __forceinline__ void tie_keys32(uint32_t e, uint64_t sg, const TieCall &c, const TieRule &t,
+                                           const uint8_t *rank, const uint8_t *arank, bool lanes, uint64_t &k1,
+                                           uint64_t &w, uint64_t &ka);
 
 // box-query combine (pyas_combine_grid): one thread per final output element,
 // chunk layers folded in C order of the reduced dims' coordinates
@@ -1361,6 +1364,23 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
                                                          int64_t n_out, int64_t n_layers,
                                                          uint32_t flags, pyas_partial *out) {
     const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    // KEY: the level-2 keys depend on the layer's position alone, so up to
+    // kKeyTab layers they are worked out once per workgroup (sign bit 0; a
+    // zero's sign is OR-ed in), not per output and zero layer
+    constexpr int kKeyTab = KEY ? 512 : 1;
+    __shared__ uint64_t ktab1[kKeyTab], ktabw[kKeyTab];
+    const bool ktab = KEY && n_layers <= kKeyTab;
+    if constexpr (KEY) {
+        if (ktab) {   // uniform over the workgroup
+            for (int e = (int)threadIdx.x; e < (int)n_layers; e += kBlock) {
+                uint64_t x1, xw, xa;
+                tie_keys32((uint32_t)e, 0u, ct.c, ct.t, ct.t.rank, ct.t.acc_rank, true, x1, xw, xa);
+                ktab1[e] = x1;
+                ktabw[e] = xw;
+            }
+            __syncthreads();
+        }
+    }
     if (f >= n_out) return;
     const bool round = (flags & PYAS_COMBINE_ROUND_TO_VAR) != 0;
     int64_t gstride[PYAS_MAX_DIMS];
@@ -1463,7 +1483,17 @@ __global__ __launch_bounds__(kBlock) void k_combine_grid(const pyas_partial *in,
                                 zneg = __builtin_signbit(v) != 0;
                                 if constexpr (KEY) {
                                     uint64_t x1, xw, xa;
-                                    tie_keys(l0 + u, zneg ? 1u : 0u, ct.c, ct.t, true, x1, xw, xa);
+                                    if (ktab) {
+                                        const uint64_t sg = zneg ? 1u : 0u;
+                                        x1 = ktab1[l0 + u];
+                                        x1 = x1 ? x1 | sg : 0u;
+                                        xw = ktabw[l0 + u] | sg;
+                                    } else {
+                                        // 32-bit keys (a layer's position is < 2^31): the
+                                        // 64-bit divisions of tie_keys cost the combine ~2x
+                                        tie_keys32((uint32_t)(l0 + u), zneg ? 1u : 0u, ct.c, ct.t, ct.t.rank,
+                                                   ct.t.acc_rank, true, x1, xw, xa);
+                                    }
                                     zk1 = x1 > zk1 ? x1 : zk1;
                                     zkw = xw < zkw ? xw : zkw;
                                 }
@@ -2790,7 +2820,8 @@ constexpr int kRowLdsStride = 17;   // 16-B vectors per LDS run (V <= 16, + 1 pa
 // the lowest lane-rank class holding one.  Its sign goes into the record.
 // Zero-free tiles cost one ballot.
 __device__ __forceinline__ int msb64(uint64_t v) { return 63 - __builtin_clzll(v); }   // v != 0
-constexpr int kRowZsWords = 4 + 64;   // rem, top, vec, box run, then the rank classes
+constexpr int kRowZsRank = 4 + 64;        // then each position's lane rank, one byte each (255: not a lane)
+constexpr int kRowZsWords = kRowZsRank + 8;   // rem, top, vec, box run, the rank classes, the ranks
 
 // The masks ZT reads (LDS, zm[kRowZsWords]) for a call of L positions e
 // (e = 0 the seed, then m = L - 1 elements: the first nv in t.lanes lanes, the
@@ -2807,6 +2838,7 @@ __device__ __forceinline__ void row_zs_masks(const TieRule &t, int L, uint64_t *
         const uint64_t cm = __ballot(rk == k);
         if (e == 0) zm[4 + k] = cm;
     }
+    reinterpret_cast<uint8_t *>(zm + kRowZsRank)[e] = vec ? (uint8_t)rk : (uint8_t)255;
     if (e == 0) {
         zm[0] = rem;
         zm[1] = top;
@@ -2816,21 +2848,40 @@ __device__ __forceinline__ void row_zs_masks(const TieRule &t, int L, uint64_t *
 }
 
 // The winning zero of a row call (box positions Z, bit e = position e).
-// (Round 6 measured a table pick of the lowest rank -- two LDS lookups
-// from the lane-class set -- slower than this search: 1.40 vs 1.20-1.32 ms
-// on the C3 slab (2,), profiles/r06/zeros2.)
+// A few lane zeros: their ranks from the per-position byte table, the loads
+// independent (at 2 % zeros a zero row holds one or two, and the class
+// search below waited on one LDS mask per class until the zero's class);
+// more: the class search, which then stops early.  (Round 6 measured a
+// table pick from lane-class sets -- two LDS lookups -- slower than the
+// search: 1.40 vs 1.20-1.32 ms on the C3 slab (2,), profiles/r06/zeros.)
 __device__ __forceinline__ int row_zs_pick(uint64_t Z, const uint64_t *zm, int lanes) {
     const uint64_t zr = Z & zm[0];
     if (zr) return msb64(zr);
     const uint64_t sig = Z & (zm[1] | 1u);
     const int e1 = sig ? msb64(sig) : -1;
     int ew = -1;
-    if (!(Z & 1u) && (Z & zm[2])) {
-        for (int k = 0; k < lanes; ++k) {
-            const uint64_t cz = Z & zm[4 + k];
-            if (cz) {
-                ew = msb64(cz);
-                break;
+    const uint64_t Zv = Z & zm[2];   // the zeros in the lanes
+    if (!(Z & 1u) && Zv) {
+        if (__builtin_popcountll(Zv) <= 8) {
+            // latest first, strictly lower rank replaces: the last zero of the lowest rank
+            const uint8_t *zr = reinterpret_cast<const uint8_t *>(zm + kRowZsRank);
+            uint32_t best = 256u;
+            for (uint64_t b = Zv; b;) {
+                const int e = msb64(b);
+                b &= ~(1ull << e);
+                const uint32_t r = zr[e];
+                if (r < best) {
+                    best = r;
+                    ew = e;
+                }
+            }
+        } else {
+            for (int k = 0; k < lanes; ++k) {
+                const uint64_t cz = Z & zm[4 + k];
+                if (cz) {
+                    ew = msb64(cz);
+                    break;
+                }
             }
         }
     }
