@@ -516,42 +516,52 @@ __device__ void decoder(const InflateArgs &x, int64_t c, Lds &L, uint32_t *in_ri
                 off = prev;
             }
             PYAS_PROF(1);
-            // output offsets along the chain: two groups per 32-bit prefix sum
-            uint32_t excl[NG], tot = 0;
+            // the window's output: past the first 32 KiB no distance reaches
+            // before the output start, and a window whose whole output fits
+            // the capacity has no token past it -- then one wave sum is all
+            // the window needs (the writer takes offsets as its own prefix sum)
+            uint32_t lsum = 0;
 #pragma unroll
-            for (int j = 0; j < NG; j += 2) {
-                const uint32_t va = ((M[j] >> lane) & 1ull) ? olen[j] : 0u;
-                uint32_t vb = 0;
-                if (j + 1 < NG) vb = ((M[j + 1] >> lane) & 1ull) ? olen[j + 1] : 0u;
-                const uint32_t inc = wave_incl_sum(va | (vb << 16));
-                const uint32_t tt = rl(inc, 63);
-                excl[j] = tot + (inc & 0xffffu) - va;
-                tot += tt & 0xffffu;
-                if (j + 1 < NG) {
-                    excl[j + 1] = tot + (inc >> 16) - vb;
-                    tot += tt >> 16;
+            for (int j = 0; j < NG; ++j) lsum += ((M[j] >> lane) & 1ull) ? olen[j] : 0u;
+            uint32_t T = rl(wave_incl_sum(lsum), 63), cut = kStop;
+            if (q < 32768u || q + T > cap) {
+                // output offsets along the chain: two groups per 32-bit prefix sum
+                uint32_t excl[NG], tot = 0;
+#pragma unroll
+                for (int j = 0; j < NG; j += 2) {
+                    const uint32_t va = ((M[j] >> lane) & 1ull) ? olen[j] : 0u;
+                    uint32_t vb = 0;
+                    if (j + 1 < NG) vb = ((M[j + 1] >> lane) & 1ull) ? olen[j + 1] : 0u;
+                    const uint32_t inc = wave_incl_sum(va | (vb << 16));
+                    const uint32_t tt = rl(inc, 63);
+                    excl[j] = tot + (inc & 0xffffu) - va;
+                    tot += tt & 0xffffu;
+                    if (j + 1 < NG) {
+                        excl[j + 1] = tot + (inc >> 16) - vb;
+                        tot += tt >> 16;
+                    }
                 }
-            }
-            // the first chain symbol reaching before the output start or past
-            // the capacity ends the chain (the serial decoder reports it)
-            uint32_t cut = kStop, T = tot;
-            bool bad_any = false;
-#pragma unroll
-            for (int j = 0; j < NG; ++j) {
-                const uint32_t a = q + excl[j];
-                bad_any = bad_any || (((M[j] >> lane) & 1ull) &&
-                                      (a + olen[j] > cap || (olen[j] > 1u && (tw[j] & 0xffffu) > a)));
-            }
-            if (__ballot(bad_any)) {   // rare: find the first such symbol in chain order
+                // the first chain symbol reaching before the output start or past
+                // the capacity ends the chain (the serial decoder reports it)
+                T = tot;
+                bool bad_any = false;
 #pragma unroll
                 for (int j = 0; j < NG; ++j) {
-                    const bool on = (M[j] >> lane) & 1ull;
                     const uint32_t a = q + excl[j];
-                    const uint64_t b = __ballot(on && (a + olen[j] > cap || (olen[j] > 1u && (tw[j] & 0xffffu) > a)));
-                    if (b && cut == kStop) {
-                        const uint32_t cc = (uint32_t)__builtin_ctzll(b);
-                        cut = 64u * (uint32_t)j + cc;
-                        T = rl(excl[j], cc);
+                    bad_any = bad_any || (((M[j] >> lane) & 1ull) &&
+                                          (a + olen[j] > cap || (olen[j] > 1u && (tw[j] & 0xffffu) > a)));
+                }
+                if (__ballot(bad_any)) {   // rare: find the first such symbol in chain order
+#pragma unroll
+                    for (int j = 0; j < NG; ++j) {
+                        const bool on = (M[j] >> lane) & 1ull;
+                        const uint32_t a = q + excl[j];
+                        const uint64_t b = __ballot(on && (a + olen[j] > cap || (olen[j] > 1u && (tw[j] & 0xffffu) > a)));
+                        if (b && cut == kStop) {
+                            const uint32_t cc = (uint32_t)__builtin_ctzll(b);
+                            cut = 64u * (uint32_t)j + cc;
+                            T = rl(excl[j], cc);
+                        }
                     }
                 }
             }
