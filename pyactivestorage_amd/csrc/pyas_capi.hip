@@ -988,6 +988,10 @@ int pyas_reduce_axes_ex(pyas_ctx *ctx, const pyas_batch *batch, const pyas_mask 
     if (rec != PYAS_REC_FULL && red_elems >= (int64_t(1) << 31))
         return fail(PYAS_ENOTSUP, "records count in int32: 2^31 or more reduced elements per output");
     x.rec = rec;
+    // k_reduce_axes' LDS offset map: one entry per reduced position of a
+    // whole chunk (a selection never reduces more; one that does, e.g. a
+    // repeated index list, takes the radix walk)
+    x.roff_cap = red_elems <= pyas::kAxesLds ? (int32_t)red_elems : 0;
     x.row = ((axes_mask >> (batch->ndim - 1)) & 1u) != 0;
     // 16-B vector walks: >= 4-byte unshuffled elements, no index tables, the
     // reduced offsets fit the LDS map and the last dim is whole 16-B vectors.

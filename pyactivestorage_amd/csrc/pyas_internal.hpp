@@ -85,6 +85,7 @@ struct AxesArgs {
     bool cuts;                        // dense launch also takes cut chunks (box, >= half the chunk)
     int32_t zs;                       // the walk keys NumPy's sign of a zero min (1) / max (2)
     TieRule t;                        // zs in the LDS row layout: the host's rule (rows are calls)
+    int32_t roff_cap;                 // k_reduce_axes: entries of its LDS offset map (dynamic LDS, <= kAxesLds)
 };
 
 // pyas_reduce_axes_grid: the chunk layers of a whole-chunk box query folded

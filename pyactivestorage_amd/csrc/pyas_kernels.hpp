@@ -1798,7 +1798,7 @@ __device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_
     const ReduceArgs &r = a.r;
     constexpr int ES = sizeof(T), N = 16 / ES;
     const bool tabs = r.tab.on[0] || r.tab.on[1];
-    const bool use_lds = !tabs && n_red <= kAxesLds;
+    const bool use_lds = !tabs && n_red <= a.roff_cap;   // roff holds a.roff_cap entries
     // 16-B vector modes: the last chunk dim is a unit-step, 16-B aligned run
     const int last = r.ndim - 1;
     int64_t cnt_last = 1, start_last = 0, step_last = 1, shape_last = 1;
@@ -1823,7 +1823,17 @@ __device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_
         __syncthreads();
     }
     if (!a.row) {
-        const int S = a.split, OT = kBlock / S;
+        int S = a.split;
+        // 16-B column walks: the host sized the split for the chunk's whole
+        // kept extent; a chunk whose selection keeps fewer vectors (a strided
+        // kept dim: [:, ::3, :] over (0,) keeps a third) splits its reduced
+        // rows over the lanes that would otherwise idle (block-uniform: per
+        // chunk), keeping >= 8 rows per lane
+        if (col_vec) {
+            const int64_t nvec = n_out / N;
+            while (S * 2 <= kBlock && nvec * S * 2 <= a.bpc * kBlock && n_red / (S * 2) >= 8) S *= 2;
+        }
+        const int OT = kBlock / S;
         const int ol = threadIdx.x % OT, sp = threadIdx.x / OT;
         const int64_t n_items = col_vec ? n_out / N : n_out;   // outputs or N-output vectors
         const uint64_t m = col_vec ? N : 1;
@@ -1839,8 +1849,11 @@ __device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_
 #pragma unroll
                 for (int k = 0; k < N; ++k) acc[k].init();
                 if (oi < n_items) {
+                    // U rows in flight per lane; output k's U values summed
+                    // in groups of 4 (widened once per group, as the dense
+                    // column walk), one NaN ballot per U rows
                     const uint8_t *bo = base + base_o.mem * ES;
-                    constexpr int U = 4;
+                    constexpr int U = 8;
                     int64_t q = sp;
                     const int64_t nfull = sp + ((n_red - sp + S - 1) / S) / U * U * S;
                     for (; q < nfull; q += U * S) {
@@ -1848,12 +1861,20 @@ __device__ void axes_block(const AxesArgs &a, int64_t c, int64_t j, const uint8_
 #pragma unroll
                         for (int u = 0; u < U; ++u)
                             v[u] = ldg16(reinterpret_cast<const uint4 *>(bo + (int64_t)roff[q + u * S] * ES));
+                        T xs[N][U];
 #pragma unroll
                         for (int u = 0; u < U; ++u) {
                             T x[N];
                             unpack16<T, BSWAP>(v[u], x);
 #pragma unroll
-                            for (int k = 0; k < N; ++k) acc[k].add_one(x[k], mk.masked(x[k]));
+                            for (int k = 0; k < N; ++k) xs[k][u] = x[k];
+                        }
+                        bool bad = false;
+#pragma unroll
+                        for (int k = 0; k < N; ++k) bad |= acc[k].template add_lazy<U, kMaskAll, false>(xs[k], mk);
+                        if (__builtin_expect(__ballot(bad) != 0, 0)) {
+#pragma unroll
+                            for (int k = 0; k < N; ++k) acc[k].template check_nan<U>(xs[k]);
                         }
                     }
                     for (; q < n_red; q += S) {
@@ -4253,7 +4274,9 @@ __global__ __launch_bounds__(kBlock) PYAS_XATTR(PYAS_FOLD_ROW_WAVES) void k_axes
 
 template <typename T, bool SHUF, bool BSWAP>
 __global__ __launch_bounds__(kBlock) void k_reduce_axes(AxesArgs a) {
-    __shared__ int32_t roff[kAxesLds];
+    // the reduced-offset map, sized by the host to the chunk's reduced extent
+    // (a.roff_cap entries): a fixed 32 KiB array held 4 workgroups per CU
+    extern __shared__ int32_t roff[];
     const int64_t c = blockIdx.x / a.bpc;
     const int64_t j = blockIdx.x - c * a.bpc;
     const ReduceArgs &r = a.r;
@@ -5434,13 +5457,17 @@ hipError_t launch_axes_fold_rows_t(const AxesArgs &a, const FoldGrid &g, bool ma
 template <typename T>
 hipError_t launch_axes_t(const AxesArgs &a, int64_t grid, hipStream_t st) {
     const dim3 g((unsigned)grid), blk(kBlock);
+    const int cap = a.roff_cap < 0 ? 0 : (a.roff_cap > kAxesLds ? kAxesLds : a.roff_cap);
+    AxesArgs b = a;
+    b.roff_cap = cap;
+    const size_t lds = (size_t)(cap > 0 ? cap : 1) * sizeof(int32_t);
     if constexpr (sizeof(T) == 1) {
-        hipLaunchKernelGGL((k_reduce_axes<T, false, false>), g, blk, 0, st, a);
+        hipLaunchKernelGGL((k_reduce_axes<T, false, false>), g, blk, lds, st, b);
     } else {
-        if (a.shuf && a.bswap) hipLaunchKernelGGL((k_reduce_axes<T, true, true>), g, blk, 0, st, a);
-        else if (a.shuf) hipLaunchKernelGGL((k_reduce_axes<T, true, false>), g, blk, 0, st, a);
-        else if (a.bswap) hipLaunchKernelGGL((k_reduce_axes<T, false, true>), g, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_reduce_axes<T, false, false>), g, blk, 0, st, a);
+        if (a.shuf && a.bswap) hipLaunchKernelGGL((k_reduce_axes<T, true, true>), g, blk, lds, st, b);
+        else if (a.shuf) hipLaunchKernelGGL((k_reduce_axes<T, true, false>), g, blk, lds, st, b);
+        else if (a.bswap) hipLaunchKernelGGL((k_reduce_axes<T, false, true>), g, blk, lds, st, b);
+        else hipLaunchKernelGGL((k_reduce_axes<T, false, false>), g, blk, lds, st, b);
     }
     return hipGetLastError();
 }
